@@ -1,0 +1,194 @@
+#!/usr/bin/env python3
+"""Headline benchmark: exact k-NN QPS@k=10 on the Cohere-shaped corpus (BASELINE.json config C3).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+  (N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N)
+
+Workload (config C3): 10,000,000 × 768 fp32 vectors, COSINE, 8 index shards of
+1,250,000 docs (shard s = global rows [s·1.25M, (s+1)·1.25M) as local docs 0…1.25M−1, one segment
+each), k = 10, from = 0, size = 10.  Synthetic data generated on the device by libosknn's counter
+generator (Irwin–Hall(4) ≈ N(0,1), rows L2-normalised; queries from seed 43).  Shard s lives on
+rank s·N/8, so the total corpus is fixed and each GPU scans 10M/N rows ("strong" scaling).
+
+One step = one batch of B queries (default 1: the single-query path the north star targets) through
+the whole hot path with inputs resident in HBM: per-shard exact scan + top-k on every GPU, per-shard
+merge, RCCL all-gather of the per-shard top-k lists, device coordinator merge (TopDocs.merge).
+value = queries answered by the whole job per second.
+
+roofline: the scan kernel (scan_f32<16,12,…>) is HBM-bound; algorithmic bytes per launch =
+rows scanned × 768 × 4 B (each corpus byte read once per launch of ≤ 8 queries).  Its average
+duration is measured live with HIP events on the launch stream (osk_view_profile).
+cpu_baseline: rank 0 at N = 1 only — the oracle's Lucene-equivalent restatement (Panama-512 order,
+not Lucene: no JDK/jar on the box) on a bounded sample, scaled to the full corpus by rows.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from opensearch_amd import _lib  # noqa: E402
+from opensearch_amd import distributed as D  # noqa: E402
+from opensearch_amd.lucene import synth_host  # noqa: E402
+
+N_SHARDS = 8
+ROWS_PER_SHARD = 1_250_000
+DIM = 768
+K = 10
+FROM, SIZE = 0, 10
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md; 6.29 TB/s measured float4 copy)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(sample_rows: int, n_queries: int, threads: int) -> dict:
+    from oracle import oracle as O
+    t0 = time.perf_counter()
+    rows = O.synth(0, sample_rows, DIM, 42, 3)
+    qs = O.synth(0, n_queries, DIM, 43, 3)
+    log(f"cpu_baseline: generated {sample_rows}x{DIM} in {time.perf_counter() - t0:.1f}s")
+    O.knn_batch(rows, qs[:2], K, 2, O.ORDER_PANAMA512, threads)   # warm-up
+    t0 = time.perf_counter()
+    O.knn_batch(rows, qs, K, 2, O.ORDER_PANAMA512, threads)
+    dt = time.perf_counter() - t0
+    qps_sample = n_queries / dt
+    total_rows = N_SHARDS * ROWS_PER_SHARD
+    return {
+        "value": qps_sample * sample_rows / total_rows,
+        "unit": "queries/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"{n_queries} queries × {sample_rows} rows × {DIM} fp32 COSINE k={K} in {dt:.2f}s "
+                   f"({qps_sample:.1f} QPS on the sample), scaled ×{sample_rows}/{total_rows} to the 10M corpus; "
+                   f"Lucene-equivalent restatement (Panama-512 summation order), not Lucene"),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--rows-per-shard", type=int, default=ROWS_PER_SHARD)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-rows", type=int, default=262_144)
+    ap.add_argument("--cpu-queries", type=int, default=32)
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    t0 = time.perf_counter()
+    shards = D.LocalShards(rank, world, N_SHARDS, a.rows_per_shard, DIM, _lib.COSINE, _lib.FLOAT32, 42,
+                           _lib.DIST_NORMALISH_UNIT, local_rank)
+    torch.cuda.synchronize()
+    rows_local = len(shards.shards) * a.rows_per_shard
+    log(f"rank {rank}: staged shards {shards.shards} ({rows_local} rows) in {time.perf_counter() - t0:.1f}s")
+
+    n_pool = 64
+    qpool = torch.from_numpy(synth_host(0, n_pool * a.batch, DIM, 43, _lib.DIST_NORMALISH_UNIT)).cuda()
+    B = a.batch
+    keys = torch.empty((B, shards.s_pad, K), dtype=torch.int64, device="cuda")
+    counts = torch.empty((B, shards.s_pad), dtype=torch.int32, device="cuda")
+    gsi = shards.global_shard_index.cuda()
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step(i):
+        q = qpool[(i % n_pool) * B:(i % n_pool + 1) * B]
+        shards.search(q.data_ptr(), B, K, keys, counts, stream)
+        gk, gc = D.gather_shard_topk(keys, counts, world)
+        return D.merge_gathered(gk, gc, gsi, K, FROM, SIZE, local_rank, stream)
+
+    for i in range(a.warmup):
+        out = step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    _lib.check(_lib.lib().osk_view_profile(shards.view, 1))
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t_start = time.perf_counter()
+    ev0.record()
+    for i in range(a.steps):
+        out = step(a.warmup + i)
+        if (i + 1) % 200 == 0:
+            log(f"rank {rank}: step {i + 1}/{a.steps}")
+    ev1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    scan_ms, calls = C.c_double(), C.c_int64()
+    _lib.check(_lib.lib().osk_view_scan_time(shards.view, C.byref(scan_ms), C.byref(calls)))
+    _lib.check(_lib.lib().osk_view_profile(shards.view, 0))
+    ev_ms = ev0.elapsed_time(ev1)
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed_max = float(t.item())
+
+    # sanity on the last step: every query got `SIZE` hits from the 10M corpus
+    cnt = out[3].cpu().numpy()
+    assert np.all(cnt == SIZE), cnt
+
+    scan_avg_ms = scan_ms.value / max(1, calls.value)
+    passes = (B + 7) // 8
+    bytes_per_launch = rows_local * DIM * 4 * passes
+    achieved = bytes_per_launch / (scan_avg_ms * 1e-3) / 1e9
+
+    if rank == 0:
+        res = {
+            "metric": "exact k-NN QPS@k=10 (recall=1.0), 10M×768 fp32, 1/2/4/8 GPUs; % HBM roofline",
+            "value": a.steps * B / elapsed_max,
+            "unit": "queries/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed_max / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (device counter generator: Irwin-Hall(4)≈N(0,1), rows L2-normalised; seed 42/43)",
+            "config": {"workload": "C3 Cohere-shaped exact k-NN: 10M×768 fp32 COSINE, 8 shards, k=10, from=0, size=10",
+                       "batch": B, "rows": N_SHARDS * a.rows_per_shard, "dim": DIM, "shards": N_SHARDS,
+                       "parallelism": f"shards over {world} GPU(s), RCCL all-gather + device merge"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "scan_f32<L=16,V=12,NQ=1,dot> (+shard merge excluded)",
+                         "scan_ms_avg": scan_avg_ms, "algorithmic_bytes_per_launch": bytes_per_launch},
+            "gpu_event_ms_per_step": ev_ms / a.steps,
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            threads = min(16, os.cpu_count() or 1)
+            res["cpu_baseline"] = cpu_baseline(a.cpu_sample_rows, a.cpu_queries, threads)
+        print(json.dumps(res), flush=True)
+    shards.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,194 @@
+/*
+ * osknn.h — C-ABI of libosknn.so, the MI355X-native exact k-NN scoring path for OpenSearch.
+ *
+ * This is the drop-in boundary. Every entry point is `extern "C"`, takes plain pointers and
+ * sizes, never throws, never aborts, and is safe to call from many threads at once (OpenSearch's
+ * `search` and `index_searcher` pools, S/threadpool/ThreadPool.java:106,126). Errors are returned
+ * as negative codes; the message of the last error on the calling thread is `osk_last_error()`.
+ * A Java caller maps a negative code to an IOException, which OpenSearch turns into a shard
+ * failure (S/search/query/QueryPhase.java:307-309) — the library never brings the node down.
+ *
+ * Citation convention: `S/` = /root/reference/server/src/main/java/org/opensearch/ ;
+ * [L] = behaviour of the un-vendored lucene-core 10.3.0 jar (gradle/libs.versions.toml:3) whose
+ * interface is evidenced by the reference call site given next to it.
+ *
+ * What each entry point replaces in the reference stack:
+ *
+ *   osk_seg_stage / osk_seg_stage_device / osk_seg_synth
+ *       [L] KnnVectorsFormat.fieldsReader(SegmentReadState) → the reader's constructor / warm step:
+ *       one segment's flat vector values (.vec, row-major little-endian) staged ONCE into HBM.
+ *       Segment open: S/index/engine/InternalEngine.java:584-589; warmers
+ *       S/index/engine/InternalEngine.java:2409-2432; codec choice S/index/codec/CodecService.java:70-99.
+ *   osk_seg_release
+ *       [L] KnnVectorsReader.close() — when the segment is merged away / its refcount drops to 0.
+ *   osk_seg_search
+ *       [L] KnnVectorsReader.search(String field, float[]|byte[] target, KnnCollector, AcceptDocs)
+ *       reached through LeafReader.searchNearestVectors (4-arg 10.3 signature evidenced at
+ *       S/index/engine/TranslogLeafReader.java:379-386). Exact (brute-force) top-k over the
+ *       segment with Lucene's exact-search semantics: score desc, ties → lower doc.
+ *   osk_view_create / osk_view_search / osk_view_search_device
+ *       A shard's leaves (and several shards on one GPU): the per-leaf exact search that
+ *       [L] AbstractKnnVectorQuery.rewrite runs for every leaf from
+ *       S/search/internal/ContextIndexSearcher.java:203-218, the per-leaf TopDocs.merge(k, …)
+ *       into the shard's top-k, and the shard collector's cut to from+size
+ *       (S/search/query/TopDocsCollectorContext.java:866-891).
+ *   osk_merge_device / osk_topdocs_merge
+ *       The coordinator's reduce: S/action/search/SearchPhaseController.java:224-246 (mergeTopDocs →
+ *       [L] TopDocs.merge(from, size, shardHits): score desc, then shardIndex asc, then doc asc),
+ *       :248-253 (setShardIndex) and TopDocsStats (:839-901: Σ totalHits, max maxScore).
+ *       osk_merge_device runs on the GPU after the RCCL all-gather of per-shard top-k lists;
+ *       osk_topdocs_merge is the same reduce over host arrays (no device needed).
+ */
+#ifndef OSKNN_H
+#define OSKNN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OSK_ABI_VERSION 1
+#define OSK_MAX_K       64   /* largest k (and from+size) the device path serves in this build */
+#define OSK_MAX_DIM     4096
+
+/* ---- return codes ---- */
+#define OSK_OK               0
+#define OSK_ERR_INVALID     -1   /* bad argument (null pointer, k <= 0, dim mismatch, ...) */
+#define OSK_ERR_DEVICE      -2   /* a HIP runtime call failed */
+#define OSK_ERR_OOM         -3   /* device or host allocation failed */
+#define OSK_ERR_UNSUPPORTED -4   /* valid request this build does not implement */
+#define OSK_ERR_NO_DEVICE   -5   /* no usable gfx950 device */
+
+/* ---- [L] VectorEncoding ---- */
+#define OSK_FLOAT32 0
+#define OSK_BYTE    1
+
+/* ---- [L] VectorSimilarityFunction (ordinal order of the Lucene enum) ---- */
+#define OSK_EUCLIDEAN             0
+#define OSK_DOT_PRODUCT           1
+#define OSK_COSINE                2
+#define OSK_MAXIMUM_INNER_PRODUCT 3
+
+/* ---- synthetic corpus distributions (bench / tests) ---- */
+#define OSK_DIST_UNIFORM01      0   /* U[0,1)                         (C1)            */
+#define OSK_DIST_UNIFORM01_X128 1   /* U[0,1)·128, SIFT-like          (C2)            */
+#define OSK_DIST_NORMALISH      2   /* Irwin–Hall(4) ≈ N(0,1)                          */
+#define OSK_DIST_NORMALISH_UNIT 3   /* Irwin–Hall(4), each row L2-normalised (C3, C4)  */
+#define OSK_DIST_INT8           4   /* U{-128..127} bytes             (C5 int8)        */
+
+typedef struct osk_seg  osk_seg;   /* one segment's vector field, resident in HBM */
+typedef struct osk_view osk_view;  /* the segments of one or more shards on ONE device */
+
+int32_t     osk_abi_version(void);
+/* Message of the last failed call on this thread ("" if none). Valid until the next call. */
+const char* osk_last_error(void);
+int32_t     osk_device_count(int32_t* n);
+
+/* Stage one segment into HBM on `device`.
+ *   rows        host, n_rows × dim elements row-major (f32 or int8 per `encoding`), ord order
+ *   ord_to_doc  NULL = dense (doc == ord), else n_rows ascending segment-local docIDs
+ *   max_doc     the leaf's maxDoc (bounds the accept bitset); must be ≥ the largest doc + 1
+ * The rows are copied; the caller's buffer may be freed on return. */
+int32_t osk_seg_stage(int32_t device, const void* rows, int64_t n_rows, int32_t dim,
+                      int32_t encoding, int32_t similarity, const int32_t* ord_to_doc,
+                      int32_t max_doc, osk_seg** out);
+/* Same, from rows already on `device` (row pitch `src_pitch_bytes`); ord_to_doc is host memory. */
+int32_t osk_seg_stage_device(int32_t device, const void* d_rows, int64_t src_pitch_bytes,
+                             int64_t n_rows, int32_t dim, int32_t encoding, int32_t similarity,
+                             const int32_t* ord_to_doc, int32_t max_doc, osk_seg** out);
+/* A synthetic dense segment generated on the device: row r of the segment is global row
+ * row0 + r of the counter-based generator (seed, dist). osk_synth_host() yields identical values. */
+int32_t osk_seg_synth(int32_t device, int64_t n_rows, int32_t dim, int32_t encoding,
+                      int32_t similarity, uint64_t seed, int32_t dist, int64_t row0,
+                      osk_seg** out);
+int32_t osk_seg_release(osk_seg* seg);
+int32_t osk_seg_info(const osk_seg* seg, int64_t* n_rows, int32_t* dim, int32_t* encoding,
+                     int32_t* similarity, int32_t* max_doc, int32_t* device);
+
+/* Host generator behind osk_seg_synth (f32 out for dists 0-3, int8 out for dist 4). */
+int32_t osk_synth_host(void* out, int64_t row0, int64_t n_rows, int32_t dim, uint64_t seed,
+                       int32_t dist);
+
+/* [L] KnnVectorsReader.search — exact top-k of one segment, host buffers, synchronous.
+ *   queries      n_queries × dim (f32 or int8, the segment's encoding)
+ *   accept_bits  NULL = all docs; else ceil(max_doc/64) words, LSB-first, bit d = doc d accepted
+ *                (Lucene AcceptDocs = liveDocs ∩ filter)
+ *   out_scores/out_docs  n_queries × k, per query score desc then doc asc; slots past
+ *                out_count[q] are score = -inf, doc = INT32_MAX
+ *   out_visited  (optional) number of vectors scored = KnnCollector.visitedCount()
+ * 1 ≤ k ≤ OSK_MAX_K. */
+int32_t osk_seg_search(osk_seg* seg, const void* queries, int32_t n_queries, int32_t k,
+                       const uint64_t* accept_bits, float* out_scores, int32_t* out_docs,
+                       int32_t* out_count, int64_t* out_visited);
+
+/* Group segments into shards on one device.
+ *   seg_shard[i]     which shard (0 … n_shards-1) segment i belongs to
+ *   seg_doc_base[i]  the leaf's docBase inside its shard (LeafReaderContext.docBase)
+ *   shard_index[s]   the coordinator's shardIndex of shard s (rank in sorted ShardId order,
+ *                    S/action/search/TransportSearchAction.java:1188,
+ *                    S/cluster/routing/GroupShardsIterator.java:59-62); NULL = 0 … n_shards-1
+ * All segments must share device, dim, encoding and similarity. */
+int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg_shard,
+                        const int32_t* seg_doc_base, int32_t n_shards,
+                        const int32_t* shard_index, osk_view** out);
+int32_t osk_view_release(osk_view* view);
+
+/* Per-shard exact top-k on the device, asynchronous on `stream` (NULL = the library's stream for
+ * the device). All buffers are DEVICE pointers:
+ *   d_queries      n_queries × dim
+ *   d_accept       NULL, or a device array of n_segs device pointers (each NULL or a bitset)
+ *   d_shard_keys   out, n_queries × n_shards × k uint64 "hit keys", best first, 0 = empty slot:
+ *                  key = (sortable(score) << 32) | (0xFFFFFFFF - doc), doc = shard-local docID
+ *   d_shard_counts out, n_queries × n_shards hits per shard (≤ k)
+ *   d_visited      optional out, n_segs int64 (vectors scored per segment, per query) */
+int32_t osk_view_search_device(osk_view* view, const void* d_queries, int32_t n_queries,
+                               int32_t k, const uint64_t* const* d_accept, uint64_t* d_shard_keys,
+                               int32_t* d_shard_counts, int64_t* d_visited, void* stream);
+
+/* Coordinator reduce on the device over per-shard lists laid out as osk_view_search_device
+ * writes them (possibly all-gathered from several GPUs: n_shards = all shards).
+ *   d_shard_index  n_shards shardIndex values (device)
+ *   top-docs size per shard = min(k, from+size) (the shard collector's cut)
+ *   outputs (device): n_queries × size scores/docs/shard indices, per-query count,
+ *   total hits (Σ shard hits) and max score (NaN if no hits). */
+int32_t osk_merge_device(int32_t device, const uint64_t* d_shard_keys,
+                         const int32_t* d_shard_counts, const int32_t* d_shard_index,
+                         int32_t n_queries, int32_t n_shards, int32_t k, int32_t from,
+                         int32_t size, float* d_scores, int32_t* d_docs, int32_t* d_shard_out,
+                         int32_t* d_count, int64_t* d_total_hits, float* d_max_score,
+                         void* stream);
+
+/* Scan-kernel timing (benchmarks): enable/disable and reset; then read the summed duration of the
+ * scan launches of every osk_view_search_device call since enabling (HIP events on the call's
+ * stream) and the number of calls.  Enabling adds one event wait per call; keep it off in
+ * production. */
+int32_t osk_view_profile(osk_view* view, int32_t enable);
+int32_t osk_view_scan_time(osk_view* view, double* total_ms, int64_t* calls);
+
+/* Host-buffer convenience: shard search + coordinator merge on one device, synchronous.
+ * accept: NULL or n_segs host pointers (each NULL or a host bitset). */
+int32_t osk_view_search(osk_view* view, const void* queries, int32_t n_queries, int32_t k,
+                        int32_t from, int32_t size, const uint64_t* const* accept,
+                        float* out_scores, int32_t* out_docs, int32_t* out_shard_index,
+                        int32_t* out_count, int64_t* out_total_hits, float* out_max_score);
+
+/* [L] TopDocs.merge(from, size, shardHits) + TopDocsStats over host arrays (no device).
+ *   shard_counts[s] hits of list s; shard_scores/shard_docs row s holds them at offset s*stride
+ *   (each already sorted score desc, doc asc, as a shard returns them).
+ *   The shardIndex of a hit is hit_shard_index[s*stride+i] when that array is given (lists that
+ *   are themselves partial merges, S/action/search/QueryPhaseResultConsumer.java:212-277), else
+ *   shard_index[s], else s. */
+int32_t osk_topdocs_merge(int32_t n_shards, const int32_t* shard_counts, const float* shard_scores,
+                          const int32_t* shard_docs, int32_t stride, const int32_t* shard_index,
+                          const int32_t* hit_shard_index, int32_t from, int32_t size, float* out_scores, int32_t* out_docs,
+                          int32_t* out_shard_index, int32_t* out_count, int64_t* out_total_hits,
+                          float* out_max_score);
+
+/* Decode hit keys (host). */
+int32_t osk_decode_keys(const uint64_t* keys, int64_t n, float* scores, int32_t* docs);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OSKNN_H */

@@ -1,0 +1,117 @@
+"""ctypes binding of libosknn.so (the C-ABI in include/osknn.h).
+
+This is the Python twin of the Panama FFM binding a Java plugin would use.
+The library is built in-tree (`python -m opensearch_amd.build`); if it is missing we fail loudly —
+there is no CPU fallback for the search path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import threading
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().with_name("libosknn.so")
+
+OSK_OK = 0
+OSK_ERR_INVALID = -1
+OSK_ERR_DEVICE = -2
+OSK_ERR_OOM = -3
+OSK_ERR_UNSUPPORTED = -4
+OSK_ERR_NO_DEVICE = -5
+OSK_MAX_K = 64
+OSK_MAX_DIM = 4096
+
+FLOAT32 = 0
+BYTE = 1
+
+EUCLIDEAN = 0
+DOT_PRODUCT = 1
+COSINE = 2
+MAXIMUM_INNER_PRODUCT = 3
+
+DIST_UNIFORM01 = 0
+DIST_UNIFORM01_X128 = 1
+DIST_NORMALISH = 2
+DIST_NORMALISH_UNIT = 3
+DIST_INT8 = 4
+
+_P = C.c_void_p
+_I32 = C.c_int32
+_I64 = C.c_int64
+_U64 = C.c_uint64
+_PI32 = C.POINTER(C.c_int32)
+_PI64 = C.POINTER(C.c_int64)
+_PF = C.POINTER(C.c_float)
+
+# name → (restype, argtypes); every symbol include/osknn.h declares
+SIGNATURES = {
+    "osk_abi_version": (_I32, []),
+    "osk_last_error": (C.c_char_p, []),
+    "osk_device_count": (_I32, [_PI32]),
+    "osk_seg_stage": (_I32, [_I32, _P, _I64, _I32, _I32, _I32, _P, _I32, C.POINTER(_P)]),
+    "osk_seg_stage_device": (_I32, [_I32, _P, _I64, _I64, _I32, _I32, _I32, _P, _I32, C.POINTER(_P)]),
+    "osk_seg_synth": (_I32, [_I32, _I64, _I32, _I32, _I32, _U64, _I32, _I64, C.POINTER(_P)]),
+    "osk_seg_release": (_I32, [_P]),
+    "osk_seg_info": (_I32, [_P, _PI64, _PI32, _PI32, _PI32, _PI32, _PI32]),
+    "osk_synth_host": (_I32, [_P, _I64, _I64, _I32, _U64, _I32]),
+    "osk_seg_search": (_I32, [_P, _P, _I32, _I32, _P, _P, _P, _P, _P]),
+    "osk_view_create": (_I32, [_P, _I32, _P, _P, _I32, _P, C.POINTER(_P)]),
+    "osk_view_release": (_I32, [_P]),
+    "osk_view_search_device": (_I32, [_P, _P, _I32, _I32, _P, _P, _P, _P, _P]),
+    "osk_merge_device": (_I32, [_I32, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
+    "osk_view_search": (_I32, [_P, _P, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
+    "osk_topdocs_merge": (_I32, [_I32, _P, _P, _P, _I32, _P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P]),
+    "osk_decode_keys": (_I32, [_P, _I64, _P, _P]),
+    "osk_view_profile": (_I32, [_P, _I32]),
+    "osk_view_scan_time": (_I32, [_P, C.POINTER(C.c_double), _PI64]),
+}
+
+
+class OskError(RuntimeError):
+    """A negative return code from libosknn (maps to an IOException / shard failure in Java)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libosknn error {code}: {msg}")
+        self.code = code
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not LIB_PATH.exists():
+                raise RuntimeError(
+                    f"{LIB_PATH} is missing: build it with `python -m opensearch_amd.build` "
+                    "(libosknn has no CPU fallback)")
+            L = C.CDLL(str(LIB_PATH))
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != OSK_OK:
+        msg = lib().osk_last_error()
+        raise OskError(rc, msg.decode() if msg else "")
+
+
+def ptr(a) -> int | None:
+    """Address of a numpy array (or None)."""
+    if a is None:
+        return None
+    return a.ctypes.data
+
+
+def device_count() -> int:
+    n = C.c_int32(0)
+    check(lib().osk_device_count(C.byref(n)))
+    return n.value

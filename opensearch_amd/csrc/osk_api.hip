@@ -1,0 +1,797 @@
+// osk_api.hip — the C-ABI of libosknn.so (declared in include/osknn.h).
+//
+// Object model:
+//   osk_seg   one segment's vector field in HBM (rows padded to 16-byte units, optional row norms,
+//             optional ord→doc map).  Staged once, released by osk_seg_release — the lifetime of a
+//             Lucene KnnVectorsReader ([L] KnnVectorsFormat.fieldsReader … close()).
+//   osk_view  the segments of one or more shards on one device plus the scan's tile table and a
+//             workspace.  A shard's exact top-k = per-leaf exact top-k merged by (score, doc)
+//             ([L] AbstractKnnVectorQuery.rewrite, driven from
+//             S/search/internal/ContextIndexSearcher.java:203-218).
+// Every entry point catches all C++ exceptions and returns an error code (see osknn.h).
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/osknn.h"
+#include "osk_internal.h"
+
+using namespace osk;
+
+namespace osk {
+void set_error(const std::string& msg);
+void clear_error();
+}  // namespace osk
+
+#define OSK_HIP(call)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (call);                                                                \
+        if (e_ != hipSuccess) {                                                                \
+            set_error(std::string(#call) + ": " + hipGetErrorString(e_));                      \
+            return OSK_ERR_DEVICE;                                                             \
+        }                                                                                      \
+    } while (0)
+
+#define OSK_REQUIRE(cond, msg)                                                                 \
+    do {                                                                                       \
+        if (!(cond)) {                                                                         \
+            set_error(msg);                                                                    \
+            return OSK_ERR_INVALID;                                                            \
+        }                                                                                      \
+    } while (0)
+
+#define OSK_GUARD_BEGIN try {
+#define OSK_GUARD_END                                                                          \
+    }                                                                                          \
+    catch (const std::bad_alloc&) {                                                            \
+        set_error("host allocation failed");                                                   \
+        return OSK_ERR_OOM;                                                                    \
+    }                                                                                          \
+    catch (const std::exception& ex) {                                                         \
+        set_error(ex.what());                                                                  \
+        return OSK_ERR_INVALID;                                                                \
+    }                                                                                          \
+    catch (...) {                                                                              \
+        set_error("unknown exception");                                                        \
+        return OSK_ERR_INVALID;                                                                \
+    }
+
+namespace {
+
+// ------------------------------------------------------------------------------------------------
+// devices and streams
+// ------------------------------------------------------------------------------------------------
+std::mutex g_dev_mu;
+std::vector<hipStream_t> g_streams;
+int g_ndev = -1;
+
+int device_count_cached() {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    if (g_ndev < 0) {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+        g_ndev = n;
+        g_streams.assign(n, nullptr);
+    }
+    return g_ndev;
+}
+
+int32_t check_device(int device) {
+    const int n = device_count_cached();
+    if (n <= 0) {
+        set_error("no HIP device visible (libosknn has no CPU fallback)");
+        return OSK_ERR_NO_DEVICE;
+    }
+    if (device < 0 || device >= n) {
+        set_error("device index out of range");
+        return OSK_ERR_INVALID;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+        set_error("hipGetDeviceProperties failed");
+        return OSK_ERR_DEVICE;
+    }
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        set_error(std::string("device is ") + prop.gcnArchName + ", libosknn is built for gfx950");
+        return OSK_ERR_NO_DEVICE;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        set_error("hipSetDevice failed");
+        return OSK_ERR_DEVICE;
+    }
+    return OSK_OK;
+}
+
+hipStream_t device_stream(int device) {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    if (!g_streams[device]) {
+        hipStream_t s;
+        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        g_streams[device] = s;
+    }
+    return g_streams[device];
+}
+
+// device buffer that grows on demand (never inside a timed/captured call once warmed)
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    hipError_t reserve(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) {
+            (void)hipFree(p);
+            p = nullptr;
+            cap = 0;
+        }
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e == hipSuccess) cap = bytes;
+        return e;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+struct HostPinned {
+    void* p = nullptr;
+    size_t cap = 0;
+    ~HostPinned() {
+        if (p) (void)hipHostFree(p);
+    }
+    hipError_t reserve(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) {
+            (void)hipHostFree(p);
+            p = nullptr;
+            cap = 0;
+        }
+        hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+        if (e == hipSuccess) cap = bytes;
+        return e;
+    }
+};
+
+int units_for(int dim, int enc) { return enc == ENC_FLOAT32 ? (dim + 3) / 4 : (dim + 15) / 16; }
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// objects
+// ------------------------------------------------------------------------------------------------
+struct osk_seg {
+    int device = 0;
+    int64_t n_rows = 0;
+    int dim = 0, enc = 0, sim = 0, max_doc = 0;
+    int units = 0, cfg = 0;
+    void* d_rows = nullptr;
+    float* d_xnorm_f = nullptr;
+    int32_t* d_xnorm_i = nullptr;
+    int32_t* d_ord_to_doc = nullptr;
+    std::mutex mu;
+    osk_view* self_view = nullptr;   // single-segment view behind osk_seg_search
+    ~osk_seg();
+};
+
+struct osk_view {
+    int device = 0, dim = 0, enc = 0, sim = 0, units = 0, cfg = 0;
+    std::vector<osk_seg*> segs;
+    int n_shards = 0;
+    std::vector<int32_t> shard_index;
+    std::vector<int32_t> shard_tile_begin;
+    int n_tiles = 0;
+    DevBuf d_segs, d_tiles, d_shard_tile_begin, d_shard_index;
+    // workspace
+    DevBuf ws_cand, ws_q, ws_qnorm, ws_qin, ws_keys, ws_counts, ws_accept_ptrs, ws_accept,
+        ws_out, ws_visited;
+    HostPinned h_stage;
+    std::mutex mu;
+    // scan-kernel timing (osk_view_profile): events bracket the scan launches on the search stream
+    bool profile = false;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double scan_ms = 0.0;
+    int64_t scan_calls = 0;
+    bool pending = false;
+    ~osk_view() {
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+    }
+};
+
+osk_seg::~osk_seg() {
+    if (self_view) delete self_view;
+    if (d_rows) (void)hipFree(d_rows);
+    if (d_xnorm_f) (void)hipFree(d_xnorm_f);
+    if (d_xnorm_i) (void)hipFree(d_xnorm_i);
+    if (d_ord_to_doc) (void)hipFree(d_ord_to_doc);
+}
+
+namespace {
+
+int32_t seg_finish(osk_seg* s, const int32_t* ord_to_doc, hipStream_t st) {
+    // row norms
+    if (s->enc == ENC_FLOAT32 && s->sim == SIM_COSINE) {
+        OSK_HIP(hipMalloc(&s->d_xnorm_f, std::max<int64_t>(1, s->n_rows) * sizeof(float)));
+        if (s->n_rows > 0)
+            OSK_HIP(launch_row_norms_f32(static_cast<const float4*>(s->d_rows), s->n_rows, s->units,
+                                         s->cfg, s->d_xnorm_f, st));
+    }
+    if (s->enc == ENC_BYTE) {
+        OSK_HIP(hipMalloc(&s->d_xnorm_i, std::max<int64_t>(1, s->n_rows) * sizeof(int32_t)));
+        if (s->n_rows > 0)
+            OSK_HIP(launch_row_norms_i8(static_cast<const int4*>(s->d_rows), s->n_rows, s->units,
+                                        s->d_xnorm_i, st));
+    }
+    if (ord_to_doc) {
+        for (int64_t i = 0; i < s->n_rows; ++i) {
+            if (ord_to_doc[i] < 0 || ord_to_doc[i] >= s->max_doc ||
+                (i > 0 && ord_to_doc[i] <= ord_to_doc[i - 1])) {
+                set_error("ord_to_doc must be strictly ascending docIDs in [0, max_doc)");
+                return OSK_ERR_INVALID;
+            }
+        }
+        OSK_HIP(hipMalloc(&s->d_ord_to_doc, std::max<int64_t>(1, s->n_rows) * sizeof(int32_t)));
+        OSK_HIP(hipMemcpyAsync(s->d_ord_to_doc, ord_to_doc, s->n_rows * sizeof(int32_t),
+                               hipMemcpyHostToDevice, st));
+    }
+    OSK_HIP(hipStreamSynchronize(st));
+    return OSK_OK;
+}
+
+int32_t seg_alloc(int device, int64_t n_rows, int dim, int enc, int sim, int max_doc,
+                  const int32_t* ord_to_doc, std::unique_ptr<osk_seg>& out) {
+    OSK_REQUIRE(n_rows >= 0, "n_rows must be >= 0");
+    OSK_REQUIRE(dim >= 1 && dim <= OSK_MAX_DIM, "dim must be in [1, 4096]");
+    OSK_REQUIRE(enc == ENC_FLOAT32 || enc == ENC_BYTE, "unknown encoding");
+    OSK_REQUIRE(sim >= 0 && sim <= 3, "unknown similarity");
+    OSK_REQUIRE(n_rows <= 0x7FFFFFFFll, "a Lucene segment holds < 2^31 docs");
+    if (ord_to_doc == nullptr) OSK_REQUIRE(max_doc >= n_rows, "max_doc < n_rows for a dense field");
+    int32_t rc = check_device(device);
+    if (rc) return rc;
+    auto s = std::make_unique<osk_seg>();
+    s->device = device;
+    s->n_rows = n_rows;
+    s->dim = dim;
+    s->enc = enc;
+    s->sim = sim;
+    s->max_doc = max_doc;
+    s->units = units_for(dim, enc);
+    s->cfg = cfg_index(s->units);
+    const size_t bytes = (size_t)std::max<int64_t>(1, n_rows) * s->units * 16;
+    hipError_t e = hipMalloc(&s->d_rows, bytes);
+    if (e != hipSuccess) {
+        set_error(std::string("hipMalloc of segment rows failed: ") + hipGetErrorString(e));
+        return OSK_ERR_OOM;
+    }
+    out = std::move(s);
+    return OSK_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// C-ABI
+// ------------------------------------------------------------------------------------------------
+extern "C" {
+
+int32_t osk_abi_version(void) { return OSK_ABI_VERSION; }
+
+int32_t osk_device_count(int32_t* n) {
+    OSK_GUARD_BEGIN
+    OSK_REQUIRE(n != nullptr, "n is null");
+    *n = device_count_cached();
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_seg_stage(int32_t device, const void* rows, int64_t n_rows, int32_t dim,
+                      int32_t encoding, int32_t similarity, const int32_t* ord_to_doc,
+                      int32_t max_doc, osk_seg** out) {
+    OSK_GUARD_BEGIN
+    clear_error();
+    OSK_REQUIRE(out != nullptr, "out is null");
+    OSK_REQUIRE(rows != nullptr || n_rows == 0, "rows is null");
+    std::unique_ptr<osk_seg> s;
+    int32_t rc = seg_alloc(device, n_rows, dim, encoding, similarity, max_doc, ord_to_doc, s);
+    if (rc) return rc;
+    hipStream_t st = device_stream(device);
+    const int64_t elem = encoding == ENC_FLOAT32 ? 4 : 1;
+    const int64_t src_pitch = (int64_t)dim * elem;
+    const int64_t dst_pitch = (int64_t)s->units * 16;
+    if (n_rows > 0) {
+        OSK_HIP(hipMemset2DAsync(s->d_rows, dst_pitch, 0, dst_pitch, n_rows, st));
+        OSK_HIP(hipMemcpy2DAsync(s->d_rows, dst_pitch, rows, src_pitch, src_pitch, n_rows,
+                                 hipMemcpyHostToDevice, st));
+    }
+    rc = seg_finish(s.get(), ord_to_doc, st);
+    if (rc) return rc;
+    *out = s.release();
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_seg_stage_device(int32_t device, const void* d_rows, int64_t src_pitch_bytes,
+                             int64_t n_rows, int32_t dim, int32_t encoding, int32_t similarity,
+                             const int32_t* ord_to_doc, int32_t max_doc, osk_seg** out) {
+    OSK_GUARD_BEGIN
+    clear_error();
+    OSK_REQUIRE(out != nullptr, "out is null");
+    OSK_REQUIRE(d_rows != nullptr || n_rows == 0, "d_rows is null");
+    std::unique_ptr<osk_seg> s;
+    int32_t rc = seg_alloc(device, n_rows, dim, encoding, similarity, max_doc, ord_to_doc, s);
+    if (rc) return rc;
+    hipStream_t st = device_stream(device);
+    const int64_t elem = encoding == ENC_FLOAT32 ? 4 : 1;
+    OSK_REQUIRE(src_pitch_bytes >= (int64_t)dim * elem, "src_pitch_bytes < dim * element size");
+    if (n_rows > 0)
+        OSK_HIP(launch_pad_rows(d_rows, src_pitch_bytes, s->d_rows, (int64_t)s->units * 16, n_rows,
+                                (int64_t)dim * elem, st));
+    rc = seg_finish(s.get(), ord_to_doc, st);
+    if (rc) return rc;
+    *out = s.release();
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_seg_synth(int32_t device, int64_t n_rows, int32_t dim, int32_t encoding,
+                      int32_t similarity, uint64_t seed, int32_t dist, int64_t row0,
+                      osk_seg** out) {
+    OSK_GUARD_BEGIN
+    clear_error();
+    OSK_REQUIRE(out != nullptr, "out is null");
+    OSK_REQUIRE(dist >= 0 && dist <= 4, "unknown dist");
+    OSK_REQUIRE((dist == DIST_INT8) == (encoding == ENC_BYTE), "dist INT8 <=> encoding BYTE");
+    OSK_REQUIRE(n_rows <= 0x7FFFFFFFll, "a Lucene segment holds < 2^31 docs");
+    std::unique_ptr<osk_seg> s;
+    int32_t rc = seg_alloc(device, n_rows, dim, encoding, similarity, (int32_t)n_rows, nullptr, s);
+    if (rc) return rc;
+    hipStream_t st = device_stream(device);
+    if (n_rows > 0)
+        OSK_HIP(launch_synth(s->d_rows, n_rows, dim, s->units, encoding, seed, dist, row0, st));
+    rc = seg_finish(s.get(), nullptr, st);
+    if (rc) return rc;
+    *out = s.release();
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_seg_release(osk_seg* seg) {
+    OSK_GUARD_BEGIN
+    if (!seg) return OSK_OK;
+    (void)hipSetDevice(seg->device);
+    delete seg;
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_seg_info(const osk_seg* seg, int64_t* n_rows, int32_t* dim, int32_t* encoding,
+                     int32_t* similarity, int32_t* max_doc, int32_t* device) {
+    OSK_GUARD_BEGIN
+    OSK_REQUIRE(seg != nullptr, "seg is null");
+    if (n_rows) *n_rows = seg->n_rows;
+    if (dim) *dim = seg->dim;
+    if (encoding) *encoding = seg->enc;
+    if (similarity) *similarity = seg->sim;
+    if (max_doc) *max_doc = seg->max_doc;
+    if (device) *device = seg->device;
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg_shard,
+                        const int32_t* seg_doc_base, int32_t n_shards, const int32_t* shard_index,
+                        osk_view** out) {
+    OSK_GUARD_BEGIN
+    clear_error();
+    OSK_REQUIRE(out != nullptr && segs != nullptr, "null argument");
+    OSK_REQUIRE(n_segs >= 1, "need at least one segment");
+    OSK_REQUIRE(n_shards >= 1, "need at least one shard");
+    const osk_seg* s0 = segs[0];
+    OSK_REQUIRE(s0 != nullptr, "null segment");
+    for (int i = 0; i < n_segs; ++i) {
+        OSK_REQUIRE(segs[i] != nullptr, "null segment");
+        OSK_REQUIRE(segs[i]->device == s0->device && segs[i]->dim == s0->dim &&
+                        segs[i]->enc == s0->enc && segs[i]->sim == s0->sim,
+                    "segments of a view must share device, dim, encoding and similarity");
+        const int sh = seg_shard ? seg_shard[i] : 0;
+        OSK_REQUIRE(sh >= 0 && sh < n_shards, "seg_shard out of range");
+        OSK_REQUIRE(!seg_doc_base || seg_doc_base[i] >= 0, "negative doc base");
+    }
+    int32_t rc = check_device(s0->device);
+    if (rc) return rc;
+    auto v = std::make_unique<osk_view>();
+    v->device = s0->device;
+    v->dim = s0->dim;
+    v->enc = s0->enc;
+    v->sim = s0->sim;
+    v->units = s0->units;
+    v->cfg = s0->cfg;
+    v->segs.assign(segs, segs + n_segs);
+    v->n_shards = n_shards;
+    v->shard_index.resize(n_shards);
+    for (int s = 0; s < n_shards; ++s) v->shard_index[s] = shard_index ? shard_index[s] : s;
+
+    // tiles: ~2048 per view (8 per CU), never smaller than 8 row-groups per wave
+    static const int kL[9] = {4, 8, 8, 16, 16, 16, 32, 64, 64};
+    const int R = 64 / kL[v->cfg];
+    int64_t total = 0;
+    for (int i = 0; i < n_segs; ++i) total += segs[i]->n_rows;
+    const int64_t min_rows = 4LL * R * 8;
+    const int64_t target = 2048;
+    const int64_t rows_per_tile = std::max<int64_t>(min_rows, (total + target - 1) / target);
+    std::vector<TileDev> tiles;
+    v->shard_tile_begin.assign(n_shards + 1, 0);
+    for (int sh = 0; sh < n_shards; ++sh) {
+        v->shard_tile_begin[sh] = (int32_t)tiles.size();
+        for (int i = 0; i < n_segs; ++i) {
+            if ((seg_shard ? seg_shard[i] : 0) != sh) continue;
+            const int64_t n = segs[i]->n_rows;
+            if (n == 0) continue;
+            const int64_t nt = (n + rows_per_tile - 1) / rows_per_tile;
+            const int64_t per = (n + nt - 1) / nt;
+            for (int64_t b = 0; b < n; b += per)
+                tiles.push_back(TileDev{i, sh, b, std::min(n, b + per)});
+        }
+    }
+    v->shard_tile_begin[n_shards] = (int32_t)tiles.size();
+    v->n_tiles = (int)tiles.size();
+    OSK_REQUIRE(v->n_tiles < (1 << 24), "too many tiles");
+
+    std::vector<SegDev> sd(n_segs);
+    for (int i = 0; i < n_segs; ++i) {
+        const osk_seg* s = segs[i];
+        sd[i] = SegDev{s->d_rows, s->d_xnorm_f, s->d_xnorm_i, s->d_ord_to_doc, s->n_rows,
+                       seg_doc_base ? seg_doc_base[i] : 0, seg_shard ? seg_shard[i] : 0};
+    }
+    hipStream_t st = device_stream(v->device);
+    OSK_HIP(v->d_segs.reserve(sizeof(SegDev) * n_segs));
+    OSK_HIP(v->d_tiles.reserve(sizeof(TileDev) * std::max<size_t>(1, tiles.size())));
+    OSK_HIP(v->d_shard_tile_begin.reserve(sizeof(int32_t) * (n_shards + 1)));
+    OSK_HIP(v->d_shard_index.reserve(sizeof(int32_t) * n_shards));
+    OSK_HIP(hipMemcpyAsync(v->d_segs.p, sd.data(), sizeof(SegDev) * n_segs, hipMemcpyHostToDevice, st));
+    if (!tiles.empty())
+        OSK_HIP(hipMemcpyAsync(v->d_tiles.p, tiles.data(), sizeof(TileDev) * tiles.size(),
+                               hipMemcpyHostToDevice, st));
+    OSK_HIP(hipMemcpyAsync(v->d_shard_tile_begin.p, v->shard_tile_begin.data(),
+                           sizeof(int32_t) * (n_shards + 1), hipMemcpyHostToDevice, st));
+    OSK_HIP(hipMemcpyAsync(v->d_shard_index.p, v->shard_index.data(), sizeof(int32_t) * n_shards,
+                           hipMemcpyHostToDevice, st));
+    OSK_HIP(hipStreamSynchronize(st));
+    *out = v.release();
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_view_release(osk_view* view) {
+    OSK_GUARD_BEGIN
+    if (!view) return OSK_OK;
+    (void)hipSetDevice(view->device);
+    delete view;
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+}  // extern "C"
+
+namespace {
+
+// Core of osk_view_search_device (caller holds no lock; device already set).
+int32_t view_search_device(osk_view* v, const void* d_queries, int nq, int k,
+                           const uint64_t* const* d_accept, uint64_t* d_shard_keys,
+                           int32_t* d_shard_counts, int64_t* d_visited, hipStream_t st) {
+    OSK_REQUIRE(nq >= 1, "n_queries must be >= 1");
+    OSK_REQUIRE(k >= 1 && k <= OSK_MAX_K, "k must be in [1, OSK_MAX_K]");
+    OSK_REQUIRE(d_queries && d_shard_keys && d_shard_counts, "null device buffer");
+    static const int kLV[9][2] = {{4, 2}, {8, 2}, {8, 4}, {16, 4}, {16, 8}, {16, 12},
+                                  {32, 8}, {64, 8}, {64, 16}};
+    const int UP = kLV[v->cfg][0] * kLV[v->cfg][1];
+    const int nq_pad = (nq + kMaxNQ - 1) / kMaxNQ * kMaxNQ;
+    const int64_t elem = v->enc == ENC_FLOAT32 ? 4 : 1;
+
+    if (v->n_tiles == 0) {   // nothing staged: every shard returns zero hits
+        OSK_HIP(hipMemsetAsync(d_shard_keys, 0, sizeof(uint64_t) * nq * v->n_shards * k, st));
+        OSK_HIP(hipMemsetAsync(d_shard_counts, 0, sizeof(int32_t) * nq * v->n_shards, st));
+        if (d_visited) OSK_HIP(hipMemsetAsync(d_visited, 0, sizeof(int64_t) * v->segs.size(), st));
+        return OSK_OK;
+    }
+    OSK_HIP(v->ws_cand.reserve(sizeof(uint64_t) * (size_t)nq * v->n_tiles * k));
+    OSK_HIP(v->ws_q.reserve((size_t)nq_pad * UP * 16));
+    OSK_HIP(v->ws_qnorm.reserve(sizeof(float) * nq_pad));
+    // queries → padded unit layout (zeros past dim and for the dummy queries of the last launch)
+    OSK_HIP(hipMemsetAsync(v->ws_q.p, 0, (size_t)nq_pad * UP * 16, st));
+    OSK_HIP(launch_pad_rows(d_queries, (int64_t)v->dim * elem, v->ws_q.p, (int64_t)UP * 16, nq,
+                            (int64_t)v->dim * elem, st));
+    OSK_HIP(hipMemsetAsync(v->ws_qnorm.p, 0, sizeof(float) * nq_pad, st));
+    if (v->enc == ENC_FLOAT32 && v->sim == SIM_COSINE)
+        OSK_HIP(launch_row_norms_f32(v->ws_q.as<float4>(), nq, UP, v->cfg, v->ws_qnorm.as<float>(), st));
+    if (v->enc == ENC_BYTE)
+        OSK_HIP(launch_row_norms_i8(v->ws_q.as<int4>(), nq, UP, v->ws_qnorm.as<int32_t>(), st));
+
+    if (d_visited) OSK_HIP(hipMemsetAsync(d_visited, 0, sizeof(int64_t) * v->segs.size(), st));
+
+    ScanParams p{};
+    p.segs = v->d_segs.as<SegDev>();
+    p.tiles = v->d_tiles.as<TileDev>();
+    p.accept = d_accept;
+    p.cand = v->ws_cand.as<uint64_t>();
+    p.visited = reinterpret_cast<unsigned long long*>(d_visited);
+    p.n_tiles = v->n_tiles;
+    p.units = v->units;
+    p.k = k;
+    p.sim = v->sim;
+    p.dim = v->dim;
+    if (v->profile) {
+        if (v->pending) {   // fold the previous call's interval (already complete or we wait)
+            float ms = 0.f;
+            OSK_HIP(hipEventSynchronize(v->ev1));
+            OSK_HIP(hipEventElapsedTime(&ms, v->ev0, v->ev1));
+            v->scan_ms += ms;
+            v->scan_calls += 1;
+            v->pending = false;
+        }
+        OSK_HIP(hipEventRecord(v->ev0, st));
+    }
+    for (int q0 = 0; q0 < nq; q0 += kMaxNQ) {
+        const int qc = std::min(kMaxNQ, nq - q0);
+        p.q0 = q0;
+        p.q_count = qc;
+        p.q = static_cast<const char*>(v->ws_q.p) + (size_t)q0 * UP * 16;
+        p.qnorm_f = v->ws_qnorm.as<float>() + q0;
+        p.qnorm_i = v->ws_qnorm.as<int32_t>() + q0;
+        OSK_HIP(launch_scan(v->enc, v->cfg, qc, p, st));
+    }
+    if (v->profile) {
+        OSK_HIP(hipEventRecord(v->ev1, st));
+        v->pending = true;
+    }
+    OSK_HIP(launch_merge_shards(v->ws_cand.as<uint64_t>(), v->n_tiles,
+                                v->d_shard_tile_begin.as<int32_t>(), v->n_shards, nq, k,
+                                d_shard_keys, d_shard_counts, st));
+    return OSK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t osk_view_search_device(osk_view* view, const void* d_queries, int32_t n_queries, int32_t k,
+                               const uint64_t* const* d_accept, uint64_t* d_shard_keys,
+                               int32_t* d_shard_counts, int64_t* d_visited, void* stream) {
+    OSK_GUARD_BEGIN
+    clear_error();
+    OSK_REQUIRE(view != nullptr, "view is null");
+    int32_t rc = check_device(view->device);
+    if (rc) return rc;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : device_stream(view->device);
+    std::lock_guard<std::mutex> lk(view->mu);
+    return view_search_device(view, d_queries, n_queries, k, d_accept, d_shard_keys, d_shard_counts,
+                              d_visited, st);
+    OSK_GUARD_END
+}
+
+int32_t osk_merge_device(int32_t device, const uint64_t* d_shard_keys, const int32_t* d_shard_counts,
+                         const int32_t* d_shard_index, int32_t n_queries, int32_t n_shards, int32_t k,
+                         int32_t from, int32_t size, float* d_scores, int32_t* d_docs,
+                         int32_t* d_shard_out, int32_t* d_count, int64_t* d_total_hits,
+                         float* d_max_score, void* stream) {
+    OSK_GUARD_BEGIN
+    clear_error();
+    OSK_REQUIRE(n_queries >= 1 && n_shards >= 1, "n_queries and n_shards must be >= 1");
+    OSK_REQUIRE(k >= 1 && k <= OSK_MAX_K, "k must be in [1, OSK_MAX_K]");
+    OSK_REQUIRE(from >= 0 && size >= 1 && (int64_t)from + size <= 100000, "bad from/size");
+    OSK_REQUIRE((int64_t)n_shards * std::min(k, from + size) <= 4096,
+                "n_shards * min(k, from+size) exceeds 4096 hits per query");
+    OSK_REQUIRE(d_shard_keys && d_shard_counts && d_shard_index && d_scores && d_docs && d_shard_out &&
+                    d_count && d_total_hits && d_max_score,
+                "null device buffer");
+    int32_t rc = check_device(device);
+    if (rc) return rc;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : device_stream(device);
+    OSK_HIP(launch_merge_coord(d_shard_keys, d_shard_counts, d_shard_index, n_queries, n_shards, k,
+                               from, size, d_scores, d_docs, d_shard_out, d_count, d_total_hits,
+                               d_max_score, st));
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+// Scan-kernel timing for bench.py: enable, then read the mean duration of the scan launches of
+// each search call (all query chunks of one call together) since enabling.
+int32_t osk_view_profile(osk_view* v, int32_t enable) {
+    OSK_GUARD_BEGIN
+    OSK_REQUIRE(v != nullptr, "view is null");
+    int32_t rc = check_device(v->device);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(v->mu);
+    if (enable && !v->ev0) {
+        OSK_HIP(hipEventCreate(&v->ev0));
+        OSK_HIP(hipEventCreate(&v->ev1));
+    }
+    v->profile = enable != 0;
+    v->scan_ms = 0.0;
+    v->scan_calls = 0;
+    v->pending = false;
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_view_scan_time(osk_view* v, double* total_ms, int64_t* calls) {
+    OSK_GUARD_BEGIN
+    OSK_REQUIRE(v != nullptr && total_ms && calls, "null argument");
+    int32_t rc = check_device(v->device);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(v->mu);
+    if (v->pending) {
+        float ms = 0.f;
+        OSK_HIP(hipEventSynchronize(v->ev1));
+        OSK_HIP(hipEventElapsedTime(&ms, v->ev0, v->ev1));
+        v->scan_ms += ms;
+        v->scan_calls += 1;
+        v->pending = false;
+    }
+    *total_ms = v->scan_ms;
+    *calls = v->scan_calls;
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+// Host-buffer search + coordinator merge on one device (synchronous).
+int32_t osk_view_search(osk_view* v, const void* queries, int32_t n_queries, int32_t k, int32_t from,
+                        int32_t size, const uint64_t* const* accept, float* out_scores,
+                        int32_t* out_docs, int32_t* out_shard_index, int32_t* out_count,
+                        int64_t* out_total_hits, float* out_max_score) {
+    OSK_GUARD_BEGIN
+    clear_error();
+    OSK_REQUIRE(v != nullptr && queries != nullptr, "null argument");
+    OSK_REQUIRE(out_scores && out_docs && out_shard_index && out_count && out_total_hits && out_max_score,
+                "null output");
+    OSK_REQUIRE(n_queries >= 1, "n_queries must be >= 1");
+    OSK_REQUIRE(from >= 0 && size >= 1, "bad from/size");
+    OSK_REQUIRE((int64_t)v->n_shards * std::min(k, from + size) <= 4096,
+                "n_shards * min(k, from+size) exceeds 4096 hits per query");
+    int32_t rc = check_device(v->device);
+    if (rc) return rc;
+    hipStream_t st = device_stream(v->device);
+    std::lock_guard<std::mutex> lk(v->mu);
+    const int nq = n_queries, S = v->n_shards, ns = (int)v->segs.size();
+    const int64_t elem = v->enc == ENC_FLOAT32 ? 4 : 1;
+    const size_t qbytes = (size_t)nq * v->dim * elem;
+
+    // accept bitsets → device
+    const uint64_t* const* d_acc = nullptr;
+    if (accept) {
+        size_t words = 0;
+        for (int i = 0; i < ns; ++i)
+            if (accept[i]) words += (size_t)(v->segs[i]->max_doc + 63) / 64;
+        OSK_HIP(v->ws_accept.reserve(std::max<size_t>(8, words * 8)));
+        OSK_HIP(v->ws_accept_ptrs.reserve(sizeof(void*) * ns));
+        std::vector<const uint64_t*> ptrs(ns, nullptr);
+        size_t off = 0;
+        for (int i = 0; i < ns; ++i) {
+            if (!accept[i]) continue;
+            const size_t w = (size_t)(v->segs[i]->max_doc + 63) / 64;
+            ptrs[i] = v->ws_accept.as<uint64_t>() + off;
+            OSK_HIP(hipMemcpyAsync(const_cast<uint64_t*>(ptrs[i]), accept[i], w * 8,
+                                   hipMemcpyHostToDevice, st));
+            off += w;
+        }
+        OSK_HIP(hipMemcpyAsync(v->ws_accept_ptrs.p, ptrs.data(), sizeof(void*) * ns,
+                               hipMemcpyHostToDevice, st));
+        d_acc = v->ws_accept_ptrs.as<const uint64_t*>();
+    }
+    OSK_HIP(v->ws_qin.reserve(std::max<size_t>(16, qbytes)));
+    OSK_HIP(hipMemcpyAsync(v->ws_qin.p, queries, qbytes, hipMemcpyHostToDevice, st));
+    OSK_HIP(v->ws_keys.reserve(sizeof(uint64_t) * (size_t)nq * S * k));
+    OSK_HIP(v->ws_counts.reserve(sizeof(int32_t) * (size_t)nq * S));
+    rc = view_search_device(v, v->ws_qin.p, nq, k, d_acc, v->ws_keys.as<uint64_t>(),
+                            v->ws_counts.as<int32_t>(), nullptr, st);
+    if (rc) return rc;
+    // outputs: scores f32 | docs i32 | shard i32 | count i32 | total i64 | max f32
+    const size_t n_out = (size_t)nq * size;
+    const size_t b_sc = n_out * 4, b_doc = n_out * 4, b_sh = n_out * 4, b_cnt = nq * 4,
+                 b_tot = nq * 8, b_max = nq * 4;
+    const size_t o_sc = 0, o_doc = o_sc + b_sc, o_sh = o_doc + b_doc, o_cnt = o_sh + b_sh,
+                 o_tot = (o_cnt + b_cnt + 7) / 8 * 8, o_max = o_tot + b_tot,
+                 total_b = o_max + b_max;
+    OSK_HIP(v->ws_out.reserve(total_b));
+    char* ob = v->ws_out.as<char>();
+    OSK_HIP(launch_merge_coord(v->ws_keys.as<uint64_t>(), v->ws_counts.as<int32_t>(),
+                               v->d_shard_index.as<int32_t>(), nq, S, k, from, size,
+                               reinterpret_cast<float*>(ob + o_sc), reinterpret_cast<int32_t*>(ob + o_doc),
+                               reinterpret_cast<int32_t*>(ob + o_sh), reinterpret_cast<int32_t*>(ob + o_cnt),
+                               reinterpret_cast<int64_t*>(ob + o_tot), reinterpret_cast<float*>(ob + o_max),
+                               st));
+    OSK_HIP(v->h_stage.reserve(total_b));
+    OSK_HIP(hipMemcpyAsync(v->h_stage.p, ob, total_b, hipMemcpyDeviceToHost, st));
+    OSK_HIP(hipStreamSynchronize(st));
+    const char* hb = static_cast<const char*>(v->h_stage.p);
+    std::memcpy(out_scores, hb + o_sc, b_sc);
+    std::memcpy(out_docs, hb + o_doc, b_doc);
+    std::memcpy(out_shard_index, hb + o_sh, b_sh);
+    std::memcpy(out_count, hb + o_cnt, b_cnt);
+    std::memcpy(out_total_hits, hb + o_tot, b_tot);
+    std::memcpy(out_max_score, hb + o_max, b_max);
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+// [L] KnnVectorsReader.search on one segment (host buffers, synchronous).
+int32_t osk_seg_search(osk_seg* seg, const void* queries, int32_t n_queries, int32_t k,
+                       const uint64_t* accept_bits, float* out_scores, int32_t* out_docs,
+                       int32_t* out_count, int64_t* out_visited) {
+    OSK_GUARD_BEGIN
+    clear_error();
+    OSK_REQUIRE(seg != nullptr && queries != nullptr, "null argument");
+    OSK_REQUIRE(out_scores && out_docs && out_count, "null output");
+    OSK_REQUIRE(n_queries >= 1, "n_queries must be >= 1");
+    OSK_REQUIRE(k >= 1 && k <= OSK_MAX_K, "k must be in [1, OSK_MAX_K]");
+    int32_t rc = check_device(seg->device);
+    if (rc) return rc;
+    osk_view* v;
+    {
+        std::lock_guard<std::mutex> lk(seg->mu);
+        if (!seg->self_view) {
+            osk_seg* one[1] = {seg};
+            rc = osk_view_create(one, 1, nullptr, nullptr, 1, nullptr, &seg->self_view);
+            if (rc) return rc;
+        }
+        v = seg->self_view;
+    }
+    (void)hipSetDevice(seg->device);
+    hipStream_t st = device_stream(seg->device);
+    std::lock_guard<std::mutex> lk(v->mu);
+    const int nq = n_queries;
+    const int64_t elem = seg->enc == ENC_FLOAT32 ? 4 : 1;
+    const size_t qbytes = (size_t)nq * seg->dim * elem;
+    const uint64_t* const* d_acc = nullptr;
+    if (accept_bits) {
+        const size_t w = (size_t)(seg->max_doc + 63) / 64;
+        OSK_HIP(v->ws_accept.reserve(std::max<size_t>(8, w * 8)));
+        OSK_HIP(v->ws_accept_ptrs.reserve(sizeof(void*)));
+        if (w) OSK_HIP(hipMemcpyAsync(v->ws_accept.p, accept_bits, w * 8, hipMemcpyHostToDevice, st));
+        const uint64_t* ptr = v->ws_accept.as<uint64_t>();
+        OSK_HIP(hipMemcpyAsync(v->ws_accept_ptrs.p, &ptr, sizeof(void*), hipMemcpyHostToDevice, st));
+        d_acc = v->ws_accept_ptrs.as<const uint64_t*>();
+    }
+    OSK_HIP(v->ws_qin.reserve(std::max<size_t>(16, qbytes)));
+    OSK_HIP(hipMemcpyAsync(v->ws_qin.p, queries, qbytes, hipMemcpyHostToDevice, st));
+    OSK_HIP(v->ws_keys.reserve(sizeof(uint64_t) * (size_t)nq * k));
+    OSK_HIP(v->ws_counts.reserve(sizeof(int32_t) * (size_t)nq));
+    OSK_HIP(v->ws_visited.reserve(sizeof(int64_t)));
+    rc = view_search_device(v, v->ws_qin.p, nq, k, d_acc, v->ws_keys.as<uint64_t>(),
+                            v->ws_counts.as<int32_t>(), v->ws_visited.as<int64_t>(), st);
+    if (rc) return rc;
+    const size_t kb = sizeof(uint64_t) * (size_t)nq * k, cb = sizeof(int32_t) * nq;
+    OSK_HIP(v->h_stage.reserve(kb + cb + 8));
+    char* hb = static_cast<char*>(v->h_stage.p);
+    OSK_HIP(hipMemcpyAsync(hb, v->ws_keys.p, kb, hipMemcpyDeviceToHost, st));
+    OSK_HIP(hipMemcpyAsync(hb + kb, v->ws_counts.p, cb, hipMemcpyDeviceToHost, st));
+    OSK_HIP(hipMemcpyAsync(hb + kb + cb, v->ws_visited.p, 8, hipMemcpyDeviceToHost, st));
+    OSK_HIP(hipStreamSynchronize(st));
+    const uint64_t* keys = reinterpret_cast<const uint64_t*>(hb);
+    const int32_t* cnt = reinterpret_cast<const int32_t*>(hb + kb);
+    int64_t visited;
+    std::memcpy(&visited, hb + kb + cb, 8);
+    for (int q = 0; q < nq; ++q) {
+        out_count[q] = cnt[q];
+        for (int i = 0; i < k; ++i) {
+            const uint64_t key = keys[(size_t)q * k + i];
+            const size_t o = (size_t)q * k + i;
+            if (i < cnt[q]) {
+                out_scores[o] = key_score(key);
+                out_docs[o] = key_doc(key);
+            } else {
+                out_scores[o] = -__builtin_inff();
+                out_docs[o] = 0x7FFFFFFF;
+            }
+        }
+        if (out_visited) out_visited[q] = visited;
+    }
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+}  // extern "C"

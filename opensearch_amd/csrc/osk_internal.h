@@ -1,0 +1,70 @@
+// osk_internal.h — device-side structures and kernel launchers shared by osk_kernels.hip and
+// osk_api.hip.  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "osk_common.h"
+
+namespace osk {
+
+// One segment as the scan kernels see it.
+struct SegDev {
+    const void* rows;            // f32: float4[n_rows][units]; byte: 16-B chunks [n_rows][units]
+    const float* xnorm_f;        // f32 COSINE: |x|² per row (lane-layout order), else null
+    const int32_t* xnorm_i;      // byte: Σx² per row (exact), else null
+    const int32_t* ord_to_doc;   // null = dense (doc == ord)
+    int64_t n_rows;
+    int32_t doc_base;            // LeafReaderContext.docBase inside the shard
+    int32_t shard;               // result group
+};
+
+// A contiguous run of rows of one segment, scanned by one 256-thread workgroup.
+struct TileDev {
+    int32_t seg;
+    int32_t shard;
+    int64_t row_begin;
+    int64_t row_end;
+};
+
+struct ScanParams {
+    const SegDev* segs;
+    const TileDev* tiles;
+    const uint64_t* const* accept;   // device array [n_segs] of bitsets (entries may be null), or null
+    const void* q;                   // this launch's queries, each padded to L*V units (zeros)
+    const float* qnorm_f;            // this launch's query norms (COSINE f32)
+    const int32_t* qnorm_i;          // this launch's query Σq² (byte)
+    uint64_t* cand;                  // [nq_total][n_tiles][k] per-tile candidate keys
+    unsigned long long* visited;     // [n_segs] or null (counted by the q0 == 0 launch only)
+    int n_tiles;
+    int q0;                          // global index of this launch's first query
+    int q_count;                     // queries in this launch (≤ NQ of the instantiation)
+    int units;                       // float4s (f32) / 16-B chunks (byte) per stored row
+    int k;
+    int sim;
+    int dim;
+};
+
+constexpr int kBlock = 256;          // 4 wavefronts per workgroup
+constexpr int kMaxNQ = 8;            // queries per streaming-scan launch
+
+int cfg_index(int units);            // index into the lane-config table (0..8)
+
+hipError_t launch_scan(int enc, int cfg, int nq, const ScanParams& p, hipStream_t s);
+hipError_t launch_row_norms_f32(const float4* rows, int64_t n_rows, int units, int cfg,
+                                float* out, hipStream_t s);
+hipError_t launch_row_norms_i8(const int4* rows, int64_t n_rows, int units, int32_t* out,
+                               hipStream_t s);
+hipError_t launch_synth(void* rows, int64_t n_rows, int dim, int units, int enc, uint64_t seed,
+                        int dist, int64_t row0, hipStream_t s);
+hipError_t launch_pad_rows(const void* src, int64_t src_pitch, void* dst, int64_t dst_pitch,
+                           int64_t n_rows, int64_t row_bytes, hipStream_t s);
+hipError_t launch_merge_shards(const uint64_t* cand, int n_tiles, const int32_t* shard_tile_begin,
+                               int n_shards, int nq, int k, uint64_t* shard_keys,
+                               int32_t* shard_counts, hipStream_t s);
+hipError_t launch_merge_coord(const uint64_t* shard_keys, const int32_t* shard_counts,
+                              const int32_t* shard_index, int nq, int n_shards, int k, int from,
+                              int size, float* scores, int32_t* docs, int32_t* shard_out,
+                              int32_t* count, int64_t* total_hits, float* max_score,
+                              hipStream_t s);
+
+}  // namespace osk

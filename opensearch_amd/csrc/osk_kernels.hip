@@ -1,0 +1,615 @@
+// osk_kernels.hip — CDNA4 (gfx950) kernels of the exact k-NN scoring path.
+//
+//   scan_f32 / scan_i8   HBM-streaming exact scoring of a shard's segments fused with a
+//                        wavefront top-k select (replaces [L] AbstractKnnVectorQuery.exactSearch's
+//                        per-doc VectorSimilarityFunction.compare loop + HitQueue, driven from
+//                        S/search/internal/ContextIndexSearcher.java:203-218).
+//   merge_shards         per-shard top-k out of the per-tile lists ([L] TopDocs.merge(k, perLeaf)
+//                        inside AbstractKnnVectorQuery.rewrite).
+//   merge_coord          coordinator reduce (S/action/search/SearchPhaseController.java:224-246,
+//                        [L] TopDocs.merge(from, size, …): score desc, shardIndex asc, doc asc).
+//   row_norms_*, synth_*, pad_rows   staging helpers.
+//
+// Design notes (full rationale in DESIGN.md):
+//   * A row is scored by L lanes of one wavefront (lane_cfg(dim)); each lane streams V 16-byte
+//     units with global_load_dwordx4, so one wave-instruction moves 1 KiB of contiguous-per-row
+//     bytes.  The batch-1 path is HBM-bound by ~30x over the VALU; nothing is staged in LDS.
+//   * Scores never round-trip through HBM: every wavefront keeps a sorted top-k list in lanes
+//     0..k-1 of a register and a wave-uniform threshold; a row-group only costs a ballot unless a
+//     score beats the threshold (rare after the first few hundred rows).
+#include "osk_internal.h"
+
+namespace osk {
+
+// ------------------------------------------------------------------------------------------------
+// wavefront helpers
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t shfl_up1_64(uint64_t v) {
+    int lo = __shfl_up((int)(uint32_t)v, 1);
+    int hi = __shfl_up((int)(uint32_t)(v >> 32), 1);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+// Insert key K (known to beat thr = lk[k-1]) into the wave's sorted-descending list held in
+// lanes 0..k-1 of lk.  Entries better than K form a prefix; K goes to lane `pos`, the tail
+// shifts down one lane and the old k-th entry falls off.
+__device__ __forceinline__ void wave_insert(uint64_t& lk, uint64_t& thr, uint64_t K, int lane,
+                                            int k) {
+    const uint64_t better = __ballot(lane < k && lk > K);
+    const int pos = __popcll(better);
+    const uint64_t up = shfl_up1_64(lk);
+    lk = lane < pos ? lk : (lane == pos ? K : up);
+    thr = readlane64(lk, k - 1);
+}
+
+// Offer each lane's key where `offer` holds; wave-uniform loop over the (few) lanes that beat thr.
+__device__ __forceinline__ void wave_offer(uint64_t key, bool offer, uint64_t& lk, uint64_t& thr,
+                                           int lane, int k) {
+    uint64_t m = __ballot(offer && key > thr);
+    while (m) {
+        const int src = __builtin_ctzll(m);
+        const uint64_t K = readlane64(key, src);
+        wave_insert(lk, thr, K, lane, k);
+        m &= ~(1ull << src);
+        m &= __ballot(offer && key > thr);
+    }
+}
+
+// Fold the lists of waves 1..3 (in LDS) into wave 0's list.
+__device__ __forceinline__ void block_fold(const uint64_t* lists /*[4][64]*/, uint64_t& lk,
+                                           uint64_t& thr, int lane, int k) {
+    for (int w = 1; w < 4; ++w) {
+        const uint64_t key = lane < k ? lists[w * 64 + lane] : 0ull;
+        wave_offer(key, true, lk, thr, lane, k);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// streaming scan, float32
+// ------------------------------------------------------------------------------------------------
+template <int L, int V, int NQ, bool L2K>
+__global__ __launch_bounds__(kBlock) void scan_f32(ScanParams p) {
+    constexpr int R = 64 / L;                 // rows per wave-iteration
+    constexpr int UP = L * V;                 // padded float4s per query
+    constexpr bool QREG = NQ * V * 4 <= 64;   // query fragments in VGPRs, else read from LDS
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float4* sq = reinterpret_cast<float4*>(smem);
+    uint64_t* slist = reinterpret_cast<uint64_t*>(smem + (QREG ? 0 : NQ * UP * 16));
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int t = lane & (L - 1), g = lane / L;
+    const TileDev tile = p.tiles[blockIdx.x];
+    const SegDev seg = p.segs[tile.seg];
+    const float4* __restrict__ X = static_cast<const float4*>(seg.rows);
+    const float4* __restrict__ Q = static_cast<const float4*>(p.q);
+    const int units = p.units;
+
+    float4 qf[QREG ? NQ : 1][QREG ? V : 1];
+    if constexpr (QREG) {
+#pragma unroll
+        for (int b = 0; b < NQ; ++b)
+#pragma unroll
+            for (int j = 0; j < V; ++j) qf[b][j] = Q[b * UP + t + j * L];
+    } else {
+        for (int i = tid; i < NQ * UP; i += kBlock) sq[i] = Q[i];
+        __syncthreads();
+    }
+    float qn[NQ];
+#pragma unroll
+    for (int b = 0; b < NQ; ++b) qn[b] = p.qnorm_f ? p.qnorm_f[b] : 0.0f;
+
+    const int64_t rows = tile.row_end - tile.row_begin;
+    const int64_t per_wave = ((rows + 4 * R - 1) / (4 * R)) * R;
+    const int64_t wb = tile.row_begin + wave * per_wave;
+    const int64_t we = min(wb + per_wave, tile.row_end);
+    const uint64_t* abits = p.accept ? p.accept[tile.seg] : nullptr;
+    const int sim = p.sim, k = p.k;
+
+    uint64_t lk[NQ], thr[NQ];
+#pragma unroll
+    for (int b = 0; b < NQ; ++b) { lk[b] = 0ull; thr[b] = 0ull; }
+    uint32_t nvis = 0;
+
+    for (int64_t r0 = wb; r0 < we; r0 += R) {
+        const int64_t row = r0 + g;
+        bool valid = row < we;
+        int32_t doc = 0;
+        if (valid) {
+            doc = seg.ord_to_doc ? seg.ord_to_doc[row] : (int32_t)row;
+            if (abits) valid = (abits[doc >> 6] >> (doc & 63)) & 1ull;
+        }
+        float4 xv[V];
+        const float4* xr = X + row * units;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const int f = t + j * L;
+            xv[j] = (valid && f < units) ? xr[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        float xn = 0.0f;
+        if (!L2K && sim == SIM_COSINE && valid) xn = seg.xnorm_f[row];
+        nvis += __popcll(__ballot(t == 0 && valid));
+
+#pragma unroll
+        for (int b = 0; b < NQ; ++b) {
+            float ax = 0.f, ay = 0.f, az = 0.f, aw = 0.f;
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                const float4 qv = QREG ? qf[QREG ? b : 0][QREG ? j : 0] : sq[b * UP + t + j * L];
+                if constexpr (L2K) {
+                    const float dx = xv[j].x - qv.x, dy = xv[j].y - qv.y;
+                    const float dz = xv[j].z - qv.z, dw = xv[j].w - qv.w;
+                    ax = fmaf(dx, dx, ax); ay = fmaf(dy, dy, ay);
+                    az = fmaf(dz, dz, az); aw = fmaf(dw, dw, aw);
+                } else {
+                    ax = fmaf(xv[j].x, qv.x, ax); ay = fmaf(xv[j].y, qv.y, ay);
+                    az = fmaf(xv[j].z, qv.z, az); aw = fmaf(xv[j].w, qv.w, aw);
+                }
+            }
+            float s = (ax + ay) + (az + aw);
+#pragma unroll
+            for (int m = 1; m < L; m <<= 1) s += __shfl_xor(s, m);
+            float sc;
+            if constexpr (L2K) sc = score_f32_l2(s);
+            else sc = score_f32(sim, s, qn[b], xn);
+            const uint64_t key = valid ? make_key(sc, (uint32_t)(seg.doc_base + doc)) : 0ull;
+            wave_offer(key, t == 0, lk[b], thr[b], lane, k);
+        }
+    }
+
+    if (p.visited && p.q0 == 0 && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
+
+#pragma unroll
+    for (int b = 0; b < NQ; ++b) slist[(b * 4 + wave) * 64 + lane] = lane < k ? lk[b] : 0ull;
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+        for (int b = 0; b < NQ; ++b) {
+            block_fold(slist + b * 4 * 64, lk[b], thr[b], lane, k);
+            if (b < p.q_count && lane < k)
+                p.cand[((size_t)(p.q0 + b) * p.n_tiles + blockIdx.x) * k + lane] = lk[b];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// streaming scan, int8 (exact int32 sums: Σab via v_dot4_i32_i8; d² = |q|² + |x|² − 2Σab)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int dot4_i8(int a, int b, int c) {
+    return __builtin_amdgcn_sdot4(a, b, c, false);
+}
+
+template <int L, int V, int NQ>
+__global__ __launch_bounds__(kBlock) void scan_i8(ScanParams p) {
+    constexpr int R = 64 / L;
+    constexpr int UP = L * V;
+    constexpr bool QREG = NQ * V * 4 <= 64;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    int4* sq = reinterpret_cast<int4*>(smem);
+    uint64_t* slist = reinterpret_cast<uint64_t*>(smem + (QREG ? 0 : NQ * UP * 16));
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int t = lane & (L - 1), g = lane / L;
+    const TileDev tile = p.tiles[blockIdx.x];
+    const SegDev seg = p.segs[tile.seg];
+    const int4* __restrict__ X = static_cast<const int4*>(seg.rows);
+    const int4* __restrict__ Q = static_cast<const int4*>(p.q);
+    const int units = p.units;
+
+    int4 qf[QREG ? NQ : 1][QREG ? V : 1];
+    if constexpr (QREG) {
+#pragma unroll
+        for (int b = 0; b < NQ; ++b)
+#pragma unroll
+            for (int j = 0; j < V; ++j) qf[b][j] = Q[b * UP + t + j * L];
+    } else {
+        for (int i = tid; i < NQ * UP; i += kBlock) sq[i] = Q[i];
+        __syncthreads();
+    }
+    int32_t qn[NQ];
+#pragma unroll
+    for (int b = 0; b < NQ; ++b) qn[b] = p.qnorm_i[b];
+
+    const int64_t rows = tile.row_end - tile.row_begin;
+    const int64_t per_wave = ((rows + 4 * R - 1) / (4 * R)) * R;
+    const int64_t wb = tile.row_begin + wave * per_wave;
+    const int64_t we = min(wb + per_wave, tile.row_end);
+    const uint64_t* abits = p.accept ? p.accept[tile.seg] : nullptr;
+    const int sim = p.sim, k = p.k, dim = p.dim;
+
+    uint64_t lk[NQ], thr[NQ];
+#pragma unroll
+    for (int b = 0; b < NQ; ++b) { lk[b] = 0ull; thr[b] = 0ull; }
+    uint32_t nvis = 0;
+
+    for (int64_t r0 = wb; r0 < we; r0 += R) {
+        const int64_t row = r0 + g;
+        bool valid = row < we;
+        int32_t doc = 0;
+        if (valid) {
+            doc = seg.ord_to_doc ? seg.ord_to_doc[row] : (int32_t)row;
+            if (abits) valid = (abits[doc >> 6] >> (doc & 63)) & 1ull;
+        }
+        int4 xv[V];
+        const int4* xr = X + row * units;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const int f = t + j * L;
+            xv[j] = (valid && f < units) ? xr[f] : make_int4(0, 0, 0, 0);
+        }
+        const int32_t xn = valid ? seg.xnorm_i[row] : 0;
+        nvis += __popcll(__ballot(t == 0 && valid));
+
+#pragma unroll
+        for (int b = 0; b < NQ; ++b) {
+            int acc = 0;
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                const int4 qv = QREG ? qf[QREG ? b : 0][QREG ? j : 0] : sq[b * UP + t + j * L];
+                acc = dot4_i8(xv[j].x, qv.x, acc);
+                acc = dot4_i8(xv[j].y, qv.y, acc);
+                acc = dot4_i8(xv[j].z, qv.z, acc);
+                acc = dot4_i8(xv[j].w, qv.w, acc);
+            }
+#pragma unroll
+            for (int m = 1; m < L; m <<= 1) acc += __shfl_xor(acc, m);
+            const int32_t s = sim == SIM_EUCLIDEAN ? qn[b] + xn - 2 * acc : acc;
+            const float sc = score_i8(sim, s, qn[b], xn, dim);
+            const uint64_t key = valid ? make_key(sc, (uint32_t)(seg.doc_base + doc)) : 0ull;
+            wave_offer(key, t == 0, lk[b], thr[b], lane, k);
+        }
+    }
+
+    if (p.visited && p.q0 == 0 && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
+
+#pragma unroll
+    for (int b = 0; b < NQ; ++b) slist[(b * 4 + wave) * 64 + lane] = lane < k ? lk[b] : 0ull;
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+        for (int b = 0; b < NQ; ++b) {
+            block_fold(slist + b * 4 * 64, lk[b], thr[b], lane, k);
+            if (b < p.q_count && lane < k)
+                p.cand[((size_t)(p.q0 + b) * p.n_tiles + blockIdx.x) * k + lane] = lk[b];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// dispatch tables: lane configs × NQ ∈ {1,2,4,8} × {L2, dot-family}
+// ------------------------------------------------------------------------------------------------
+int cfg_index(int units) {
+    if (units <= 8) return 0;
+    if (units <= 16) return 1;
+    if (units <= 32) return 2;
+    if (units <= 64) return 3;
+    if (units <= 128) return 4;
+    if (units <= 192) return 5;
+    if (units <= 256) return 6;
+    if (units <= 512) return 7;
+    return 8;
+}
+
+using ScanFn = void (*)(ScanParams);
+
+#define OSK_F32_ROW(L, V)                                                                        \
+    {scan_f32<L, V, 1, true>, scan_f32<L, V, 2, true>, scan_f32<L, V, 4, true>,                  \
+     scan_f32<L, V, 8, true>, scan_f32<L, V, 1, false>, scan_f32<L, V, 2, false>,                \
+     scan_f32<L, V, 4, false>, scan_f32<L, V, 8, false>}
+#define OSK_I8_ROW(L, V) {scan_i8<L, V, 1>, scan_i8<L, V, 2>, scan_i8<L, V, 4>, scan_i8<L, V, 8>}
+
+static const ScanFn kScanF32[9][8] = {
+    OSK_F32_ROW(4, 2),  OSK_F32_ROW(8, 2),  OSK_F32_ROW(8, 4),
+    OSK_F32_ROW(16, 4), OSK_F32_ROW(16, 8), OSK_F32_ROW(16, 12),
+    OSK_F32_ROW(32, 8), OSK_F32_ROW(64, 8), OSK_F32_ROW(64, 16)};
+static const ScanFn kScanI8[9][4] = {
+    OSK_I8_ROW(4, 2),  OSK_I8_ROW(8, 2),  OSK_I8_ROW(8, 4),
+    OSK_I8_ROW(16, 4), OSK_I8_ROW(16, 8), OSK_I8_ROW(16, 12),
+    OSK_I8_ROW(32, 8), OSK_I8_ROW(64, 8), OSK_I8_ROW(64, 16)};
+static const int kCfgLV[9][2] = {{4, 2}, {8, 2}, {8, 4}, {16, 4}, {16, 8}, {16, 12},
+                                 {32, 8}, {64, 8}, {64, 16}};
+
+static int nq_slot(int nq) { return nq <= 1 ? 0 : nq <= 2 ? 1 : nq <= 4 ? 2 : 3; }
+static int nq_of_slot(int s) { return 1 << s; }
+
+hipError_t launch_scan(int enc, int cfg, int nq, const ScanParams& p, hipStream_t s) {
+    const int slot = nq_slot(nq);
+    const int NQ = nq_of_slot(slot);
+    const int V = kCfgLV[cfg][1], L = kCfgLV[cfg][0];
+    const bool qreg = NQ * V * 4 <= 64;
+    const size_t lds = (qreg ? 0 : (size_t)NQ * L * V * 16) + (size_t)NQ * 4 * 64 * 8;
+    ScanFn fn;
+    if (enc == ENC_FLOAT32) {
+        const bool l2 = p.sim == SIM_EUCLIDEAN;
+        fn = kScanF32[cfg][(l2 ? 0 : 4) + slot];
+    } else {
+        fn = kScanI8[cfg][slot];
+    }
+    hipLaunchKernelGGL(fn, dim3(p.n_tiles), dim3(kBlock), lds, s, p);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// per-row |x|² in the scan's lane layout (f32) — used for COSINE rows and queries
+// ------------------------------------------------------------------------------------------------
+template <int L, int V>
+__global__ __launch_bounds__(kBlock) void row_norms_f32(const float4* __restrict__ X,
+                                                        int64_t n_rows, int units,
+                                                        float* __restrict__ out) {
+    constexpr int R = 64 / L;
+    const int lane = threadIdx.x & 63;
+    const int t = lane & (L - 1), g = lane / L;
+    const int64_t wave_global = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) >> 6;
+    for (int64_t r0 = wave_global * R; r0 < n_rows; r0 += n_waves * R) {
+        const int64_t row = r0 + g;
+        const bool valid = row < n_rows;
+        float ax = 0.f, ay = 0.f, az = 0.f, aw = 0.f;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const int f = t + j * L;
+            const float4 x = (valid && f < units) ? X[row * units + f] : make_float4(0.f, 0.f, 0.f, 0.f);
+            ax = fmaf(x.x, x.x, ax); ay = fmaf(x.y, x.y, ay);
+            az = fmaf(x.z, x.z, az); aw = fmaf(x.w, x.w, aw);
+        }
+        float s = (ax + ay) + (az + aw);
+#pragma unroll
+        for (int m = 1; m < L; m <<= 1) s += __shfl_xor(s, m);
+        if (valid && t == 0) out[row] = s;
+    }
+}
+
+using NormFn = void (*)(const float4*, int64_t, int, float*);
+static const NormFn kNormF32[9] = {row_norms_f32<4, 2>,  row_norms_f32<8, 2>,  row_norms_f32<8, 4>,
+                                   row_norms_f32<16, 4>, row_norms_f32<16, 8>, row_norms_f32<16, 12>,
+                                   row_norms_f32<32, 8>, row_norms_f32<64, 8>, row_norms_f32<64, 16>};
+
+static int grid_for(int64_t waves_needed) {
+    int64_t blocks = (waves_needed + 3) / 4;
+    if (blocks < 1) blocks = 1;
+    if (blocks > 8192) blocks = 8192;
+    return (int)blocks;
+}
+
+hipError_t launch_row_norms_f32(const float4* rows, int64_t n_rows, int units, int cfg, float* out,
+                                hipStream_t s) {
+    const int R = 64 / kCfgLV[cfg][0];
+    hipLaunchKernelGGL(kNormF32[cfg], dim3(grid_for((n_rows + R - 1) / R)), dim3(kBlock), 0, s,
+                       rows, n_rows, units, out);
+    return hipGetLastError();
+}
+
+// byte rows: Σx² exact (order irrelevant); one wave per row.
+__global__ __launch_bounds__(kBlock) void row_norms_i8(const int4* __restrict__ X, int64_t n_rows,
+                                                       int units, int32_t* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave_global = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) >> 6;
+    for (int64_t row = wave_global; row < n_rows; row += n_waves) {
+        int acc = 0;
+        for (int f = lane; f < units; f += 64) {
+            const int4 x = X[row * units + f];
+            acc = dot4_i8(x.x, x.x, acc); acc = dot4_i8(x.y, x.y, acc);
+            acc = dot4_i8(x.z, x.z, acc); acc = dot4_i8(x.w, x.w, acc);
+        }
+        for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m);
+        if (lane == 0) out[row] = acc;
+    }
+}
+
+hipError_t launch_row_norms_i8(const int4* rows, int64_t n_rows, int units, int32_t* out,
+                               hipStream_t s) {
+    hipLaunchKernelGGL(row_norms_i8, dim3(grid_for(n_rows)), dim3(kBlock), 0, s, rows, n_rows,
+                       units, out);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// synthetic corpus (one wave per row; identical values to osk_synth_host)
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void synth_rows(void* __restrict__ out, int64_t n_rows, int dim,
+                                                     int units, int enc, uint64_t seed_mix, int dist,
+                                                     int64_t row0) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave_global = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) >> 6;
+    for (int64_t r = wave_global; r < n_rows; r += n_waves) {
+        const uint64_t grow = (uint64_t)(row0 + r);
+        if (enc == ENC_BYTE) {
+            int8_t* orow = static_cast<int8_t*>(out) + r * (int64_t)units * 16;
+            for (int f = lane; f < units; f += 64) {
+                alignas(16) int8_t v[16];
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int c = f * 16 + e;
+                    v[e] = c < dim ? synth_i8(synth_bits(seed_mix, grow, dim, c)) : (int8_t)0;
+                }
+                *reinterpret_cast<int4*>(orow + f * 16) = *reinterpret_cast<const int4*>(v);
+            }
+            continue;
+        }
+        float inv_norm_den = 1.0f;
+        if (dist == DIST_NORMALISH_UNIT) {
+            float acc = 0.0f;
+            for (int c = lane; c < dim; c += 64) {
+                const float z = synth_f32_raw(dist, synth_bits(seed_mix, grow, dim, c));
+                acc = fmaf(z, z, acc);
+            }
+            for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m);
+            inv_norm_den = sqrtf(acc);
+        }
+        float4* orow = static_cast<float4*>(out) + r * (int64_t)units;
+        for (int f = lane; f < units; f += 64) {
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int c = f * 4 + e;
+                float z = c < dim ? synth_f32_raw(dist, synth_bits(seed_mix, grow, dim, c)) : 0.0f;
+                if (dist == DIST_NORMALISH_UNIT && c < dim) z = z / inv_norm_den;
+                v[e] = z;
+            }
+            orow[f] = make_float4(v[0], v[1], v[2], v[3]);
+        }
+    }
+}
+
+hipError_t launch_synth(void* rows, int64_t n_rows, int dim, int units, int enc, uint64_t seed,
+                        int dist, int64_t row0, hipStream_t s) {
+    hipLaunchKernelGGL(synth_rows, dim3(grid_for(n_rows)), dim3(kBlock), 0, s, rows, n_rows, dim,
+                       units, enc, splitmix64(seed), dist, row0);
+    return hipGetLastError();
+}
+
+// copy rows into the padded (16-byte unit) layout; pad bytes are zeroed.
+__global__ __launch_bounds__(kBlock) void pad_rows(const uint8_t* __restrict__ src, int64_t src_pitch,
+                                                   uint8_t* __restrict__ dst, int64_t dst_pitch,
+                                                   int64_t n_rows, int64_t row_bytes) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave_global = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) >> 6;
+    for (int64_t r = wave_global; r < n_rows; r += n_waves)
+        for (int64_t b = lane; b < dst_pitch; b += 64)
+            dst[r * dst_pitch + b] = b < row_bytes ? src[r * src_pitch + b] : (uint8_t)0;
+}
+
+hipError_t launch_pad_rows(const void* src, int64_t src_pitch, void* dst, int64_t dst_pitch,
+                           int64_t n_rows, int64_t row_bytes, hipStream_t s) {
+    hipLaunchKernelGGL(pad_rows, dim3(grid_for(n_rows)), dim3(kBlock), 0, s,
+                       static_cast<const uint8_t*>(src), src_pitch, static_cast<uint8_t*>(dst),
+                       dst_pitch, n_rows, row_bytes);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// per-shard top-k from per-tile lists: one workgroup per (shard, query)
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void merge_shards(const uint64_t* __restrict__ cand, int n_tiles,
+                                                       const int32_t* __restrict__ shard_tile_begin,
+                                                       int n_shards, int k,
+                                                       uint64_t* __restrict__ shard_keys,
+                                                       int32_t* __restrict__ shard_counts) {
+    __shared__ uint64_t lists[4 * 64];
+    const int s = blockIdx.x, b = blockIdx.y;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int t0 = shard_tile_begin[s], t1 = shard_tile_begin[s + 1];
+    const uint64_t* c = cand + ((size_t)b * n_tiles + t0) * k;
+    const int64_t n = (int64_t)(t1 - t0) * k;
+    uint64_t lk = 0ull, thr = 0ull;
+    for (int64_t base = (int64_t)wave * 64; base < n; base += kBlock) {
+        const int64_t i = base + lane;
+        const uint64_t key = i < n ? c[i] : 0ull;
+        wave_offer(key, true, lk, thr, lane, k);
+    }
+    lists[wave * 64 + lane] = lane < k ? lk : 0ull;
+    __syncthreads();
+    if (wave == 0) {
+        block_fold(lists, lk, thr, lane, k);
+        const size_t o = (size_t)b * n_shards + s;
+        if (lane < k) shard_keys[o * k + lane] = lk;
+        const int cnt = __popcll(__ballot(lane < k && lk != 0ull));
+        if (lane == 0) shard_counts[o] = cnt;
+    }
+}
+
+hipError_t launch_merge_shards(const uint64_t* cand, int n_tiles, const int32_t* shard_tile_begin,
+                               int n_shards, int nq, int k, uint64_t* shard_keys,
+                               int32_t* shard_counts, hipStream_t s) {
+    hipLaunchKernelGGL(merge_shards, dim3(n_shards, nq), dim3(kBlock), 0, s, cand, n_tiles,
+                       shard_tile_begin, n_shards, k, shard_keys, shard_counts);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// coordinator reduce: one workgroup per query.  Each shard contributes its first min(k, from+size)
+// hits (the shard collector's numDocs cut); hits are ranked by (score desc, shardIndex asc, doc asc)
+// and ranks [from, from+size) are emitted.  Σ shard hits → total hits; max top score → max score.
+// ------------------------------------------------------------------------------------------------
+constexpr int kCoordMax = 4096;   // shard hits considered per query
+
+__global__ __launch_bounds__(kBlock) void merge_coord(const uint64_t* __restrict__ shard_keys,
+                                                      const int32_t* __restrict__ shard_counts,
+                                                      const int32_t* __restrict__ shard_index,
+                                                      int n_shards, int k, int from, int size,
+                                                      float* __restrict__ scores,
+                                                      int32_t* __restrict__ docs,
+                                                      int32_t* __restrict__ shard_out,
+                                                      int32_t* __restrict__ count,
+                                                      int64_t* __restrict__ total_hits,
+                                                      float* __restrict__ max_score) {
+    __shared__ uint32_t s_su[kCoordMax];
+    __shared__ int32_t s_sidx[kCoordMax];
+    __shared__ int32_t s_doc[kCoordMax];
+    __shared__ int32_t s_n;
+    __shared__ unsigned long long s_total;
+    __shared__ uint32_t s_max;
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const int topn = min(k, from + size);
+    if (tid == 0) { s_n = 0; s_total = 0ull; s_max = 0u; }
+    __syncthreads();
+    for (int s = tid; s < n_shards; s += kBlock) {
+        const int c = shard_counts[(size_t)b * n_shards + s];
+        atomicAdd(&s_total, (unsigned long long)c);
+        if (c > 0) atomicMax(&s_max, (uint32_t)(shard_keys[((size_t)b * n_shards + s) * k] >> 32));
+    }
+    for (int s = 0; s < n_shards; ++s) {   // append in shard order (deterministic slots)
+        const int c = min(shard_counts[(size_t)b * n_shards + s], topn);
+        const int base = s_n;
+        for (int i = tid; i < c; i += kBlock) {
+            const int slot = base + i;
+            if (slot < kCoordMax) {
+                const uint64_t key = shard_keys[((size_t)b * n_shards + s) * k + i];
+                s_su[slot] = (uint32_t)(key >> 32);
+                s_sidx[slot] = shard_index[s];
+                s_doc[slot] = key_doc(key);
+            }
+        }
+        __syncthreads();
+        if (tid == 0) s_n = min(base + c, kCoordMax);
+        __syncthreads();
+    }
+    const int n = s_n;
+    for (int i = tid; i < n; i += kBlock) {
+        const uint32_t su = s_su[i];
+        const int32_t si = s_sidx[i], d = s_doc[i];
+        int rank = 0;
+        for (int j = 0; j < n; ++j) {
+            const uint32_t sj = s_su[j];
+            rank += (sj > su) || (sj == su && (s_sidx[j] < si || (s_sidx[j] == si && s_doc[j] < d)));
+        }
+        if (rank >= from && rank < from + size) {
+            const size_t o = (size_t)b * size + (rank - from);
+            scores[o] = sortable_to_float(su);
+            docs[o] = d;
+            shard_out[o] = si;
+        }
+    }
+    const int got = max(0, min(size, n - from));
+    for (int r = got + tid; r < size; r += kBlock) {
+        const size_t o = (size_t)b * size + r;
+        scores[o] = -__builtin_inff();
+        docs[o] = 0x7FFFFFFF;
+        shard_out[o] = -1;
+    }
+    if (tid == 0) {
+        count[b] = got;
+        total_hits[b] = (int64_t)s_total;
+        max_score[b] = s_total > 0 ? sortable_to_float(s_max) : __builtin_nanf("");
+    }
+}
+
+hipError_t launch_merge_coord(const uint64_t* shard_keys, const int32_t* shard_counts,
+                              const int32_t* shard_index, int nq, int n_shards, int k, int from,
+                              int size, float* scores, int32_t* docs, int32_t* shard_out,
+                              int32_t* count, int64_t* total_hits, float* max_score,
+                              hipStream_t s) {
+    hipLaunchKernelGGL(merge_coord, dim3(nq), dim3(kBlock), 0, s, shard_keys, shard_counts,
+                       shard_index, n_shards, k, from, size, scores, docs, shard_out, count,
+                       total_hits, max_score);
+    return hipGetLastError();
+}
+
+}  // namespace osk
