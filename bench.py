@@ -47,6 +47,20 @@ DIM = 768
 K = 10
 FROM, SIZE = 0, 10
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md; 6.29 TB/s measured float4 copy)
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_traffic_c3_b1.json")
+
+
+def pmc_traffic(rows_local: int, batch: int):
+    """HBM bytes per scan launch from the committed rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes of this
+    same command (tools/pmc_traffic.py; gfx950 ×2 FETCH correction applied), scaled to this rank's rows.
+    The passes were taken at N=1 (10M rows, batch 1).  None when absent or for another batch size."""
+    if batch != 1 or not os.path.exists(PMC_SUMMARY):
+        return None, None
+    data = json.load(open(PMC_SUMMARY))
+    for name, v in data.items():
+        if "scan_f32<16, 12, 1, false" in name:
+            return v["hbm_bytes"] * rows_local / (N_SHARDS * ROWS_PER_SHARD), os.path.relpath(PMC_SUMMARY, ROOT)
+    return None, None
 
 
 def log(*a):
@@ -158,6 +172,7 @@ def main():
     bytes_per_launch = rows_local * DIM * 4 * passes
     achieved = bytes_per_launch / (scan_avg_ms * 1e-3) / 1e9
 
+    traffic, traffic_src = pmc_traffic(rows_local, B)
     if rank == 0:
         res = {
             "metric": "exact k-NN QPS@k=10 (recall=1.0), 10M×768 fp32, 1/2/4/8 GPUs; % HBM roofline",
@@ -176,7 +191,7 @@ def main():
                        "batch": B, "rows": N_SHARDS * a.rows_per_shard, "dim": DIM, "shards": N_SHARDS,
                        "parallelism": f"shards over {world} GPU(s), RCCL all-gather + device merge"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "scan_f32<L=16,V=12,NQ=1,dot> (+shard merge excluded)",
                          "scan_ms_avg": scan_avg_ms, "algorithmic_bytes_per_launch": bytes_per_launch},
             "gpu_event_ms_per_step": ev_ms / a.steps,

@@ -166,6 +166,10 @@ int32_t osk_merge_device(int32_t device, const uint64_t* d_shard_keys,
 int32_t osk_view_profile(osk_view* view, int32_t enable);
 int32_t osk_view_scan_time(osk_view* view, double* total_ms, int64_t* calls);
 
+/* Process-wide tuning knobs for benchmarks / A-B runs ("scan_nt": 0|1 non-temporal corpus loads;
+ * "tiles_target": workgroup tiles per view, applied at osk_view_create). */
+int32_t osk_tune_set(const char* key, int64_t value);
+
 /* Host-buffer convenience: shard search + coordinator merge on one device, synchronous.
  * accept: NULL or n_segs host pointers (each NULL or a host bitset). */
 int32_t osk_view_search(osk_view* view, const void* queries, int32_t n_queries, int32_t k,

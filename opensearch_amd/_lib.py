@@ -63,6 +63,7 @@ SIGNATURES = {
     "osk_topdocs_merge": (_I32, [_I32, _P, _P, _P, _I32, _P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     "osk_decode_keys": (_I32, [_P, _I64, _P, _P]),
     "osk_view_profile": (_I32, [_P, _I32]),
+    "osk_tune_set": (_I32, [C.c_char_p, _I64]),
     "osk_view_scan_time": (_I32, [_P, C.POINTER(C.c_double), _PI64]),
 }
 

@@ -280,6 +280,22 @@ extern "C" {
 
 int32_t osk_abi_version(void) { return OSK_ABI_VERSION; }
 
+int32_t osk_tune_set(const char* key, int64_t value) {
+    OSK_GUARD_BEGIN
+    OSK_REQUIRE(key != nullptr, "key is null");
+    const std::string k(key);
+    if (k == "scan_nt") g_tuning.scan_nt = value != 0;
+    else if (k == "tiles_target") {
+        OSK_REQUIRE(value >= 1 && value <= (1 << 22), "tiles_target out of range");
+        g_tuning.tiles_target = (int)value;
+    } else {
+        set_error("unknown tuning key: " + k);
+        return OSK_ERR_INVALID;
+    }
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
 int32_t osk_device_count(int32_t* n) {
     OSK_GUARD_BEGIN
     OSK_REQUIRE(n != nullptr, "n is null");
@@ -421,7 +437,7 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
     int64_t total = 0;
     for (int i = 0; i < n_segs; ++i) total += segs[i]->n_rows;
     const int64_t min_rows = 4LL * R * 8;
-    const int64_t target = 2048;
+    const int64_t target = std::max(1, g_tuning.tiles_target);
     const int64_t rows_per_tile = std::max<int64_t>(min_rows, (total + target - 1) / target);
     std::vector<TileDev> tiles;
     v->shard_tile_begin.assign(n_shards + 1, 0);

@@ -47,7 +47,14 @@ struct ScanParams {
 constexpr int kBlock = 256;          // 4 wavefronts per workgroup
 constexpr int kMaxNQ = 8;            // queries per streaming-scan launch
 
-int cfg_index(int units);            // index into the lane-config table (0..8)
+int cfg_index(int units);
+
+// Process-wide tuning knobs (osk_tune_set; benchmarks and A/B runs only).
+struct Tuning {
+    int scan_nt = 1;          // non-temporal corpus loads in scan_f32 (+4% HBM rate, profiles/r01_scan_ab.txt)
+    int tiles_target = 4096;  // workgroup tiles per view (scan grid size)
+};
+extern Tuning g_tuning;
 
 hipError_t launch_scan(int enc, int cfg, int nq, const ScanParams& p, hipStream_t s);
 hipError_t launch_row_norms_f32(const float4* rows, int64_t n_rows, int units, int cfg,

@@ -72,7 +72,20 @@ __device__ __forceinline__ void block_fold(const uint64_t* lists /*[4][64]*/, ui
 // ------------------------------------------------------------------------------------------------
 // streaming scan, float32
 // ------------------------------------------------------------------------------------------------
-template <int L, int V, int NQ, bool L2K>
+// NT: corpus loads carry the non-temporal hint (global_load_dwordx4 … nt): every corpus byte is read
+// exactly once per launch, so there is nothing to gain from keeping it in L2 / the Infinity Cache.
+template <bool NT>
+__device__ __forceinline__ float4 load_row4(const float4* p) {
+    if constexpr (NT) {
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+        return make_float4(v.x, v.y, v.z, v.w);
+    } else {
+        return *p;
+    }
+}
+
+template <int L, int V, int NQ, bool L2K, bool NT>
 __global__ __launch_bounds__(kBlock) void scan_f32(ScanParams p) {
     constexpr int R = 64 / L;                 // rows per wave-iteration
     constexpr int UP = L * V;                 // padded float4s per query
@@ -128,7 +141,7 @@ __global__ __launch_bounds__(kBlock) void scan_f32(ScanParams p) {
 #pragma unroll
         for (int j = 0; j < V; ++j) {
             const int f = t + j * L;
-            xv[j] = (valid && f < units) ? xr[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+            xv[j] = (valid && f < units) ? load_row4<NT>(xr + f) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
         float xn = 0.0f;
         if (!L2K && sim == SIM_COSINE && valid) xn = seg.xnorm_f[row];
@@ -296,13 +309,14 @@ int cfg_index(int units) {
 
 using ScanFn = void (*)(ScanParams);
 
-#define OSK_F32_ROW(L, V)                                                                        \
-    {scan_f32<L, V, 1, true>, scan_f32<L, V, 2, true>, scan_f32<L, V, 4, true>,                  \
-     scan_f32<L, V, 8, true>, scan_f32<L, V, 1, false>, scan_f32<L, V, 2, false>,                \
-     scan_f32<L, V, 4, false>, scan_f32<L, V, 8, false>}
+#define OSK_F32_ROW_NT(L, V, NT)                                                                 \
+    scan_f32<L, V, 1, true, NT>, scan_f32<L, V, 2, true, NT>, scan_f32<L, V, 4, true, NT>,         \
+        scan_f32<L, V, 8, true, NT>, scan_f32<L, V, 1, false, NT>, scan_f32<L, V, 2, false, NT>,   \
+        scan_f32<L, V, 4, false, NT>, scan_f32<L, V, 8, false, NT>
+#define OSK_F32_ROW(L, V) {OSK_F32_ROW_NT(L, V, false), OSK_F32_ROW_NT(L, V, true)}
 #define OSK_I8_ROW(L, V) {scan_i8<L, V, 1>, scan_i8<L, V, 2>, scan_i8<L, V, 4>, scan_i8<L, V, 8>}
 
-static const ScanFn kScanF32[9][8] = {
+static const ScanFn kScanF32[9][16] = {
     OSK_F32_ROW(4, 2),  OSK_F32_ROW(8, 2),  OSK_F32_ROW(8, 4),
     OSK_F32_ROW(16, 4), OSK_F32_ROW(16, 8), OSK_F32_ROW(16, 12),
     OSK_F32_ROW(32, 8), OSK_F32_ROW(64, 8), OSK_F32_ROW(64, 16)};
@@ -316,6 +330,8 @@ static const int kCfgLV[9][2] = {{4, 2}, {8, 2}, {8, 4}, {16, 4}, {16, 8}, {16, 
 static int nq_slot(int nq) { return nq <= 1 ? 0 : nq <= 2 ? 1 : nq <= 4 ? 2 : 3; }
 static int nq_of_slot(int s) { return 1 << s; }
 
+Tuning g_tuning;
+
 hipError_t launch_scan(int enc, int cfg, int nq, const ScanParams& p, hipStream_t s) {
     const int slot = nq_slot(nq);
     const int NQ = nq_of_slot(slot);
@@ -325,7 +341,7 @@ hipError_t launch_scan(int enc, int cfg, int nq, const ScanParams& p, hipStream_
     ScanFn fn;
     if (enc == ENC_FLOAT32) {
         const bool l2 = p.sim == SIM_EUCLIDEAN;
-        fn = kScanF32[cfg][(l2 ? 0 : 4) + slot];
+        fn = kScanF32[cfg][(g_tuning.scan_nt ? 8 : 0) + (l2 ? 0 : 4) + slot];
     } else {
         fn = kScanI8[cfg][slot];
     }
