@@ -168,9 +168,13 @@ def main():
     assert np.all(cnt == SIZE), cnt
 
     scan_avg_ms = scan_ms.value / max(1, calls.value)
-    passes = (B + 7) // 8
+    batched = B >= 16 and K <= 12           # the library's batched MFMA path (osk_tune "mfma_min_batch")
+    passes = (B + 255) // 256 if batched else (B + 7) // 8
     bytes_per_launch = rows_local * DIM * 4 * passes
     achieved = bytes_per_launch / (scan_avg_ms * 1e-3) / 1e9
+    kernel_name = ("mfma_cand (bf16x3 split MFMA candidates; bytes = the hi/lo copy read once per 256 queries)"
+                   if batched else "scan_f32<L=16,V=12,NQ=min(B,8),dot,nt>")
+    mfma_tflops = (3 * 2 * B * rows_local * DIM) / (scan_avg_ms * 1e-3) / 1e12 if batched else None
 
     traffic, traffic_src = pmc_traffic(rows_local, B)
     if rank == 0:
@@ -192,8 +196,9 @@ def main():
                        "parallelism": f"shards over {world} GPU(s), RCCL all-gather + device merge"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "scan_f32<L=16,V=12,NQ=1,dot> (+shard merge excluded)",
-                         "scan_ms_avg": scan_avg_ms, "algorithmic_bytes_per_launch": bytes_per_launch},
+                         "kernel": kernel_name, "scan_ms_avg": scan_avg_ms,
+                         "algorithmic_bytes_per_launch": bytes_per_launch,
+                         "bf16_mfma_tflops": mfma_tflops},
             "gpu_event_ms_per_step": ev_ms / a.steps,
         }
         if world == 1 and not a.no_cpu_baseline:

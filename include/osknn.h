@@ -166,9 +166,20 @@ int32_t osk_merge_device(int32_t device, const uint64_t* d_shard_keys,
 int32_t osk_view_profile(osk_view* view, int32_t enable);
 int32_t osk_view_scan_time(osk_view* view, double* total_ms, int64_t* calls);
 
-/* Process-wide tuning knobs for benchmarks / A-B runs ("scan_nt": 0|1 non-temporal corpus loads;
- * "tiles_target": workgroup tiles per view, applied at osk_view_create). */
+/* Process-wide tuning knobs for benchmarks / A-B runs:
+ *   "scan_nt"         0|1 non-temporal corpus loads in the streaming scan (default 1)
+ *   "tiles_target"    workgroup tiles per view for the streaming scan (default 4096; at view create)
+ *   "mfma_min_batch"  batches of at least this many float32 queries (and k ≤ 12) take the batched
+ *                     MFMA path (default 16; 0 = never)
+ *   "mfma_units"      workgroup units of the MFMA candidate pass per view (default 512) */
 int32_t osk_tune_set(const char* key, int64_t value);
+
+/* Batched-path counters of a view: searches that took the MFMA path, and queries among them whose
+ * certificate failed and were recomputed by the exact streaming scan. */
+int32_t osk_view_stats(osk_view* view, int64_t* batched_calls, int64_t* fallback_queries);
+/* Tests / debugging only: copy `bytes` of an internal buffer of the view's last search
+ * ("akeys", "cand_a", "flags", "qsplit", "qnorm") to host memory. */
+int32_t osk_view_debug_copy(osk_view* view, const char* name, void* host, int64_t bytes);
 
 /* Host-buffer convenience: shard search + coordinator merge on one device, synchronous.
  * accept: NULL or n_segs host pointers (each NULL or a host bitset). */

@@ -64,6 +64,8 @@ SIGNATURES = {
     "osk_decode_keys": (_I32, [_P, _I64, _P, _P]),
     "osk_view_profile": (_I32, [_P, _I32]),
     "osk_tune_set": (_I32, [C.c_char_p, _I64]),
+    "osk_view_stats": (_I32, [_P, _PI64, _PI64]),
+    "osk_view_debug_copy": (_I32, [_P, C.c_char_p, _P, _I64]),
     "osk_view_scan_time": (_I32, [_P, C.POINTER(C.c_double), _PI64]),
 }
 
@@ -110,6 +112,11 @@ def ptr(a) -> int | None:
     if a is None:
         return None
     return a.ctypes.data
+
+
+def tune(key: str, value: int) -> None:
+    """Process-wide tuning knob (osk_tune_set): scan_nt, tiles_target, mfma_min_batch, mfma_units."""
+    check(lib().osk_tune_set(key.encode(), int(value)))
 
 
 def device_count() -> int:

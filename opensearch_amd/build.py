@@ -22,7 +22,7 @@ INCLUDE = ROOT / "include"
 LIB = PKG / "libosknn.so"
 OBJDIR = ROOT / "build" / "osknn"
 
-SOURCES = ["osk_kernels.hip", "osk_api.hip", "osk_host.cpp"]
+SOURCES = ["osk_kernels.hip", "osk_mfma.hip", "osk_api.hip", "osk_host.cpp"]
 HEADERS = ["osk_common.h", "osk_internal.h"]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -172,6 +172,12 @@ struct osk_seg {
     float* d_xnorm_f = nullptr;
     int32_t* d_xnorm_i = nullptr;
     int32_t* d_ord_to_doc = nullptr;
+    // batched MFMA path (built on first batched search): bf16 hi/lo copy in MFMA fragment order,
+    // |x|² per row (device lane order) and max |x|² of the segment
+    void* d_split = nullptr;
+    int split_KS = 0;
+    unsigned* d_maxnorm2 = nullptr;
+    float h_maxnorm2 = 0.0f;
     std::mutex mu;
     osk_view* self_view = nullptr;   // single-segment view behind osk_seg_search
     ~osk_seg();
@@ -180,6 +186,7 @@ struct osk_seg {
 struct osk_view {
     int device = 0, dim = 0, enc = 0, sim = 0, units = 0, cfg = 0;
     std::vector<osk_seg*> segs;
+    std::vector<int32_t> seg_shard, seg_doc_base;
     int n_shards = 0;
     std::vector<int32_t> shard_index;
     std::vector<int32_t> shard_tile_begin;
@@ -189,6 +196,15 @@ struct osk_view {
     DevBuf ws_cand, ws_q, ws_qnorm, ws_qin, ws_keys, ws_counts, ws_accept_ptrs, ws_accept,
         ws_out, ws_visited;
     HostPinned h_stage;
+    // batched MFMA path
+    bool mfma_ready = false;
+    int n_munits = 0;
+    int mfma_KS = 0;
+    double mfma_c = 0.0;
+    DevBuf d_munits, d_seg_split, d_seg_vrow, d_shard_unit_begin, d_shard_maxnorm2;
+    DevBuf ws_qsplit, ws_cand_a, ws_akeys, ws_acounts, ws_flags, ws_fbq, ws_fbkeys, ws_fbcounts;
+    HostPinned h_flags;
+    int64_t mfma_calls = 0, mfma_fallback_queries = 0;
     std::mutex mu;
     // scan-kernel timing (osk_view_profile): events bracket the scan launches on the search stream
     bool profile = false;
@@ -202,12 +218,25 @@ struct osk_view {
     }
 };
 
+// The device view of a view's segments (pointers re-read: staging may add row norms later).
+static std::vector<SegDev> seg_devs(const osk_view* v) {
+    std::vector<SegDev> sd(v->segs.size());
+    for (size_t i = 0; i < v->segs.size(); ++i) {
+        const osk_seg* s = v->segs[i];
+        sd[i] = SegDev{s->d_rows, s->d_xnorm_f, s->d_xnorm_i, s->d_ord_to_doc, s->n_rows,
+                       v->seg_doc_base[i], v->seg_shard[i]};
+    }
+    return sd;
+}
+
 osk_seg::~osk_seg() {
     if (self_view) delete self_view;
     if (d_rows) (void)hipFree(d_rows);
     if (d_xnorm_f) (void)hipFree(d_xnorm_f);
     if (d_xnorm_i) (void)hipFree(d_xnorm_i);
     if (d_ord_to_doc) (void)hipFree(d_ord_to_doc);
+    if (d_split) (void)hipFree(d_split);
+    if (d_maxnorm2) (void)hipFree(d_maxnorm2);
 }
 
 namespace {
@@ -285,7 +314,15 @@ int32_t osk_tune_set(const char* key, int64_t value) {
     OSK_REQUIRE(key != nullptr, "key is null");
     const std::string k(key);
     if (k == "scan_nt") g_tuning.scan_nt = value != 0;
-    else if (k == "tiles_target") {
+    else if (k == "mfma_min_batch") {
+        OSK_REQUIRE(value >= 0, "mfma_min_batch must be >= 0");
+        g_tuning.mfma_min_batch = (int)value;
+    } else if (k == "mfma_ablate") {
+        g_tuning.mfma_ablate = (int)value;
+    } else if (k == "mfma_units") {
+        OSK_REQUIRE(value >= 1 && value <= 32768, "mfma_units out of range");
+        g_tuning.mfma_units = (int)value;
+    } else if (k == "tiles_target") {
         OSK_REQUIRE(value >= 1 && value <= (1 << 22), "tiles_target out of range");
         g_tuning.tiles_target = (int)value;
     } else {
@@ -427,6 +464,8 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
     v->units = s0->units;
     v->cfg = s0->cfg;
     v->segs.assign(segs, segs + n_segs);
+    v->seg_shard.resize(n_segs);
+    for (int i = 0; i < n_segs; ++i) v->seg_shard[i] = seg_shard ? seg_shard[i] : 0;
     v->n_shards = n_shards;
     v->shard_index.resize(n_shards);
     for (int s = 0; s < n_shards; ++s) v->shard_index[s] = shard_index ? shard_index[s] : s;
@@ -457,12 +496,9 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
     v->n_tiles = (int)tiles.size();
     OSK_REQUIRE(v->n_tiles < (1 << 24), "too many tiles");
 
-    std::vector<SegDev> sd(n_segs);
-    for (int i = 0; i < n_segs; ++i) {
-        const osk_seg* s = segs[i];
-        sd[i] = SegDev{s->d_rows, s->d_xnorm_f, s->d_xnorm_i, s->d_ord_to_doc, s->n_rows,
-                       seg_doc_base ? seg_doc_base[i] : 0, seg_shard ? seg_shard[i] : 0};
-    }
+    v->seg_doc_base.resize(n_segs);
+    for (int i = 0; i < n_segs; ++i) v->seg_doc_base[i] = seg_doc_base ? seg_doc_base[i] : 0;
+    std::vector<SegDev> sd = seg_devs(v.get());
     hipStream_t st = device_stream(v->device);
     OSK_HIP(v->d_segs.reserve(sizeof(SegDev) * n_segs));
     OSK_HIP(v->d_tiles.reserve(sizeof(TileDev) * std::max<size_t>(1, tiles.size())));
@@ -494,6 +530,245 @@ int32_t osk_view_release(osk_view* view) {
 }  // extern "C"
 
 namespace {
+
+int32_t profile_begin(osk_view* v, hipStream_t st) {
+    if (v->pending) {   // fold the previous call's interval (already complete or we wait)
+        float ms = 0.f;
+        OSK_HIP(hipEventSynchronize(v->ev1));
+        OSK_HIP(hipEventElapsedTime(&ms, v->ev0, v->ev1));
+        v->scan_ms += ms;
+        v->scan_calls += 1;
+        v->pending = false;
+    }
+    OSK_HIP(hipEventRecord(v->ev0, st));
+    return OSK_OK;
+}
+
+int32_t profile_end(osk_view* v, hipStream_t st) {
+    if (!v->profile) return OSK_OK;
+    OSK_HIP(hipEventRecord(v->ev1, st));
+    v->pending = true;
+    return OSK_OK;
+}
+
+// Streaming exact scan of queries already in the padded unit layout (≤ 8 per launch) + per-shard merge.
+int32_t stream_search(osk_view* v, const void* qpad, const void* qnorm, int nq, int k, int UP,
+                      const uint64_t* const* d_accept, uint64_t* d_shard_keys, int32_t* d_shard_counts,
+                      int64_t* d_visited, hipStream_t st) {
+    OSK_HIP(v->ws_cand.reserve(sizeof(uint64_t) * (size_t)nq * v->n_tiles * k));
+    ScanParams p{};
+    p.segs = v->d_segs.as<SegDev>();
+    p.tiles = v->d_tiles.as<TileDev>();
+    p.accept = d_accept;
+    p.cand = v->ws_cand.as<uint64_t>();
+    p.visited = reinterpret_cast<unsigned long long*>(d_visited);
+    p.n_tiles = v->n_tiles;
+    p.units = v->units;
+    p.k = k;
+    p.sim = v->sim;
+    p.dim = v->dim;
+    for (int q0 = 0; q0 < nq; q0 += kMaxNQ) {
+        const int qc = std::min(kMaxNQ, nq - q0);
+        p.q0 = q0;
+        p.q_count = qc;
+        p.q = static_cast<const char*>(qpad) + (size_t)q0 * UP * 16;
+        p.qnorm_f = static_cast<const float*>(qnorm) + q0;
+        p.qnorm_i = static_cast<const int32_t*>(qnorm) + q0;
+        OSK_HIP(launch_scan(v->enc, v->cfg, qc, p, st));
+    }
+    int32_t rc = profile_end(v, st);
+    if (rc) return rc;
+    OSK_HIP(launch_merge_shards(v->ws_cand.as<uint64_t>(), v->n_tiles,
+                                v->d_shard_tile_begin.as<int32_t>(), v->n_shards, nq, k,
+                                d_shard_keys, d_shard_counts, st));
+    return OSK_OK;
+}
+
+// The segment's bf16 hi/lo copy in MFMA fragment order (+ |x|² rows and their max).  Built once.
+int32_t ensure_split(osk_seg* s, hipStream_t st) {
+    std::lock_guard<std::mutex> lk(s->mu);
+    if (s->d_split) return OSK_OK;
+    const int KS = (s->units + 7) / 8;                      // 32-dim K-steps
+    const int64_t n_tiles = (s->n_rows + 127) / 128;        // 128-row tiles
+    const int64_t n_rb = std::max<int64_t>(1, n_tiles) * 8;
+    if (!s->d_xnorm_f) {
+        OSK_HIP(hipMalloc(&s->d_xnorm_f, std::max<int64_t>(1, s->n_rows) * sizeof(float)));
+        if (s->n_rows > 0)
+            OSK_HIP(launch_row_norms_f32(static_cast<const float4*>(s->d_rows), s->n_rows, s->units, s->cfg,
+                                         s->d_xnorm_f, st));
+    }
+    void* split = nullptr;
+    hipError_t e = hipMalloc(&split, (size_t)n_rb * KS * 2 * 1024);
+    if (e != hipSuccess) {
+        set_error(std::string("hipMalloc of the MFMA split copy failed: ") + hipGetErrorString(e));
+        return OSK_ERR_OOM;
+    }
+    OSK_HIP(launch_split_rows(static_cast<const float4*>(s->d_rows), s->n_rows, s->units, KS, n_rb, split, st));
+    OSK_HIP(hipMalloc(&s->d_maxnorm2, sizeof(unsigned)));
+    OSK_HIP(hipMemsetAsync(s->d_maxnorm2, 0, sizeof(unsigned), st));
+    if (s->n_rows > 0) OSK_HIP(launch_max_norm2(s->d_xnorm_f, s->n_rows, s->d_maxnorm2, st));
+    unsigned bits = 0;
+    OSK_HIP(hipMemcpyAsync(&bits, s->d_maxnorm2, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    OSK_HIP(hipStreamSynchronize(st));
+    std::memcpy(&s->h_maxnorm2, &bits, 4);
+    s->d_split = split;
+    s->split_KS = KS;
+    return OSK_OK;
+}
+
+// MFMA work units (runs of 128-row tiles, contiguous per shard) and per-shard bounds.  Built once.
+int32_t ensure_mfma(osk_view* v, hipStream_t st) {
+    if (v->mfma_ready) return OSK_OK;
+    const int ns = (int)v->segs.size();
+    std::vector<const void*> splits(ns);
+    std::vector<int64_t> vrow(ns);
+    int64_t acc = 0, total_tiles = 0;
+    for (int i = 0; i < ns; ++i) {
+        int32_t rc = ensure_split(v->segs[i], st);
+        if (rc) return rc;
+        splits[i] = v->segs[i]->d_split;
+        vrow[i] = acc;
+        acc += v->segs[i]->n_rows;
+        total_tiles += (v->segs[i]->n_rows + 127) / 128;
+    }
+    OSK_REQUIRE(acc < 0xFFFFFFFFll, "a view holds < 2^32 rows");
+    {   // ensure_split may have added row norms: refresh the device segment table
+        const std::vector<SegDev> sd = seg_devs(v);
+        OSK_HIP(hipMemcpyAsync(v->d_segs.p, sd.data(), sizeof(SegDev) * sd.size(), hipMemcpyHostToDevice, st));
+    }
+    const int64_t target = std::max(1, g_tuning.mfma_units);
+    const int64_t per = std::max<int64_t>(1, (total_tiles + target - 1) / target);
+    std::vector<MfmaUnit> units;
+    std::vector<int32_t> shard_list_begin(v->n_shards + 1, 0);
+    std::vector<float> shard_max(v->n_shards, 0.0f);
+    for (int sh = 0; sh < v->n_shards; ++sh) {
+        shard_list_begin[sh] = (int32_t)units.size() * 2;
+        for (int i = 0; i < ns; ++i) {
+            if (v->seg_shard[i] != sh) continue;
+            shard_max[sh] = std::max(shard_max[sh], v->segs[i]->h_maxnorm2);
+            const int64_t nt = (v->segs[i]->n_rows + 127) / 128;
+            for (int64_t t = 0; t < nt; t += per)
+                units.push_back(MfmaUnit{i, sh, t, std::min(nt, t + per), vrow[i]});
+        }
+    }
+    shard_list_begin[v->n_shards] = (int32_t)units.size() * 2;
+    v->n_munits = (int)units.size();
+    OSK_REQUIRE(v->n_munits > 0 && v->n_munits < 65536, "bad MFMA unit count");
+    v->mfma_KS = (v->units + 7) / 8;
+    // |Σ approx − Σ device order| ≤ c·|x||q|: bf16 split (3·2^-16) + fp32 accumulation of the
+    // 3·Kpad MFMA products and of the Kpad device-order products (γ_n ≈ n·2^-24), ×1.5 margin.
+    const double kpad = 32.0 * v->mfma_KS;
+    v->mfma_c = 1.5 * (3.0 * std::ldexp(1.0, -16) + 4.0 * kpad * std::ldexp(1.0, -24));
+    OSK_HIP(v->d_munits.reserve(sizeof(MfmaUnit) * units.size()));
+    OSK_HIP(v->d_seg_split.reserve(sizeof(void*) * ns));
+    OSK_HIP(v->d_seg_vrow.reserve(sizeof(int64_t) * ns));
+    OSK_HIP(v->d_shard_unit_begin.reserve(sizeof(int32_t) * (v->n_shards + 1)));
+    OSK_HIP(v->d_shard_maxnorm2.reserve(sizeof(float) * v->n_shards));
+    OSK_HIP(hipMemcpyAsync(v->d_munits.p, units.data(), sizeof(MfmaUnit) * units.size(), hipMemcpyHostToDevice, st));
+    OSK_HIP(hipMemcpyAsync(v->d_seg_split.p, splits.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
+    OSK_HIP(hipMemcpyAsync(v->d_seg_vrow.p, vrow.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice, st));
+    OSK_HIP(hipMemcpyAsync(v->d_shard_unit_begin.p, shard_list_begin.data(), sizeof(int32_t) * (v->n_shards + 1),
+                           hipMemcpyHostToDevice, st));
+    OSK_HIP(hipMemcpyAsync(v->d_shard_maxnorm2.p, shard_max.data(), sizeof(float) * v->n_shards,
+                           hipMemcpyHostToDevice, st));
+    OSK_HIP(hipStreamSynchronize(st));
+    v->mfma_ready = true;
+    return OSK_OK;
+}
+
+// Batched search: MFMA candidates → per-shard approx top-k' → exact re-score + certificate →
+// exact streaming scan for any query whose certificate failed.  ws_q / ws_qnorm hold the padded
+// queries and their |q|² in the device lane order.
+int32_t batched_search(osk_view* v, int nq, int k, int UP, const uint64_t* const* d_accept,
+                       uint64_t* d_shard_keys, int32_t* d_shard_counts, int64_t* d_visited, hipStream_t st) {
+    int32_t rc = ensure_mfma(v, st);
+    if (rc) return rc;
+    const int S = v->n_shards, KS = v->mfma_KS;
+    const int n_qb = (nq + 255) / 256;
+    const int nq_pad = n_qb * 256;
+    OSK_HIP(v->ws_qsplit.reserve((size_t)(nq_pad / 16) * KS * 2 * 1024));
+    OSK_HIP(launch_split_rows(v->ws_q.as<float4>(), nq, UP, KS, nq_pad / 16, v->ws_qsplit.p, st));
+    OSK_HIP(v->ws_cand_a.reserve(sizeof(uint64_t) * (size_t)nq * v->n_munits * 2 * kKC));
+    MfmaParams mp{};
+    mp.segs = v->d_segs.as<SegDev>();
+    mp.units = v->d_munits.as<MfmaUnit>();
+    mp.seg_split = v->d_seg_split.as<const void*>();
+    mp.accept = d_accept;
+    mp.qsplit = v->ws_qsplit.p;
+    mp.qnorm = v->ws_qnorm.as<float>();
+    mp.cand = v->ws_cand_a.as<uint64_t>();
+    mp.visited = reinterpret_cast<unsigned long long*>(d_visited);
+    mp.n_units = v->n_munits;
+    mp.KS = KS;
+    mp.nq = nq;
+    mp.nq_pad = std::min(nq_pad, (int)(v->ws_qnorm.cap / sizeof(float)));
+    mp.sim = v->sim;
+    mp.ablate = g_tuning.mfma_ablate;
+    OSK_HIP(launch_mfma_cand(mp, n_qb, st));
+    rc = profile_end(v, st);
+    if (rc) return rc;
+    OSK_HIP(v->ws_akeys.reserve(sizeof(uint64_t) * (size_t)nq * S * kKC));
+    OSK_HIP(v->ws_acounts.reserve(sizeof(int32_t) * (size_t)nq * S));
+    OSK_HIP(launch_merge_shards(v->ws_cand_a.as<uint64_t>(), v->n_munits * 2, v->d_shard_unit_begin.as<int32_t>(),
+                                S, nq, kKC, v->ws_akeys.as<uint64_t>(), v->ws_acounts.as<int32_t>(), st));
+    OSK_HIP(v->ws_flags.reserve(sizeof(int) * nq));
+    OSK_HIP(hipMemsetAsync(v->ws_flags.p, 0, sizeof(int) * nq, st));
+    RescoreParams rp{};
+    rp.segs = v->d_segs.as<SegDev>();
+    rp.seg_vrow_begin = v->d_seg_vrow.as<int64_t>();
+    rp.akeys = v->ws_akeys.as<uint64_t>();
+    rp.q = v->ws_q.p;
+    rp.qnorm_dev = v->ws_qnorm.as<float>();
+    rp.qnorm_approx = v->ws_qnorm.as<float>();
+    rp.shard_maxnorm2 = v->d_shard_maxnorm2.as<float>();
+    rp.shard_keys = d_shard_keys;
+    rp.shard_counts = d_shard_counts;
+    rp.flags = v->ws_flags.as<int>();
+    rp.c = v->mfma_c;
+    rp.n_shards = S;
+    rp.n_segs = (int)v->segs.size();
+    rp.units = v->units;
+    rp.k = k;
+    rp.sim = v->sim;
+    OSK_HIP(launch_rescore(v->cfg, nq, rp, st));
+    // certificate failures → exact streaming scan of those queries (rare; needs the flags on host)
+    OSK_HIP(v->h_flags.reserve(sizeof(int) * nq));
+    OSK_HIP(hipMemcpyAsync(v->h_flags.p, v->ws_flags.p, sizeof(int) * nq, hipMemcpyDeviceToHost, st));
+    OSK_HIP(hipStreamSynchronize(st));
+    const int* fl = static_cast<const int*>(v->h_flags.p);
+    std::vector<int> fail;
+    for (int q = 0; q < nq; ++q)
+        if (fl[q]) fail.push_back(q);
+    v->mfma_calls += 1;
+    v->mfma_fallback_queries += (int64_t)fail.size();
+    if (fail.empty() || g_tuning.mfma_ablate) return OSK_OK;
+    const int nf = (int)fail.size();
+    const int nf_pad = (nf + kMaxNQ - 1) / kMaxNQ * kMaxNQ;
+    OSK_HIP(v->ws_fbq.reserve((size_t)nf_pad * UP * 16 + sizeof(float) * nf_pad));
+    OSK_HIP(hipMemsetAsync(v->ws_fbq.p, 0, (size_t)nf_pad * UP * 16 + sizeof(float) * nf_pad, st));
+    char* fbq = v->ws_fbq.as<char>();
+    float* fbn = reinterpret_cast<float*>(fbq + (size_t)nf_pad * UP * 16);
+    for (int i = 0; i < nf; ++i) {
+        OSK_HIP(hipMemcpyAsync(fbq + (size_t)i * UP * 16, v->ws_q.as<char>() + (size_t)fail[i] * UP * 16,
+                               (size_t)UP * 16, hipMemcpyDeviceToDevice, st));
+        OSK_HIP(hipMemcpyAsync(fbn + i, v->ws_qnorm.as<float>() + fail[i], sizeof(float), hipMemcpyDeviceToDevice, st));
+    }
+    OSK_HIP(v->ws_fbkeys.reserve(sizeof(uint64_t) * (size_t)nf * S * k));
+    OSK_HIP(v->ws_fbcounts.reserve(sizeof(int32_t) * (size_t)nf * S));
+    const bool prof = v->profile;
+    v->profile = false;
+    rc = stream_search(v, fbq, fbn, nf, k, UP, d_accept, v->ws_fbkeys.as<uint64_t>(),
+                       v->ws_fbcounts.as<int32_t>(), nullptr, st);
+    v->profile = prof;
+    if (rc) return rc;
+    for (int i = 0; i < nf; ++i) {
+        OSK_HIP(hipMemcpyAsync(d_shard_keys + (size_t)fail[i] * S * k, v->ws_fbkeys.as<uint64_t>() + (size_t)i * S * k,
+                               sizeof(uint64_t) * S * k, hipMemcpyDeviceToDevice, st));
+        OSK_HIP(hipMemcpyAsync(d_shard_counts + (size_t)fail[i] * S, v->ws_fbcounts.as<int32_t>() + (size_t)i * S,
+                               sizeof(int32_t) * S, hipMemcpyDeviceToDevice, st));
+    }
+    return OSK_OK;
+}
 
 // Core of osk_view_search_device (caller holds no lock; device already set).
 int32_t view_search_device(osk_view* v, const void* d_queries, int nq, int k,
@@ -529,44 +804,19 @@ int32_t view_search_device(osk_view* v, const void* d_queries, int nq, int k,
 
     if (d_visited) OSK_HIP(hipMemsetAsync(d_visited, 0, sizeof(int64_t) * v->segs.size(), st));
 
-    ScanParams p{};
-    p.segs = v->d_segs.as<SegDev>();
-    p.tiles = v->d_tiles.as<TileDev>();
-    p.accept = d_accept;
-    p.cand = v->ws_cand.as<uint64_t>();
-    p.visited = reinterpret_cast<unsigned long long*>(d_visited);
-    p.n_tiles = v->n_tiles;
-    p.units = v->units;
-    p.k = k;
-    p.sim = v->sim;
-    p.dim = v->dim;
-    if (v->profile) {
-        if (v->pending) {   // fold the previous call's interval (already complete or we wait)
-            float ms = 0.f;
-            OSK_HIP(hipEventSynchronize(v->ev1));
-            OSK_HIP(hipEventElapsedTime(&ms, v->ev0, v->ev1));
-            v->scan_ms += ms;
-            v->scan_calls += 1;
-            v->pending = false;
-        }
-        OSK_HIP(hipEventRecord(v->ev0, st));
+    const bool batched = v->enc == ENC_FLOAT32 && g_tuning.mfma_min_batch > 0 &&
+                         nq >= g_tuning.mfma_min_batch && k <= kKC - 4;
+    int32_t rc;
+    if (v->profile && (rc = profile_begin(v, st)) != OSK_OK) return rc;
+    if (batched) {
+        if (v->enc == ENC_FLOAT32 && v->sim != SIM_COSINE)   // |q|² for the bound / approx L2
+            OSK_HIP(launch_row_norms_f32(v->ws_q.as<float4>(), nq, UP, v->cfg, v->ws_qnorm.as<float>(), st));
+        rc = batched_search(v, nq, k, UP, d_accept, d_shard_keys, d_shard_counts, d_visited, st);
+    } else {
+        rc = stream_search(v, v->ws_q.p, v->ws_qnorm.p, nq, k, UP, d_accept, d_shard_keys, d_shard_counts,
+                           d_visited, st);
     }
-    for (int q0 = 0; q0 < nq; q0 += kMaxNQ) {
-        const int qc = std::min(kMaxNQ, nq - q0);
-        p.q0 = q0;
-        p.q_count = qc;
-        p.q = static_cast<const char*>(v->ws_q.p) + (size_t)q0 * UP * 16;
-        p.qnorm_f = v->ws_qnorm.as<float>() + q0;
-        p.qnorm_i = v->ws_qnorm.as<int32_t>() + q0;
-        OSK_HIP(launch_scan(v->enc, v->cfg, qc, p, st));
-    }
-    if (v->profile) {
-        OSK_HIP(hipEventRecord(v->ev1, st));
-        v->pending = true;
-    }
-    OSK_HIP(launch_merge_shards(v->ws_cand.as<uint64_t>(), v->n_tiles,
-                                v->d_shard_tile_begin.as<int32_t>(), v->n_shards, nq, k,
-                                d_shard_keys, d_shard_counts, st));
+    if (rc) return rc;
     return OSK_OK;
 }
 
@@ -630,6 +880,33 @@ int32_t osk_view_profile(osk_view* v, int32_t enable) {
     v->scan_ms = 0.0;
     v->scan_calls = 0;
     v->pending = false;
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+// Test/debug only: copy an internal workspace buffer of the last search to host memory.
+int32_t osk_view_debug_copy(osk_view* v, const char* name, void* host, int64_t bytes) {
+    OSK_GUARD_BEGIN
+    OSK_REQUIRE(v && name && host && bytes >= 0, "null argument");
+    int32_t rc = check_device(v->device);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(v->mu);
+    const std::string n(name);
+    const DevBuf* b = n == "akeys" ? &v->ws_akeys : n == "cand_a" ? &v->ws_cand_a : n == "flags" ? &v->ws_flags
+                    : n == "qsplit" ? &v->ws_qsplit : n == "qnorm" ? &v->ws_qnorm : nullptr;
+    OSK_REQUIRE(b != nullptr, "unknown buffer");
+    OSK_REQUIRE((size_t)bytes <= b->cap, "bytes exceed the buffer");
+    OSK_HIP(hipMemcpy(host, b->p, bytes, hipMemcpyDeviceToHost));
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_view_stats(osk_view* v, int64_t* batched_calls, int64_t* fallback_queries) {
+    OSK_GUARD_BEGIN
+    OSK_REQUIRE(v != nullptr && batched_calls && fallback_queries, "null argument");
+    std::lock_guard<std::mutex> lk(v->mu);
+    *batched_calls = v->mfma_calls;
+    *fallback_queries = v->mfma_fallback_queries;
     return OSK_OK;
     OSK_GUARD_END
 }

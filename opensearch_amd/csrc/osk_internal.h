@@ -46,6 +46,58 @@ struct ScanParams {
 
 constexpr int kBlock = 256;          // 4 wavefronts per workgroup
 constexpr int kMaxNQ = 8;            // queries per streaming-scan launch
+constexpr int kKC = 16;              // candidates per (query, shard) of the batched MFMA path (k ≤ kKC − 4)
+
+// ---- batched MFMA path (osk_mfma.hip) ----
+struct MfmaUnit {            // a run of 128-row tiles of one segment, one workgroup
+    int32_t seg;
+    int32_t shard;
+    int64_t tile_begin;      // in 128-row tiles of the segment
+    int64_t tile_end;
+    int64_t vrow_base;       // view-global row index of the segment's ord 0
+};
+
+struct MfmaParams {
+    const SegDev* segs;
+    const MfmaUnit* units;
+    const void* const* seg_split;     // per segment: fragment-ordered bf16 hi/lo copy
+    const uint64_t* const* accept;
+    const void* qsplit;               // queries in the same fragment order
+    const float* qnorm;               // per query |q|² (approx transforms)
+    uint64_t* cand;                   // [nq][n_units*2][kKC] approx candidate keys (doc = view row)
+    unsigned long long* visited;
+    int n_units;
+    int KS;                           // 32-dim K-steps
+    int nq;
+    int nq_pad;
+    int ablate;
+    int sim;
+};
+
+struct RescoreParams {
+    const SegDev* segs;
+    const int64_t* seg_vrow_begin;    // view row of each segment's ord 0 (ascending)
+    const uint64_t* akeys;            // [nq][n_shards][kKC] merged approx candidates
+    const void* q;                    // padded fp32 queries ([nq][L·V] float4)
+    const float* qnorm_dev;           // |q|² in the device lane order (COSINE) or null
+    const float* qnorm_approx;        // |q|² (any order) for the bound
+    const float* shard_maxnorm2;      // max |x|² per shard
+    uint64_t* shard_keys;             // [nq][n_shards][k]
+    int32_t* shard_counts;
+    int* flags;                       // [nq] set when a certificate fails
+    double c;                         // error-bound constant
+    int n_shards;
+    int n_segs;
+    int units;
+    int k;
+    int sim;
+};
+
+hipError_t launch_split_rows(const float4* rows, int64_t n_rows, int units, int KS, int64_t n_rb,
+                             void* out, hipStream_t s);
+hipError_t launch_max_norm2(const float* xn, int64_t n, unsigned* out, hipStream_t s);
+hipError_t launch_mfma_cand(const MfmaParams& p, int n_qblocks, hipStream_t s);
+hipError_t launch_rescore(int cfg, int nq, const RescoreParams& p, hipStream_t s);
 
 int cfg_index(int units);
 
@@ -53,6 +105,10 @@ int cfg_index(int units);
 struct Tuning {
     int scan_nt = 1;          // non-temporal corpus loads in scan_f32 (+4% HBM rate, profiles/r01_scan_ab.txt)
     int tiles_target = 4096;  // workgroup tiles per view (scan grid size)
+    int mfma_min_batch = 16;  // batches ≥ this use the MFMA candidate path (0 = never)
+    int mfma_units = 512;     // workgroup units of the MFMA candidate pass per view
+    int mfma_ablate = 0;      // A/B only: 1 skip selection, 2 skip query staging, 4 skip corpus staging
+                              // (results are wrong and the exact fallback is skipped)
 };
 extern Tuning g_tuning;
 

@@ -344,6 +344,12 @@ class DeviceShardSet:
                                     ptr(docs), ptr(shard), ptr(count), ptr(total), ptr(mx)))
         return scores, docs, shard, count, total, mx
 
+    def stats(self) -> tuple[int, int]:
+        """(searches that took the batched MFMA path, queries recomputed after a failed certificate)."""
+        a, b = C.c_int64(), C.c_int64()
+        check(lib().osk_view_stats(self.handle, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
     def close(self):
         if self._h.value:
             check(lib().osk_view_release(self._h))

@@ -1,0 +1,148 @@
+#!/usr/bin/env python3
+"""Measure every BASELINE.json config on one MI355X (bench.py measures the headline C3 only).
+
+  python tools/bench_configs.py [--only C2,C3,...] [--steps N]
+
+Prints one JSON line per (config, batch): QPS, ms per batch, the dominant kernel's mean duration
+(HIP events, osk_view_profile) and its algorithmic HBM rate.  Synthetic data from the device generator:
+  C1  100k × 128 fp32 L2, 1 shard, k=10                      (the CPU plumbing config, run here on the GPU)
+  C2  1M × 128 fp32 L2 (U[0,1)·128, SIFT-like), 1 shard       batch 1 and 256
+  C3  10M × 768 fp32 COSINE, 8 shards                         batch 1 and 256
+  C4  100M × 96 fp32 DOT_PRODUCT (unit rows), 8 shards        batch 1 and 1024 (one GPU holds all 100M)
+  C5f 10M × 768 COSINE, Bernoulli(s) accept bitsets, s ∈ {1%, 10%, 50%}, batch 1
+  C5i 10M × 768 int8 (U{−128..127}), EUCLIDEAN, batch 1
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from opensearch_amd import _lib  # noqa: E402
+from opensearch_amd.lucene import bits_from_bool, synth_host  # noqa: E402
+
+L = _lib.lib()
+
+
+class View:
+    def __init__(self, n_shards, rows_per_shard, dim, sim, enc, dist, seed=42):
+        self.segs = []
+        for s in range(n_shards):
+            h = C.c_void_p()
+            _lib.check(L.osk_seg_synth(0, rows_per_shard, dim, enc, sim, seed, dist, s * rows_per_shard, C.byref(h)))
+            self.segs.append(h.value)
+        arr = (C.c_void_p * n_shards)(*self.segs)
+        ss = np.arange(n_shards, dtype=np.int32)
+        self.v = C.c_void_p()
+        _lib.check(L.osk_view_create(arr, n_shards, ss.ctypes.data, None, n_shards, None, C.byref(self.v)))
+        self.n_shards, self.rows, self.dim, self.enc = n_shards, rows_per_shard, dim, enc
+
+    def close(self):
+        L.osk_view_release(self.v)
+        for h in self.segs:
+            L.osk_seg_release(C.c_void_p(h))
+
+
+def run(view, queries, batch, steps, warmup, accept_ptrs=None, k=10):
+    S = view.n_shards
+    keys = torch.empty((batch, S, k), dtype=torch.int64, device="cuda")
+    cnt = torch.empty((batch, S), dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    nq_pool = queries.shape[0] // batch
+    acc = None if accept_ptrs is None else accept_ptrs.data_ptr()
+
+    def step(i):
+        q = queries[(i % nq_pool) * batch:(i % nq_pool + 1) * batch]
+        _lib.check(L.osk_view_search_device(view.v, q.data_ptr(), batch, k, acc, keys.data_ptr(), cnt.data_ptr(), None, stream))
+
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize()
+    _lib.check(L.osk_view_profile(view.v, 1))
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ms, calls = C.c_double(), C.c_int64()
+    _lib.check(L.osk_view_scan_time(view.v, C.byref(ms), C.byref(calls)))
+    _lib.check(L.osk_view_profile(view.v, 0))
+    assert int(cnt.min()) >= 0
+    return dt / steps * 1e3, ms.value / max(1, calls.value)
+
+
+def emit(name, view, batch, ms_step, kernel_ms, bytes_per_launch, extra=None):
+    rec = {"config": name, "batch": batch, "qps": batch / (ms_step * 1e-3), "ms_per_batch": ms_step,
+           "kernel_ms": kernel_ms, "kernel_algorithmic_GBps": bytes_per_launch / (kernel_ms * 1e-3) / 1e9,
+           "rows": view.n_shards * view.rows, "dim": view.dim, "shards": view.n_shards}
+    if extra:
+        rec.update(extra)
+    print(json.dumps(rec), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="C1,C2,C3,C4,C5f,C5i")
+    ap.add_argument("--steps", type=int, default=20)
+    a = ap.parse_args()
+    only = set(a.only.split(","))
+    torch.cuda.set_device(0)
+    st, wu = a.steps, 3
+
+    def qpool(n, dim, dist, enc=_lib.FLOAT32):
+        return torch.from_numpy(synth_host(0, n, dim, 43, dist)).cuda()
+
+    if "C1" in only:
+        v = View(1, 100_000, 128, _lib.EUCLIDEAN, _lib.FLOAT32, _lib.DIST_UNIFORM01)
+        q = qpool(64, 128, _lib.DIST_UNIFORM01)
+        ms, km = run(v, q, 1, st * 5, wu)
+        emit("C1", v, 1, ms, km, 100_000 * 128 * 4)
+        v.close()
+    if "C2" in only:
+        v = View(1, 1_000_000, 128, _lib.EUCLIDEAN, _lib.FLOAT32, _lib.DIST_UNIFORM01_X128)
+        q = qpool(1024, 128, _lib.DIST_UNIFORM01_X128)
+        ms, km = run(v, q, 1, st * 5, wu)
+        emit("C2", v, 1, ms, km, 1_000_000 * 128 * 4)
+        ms, km = run(v, q, 256, st, wu)
+        emit("C2", v, 256, ms, km, 1_000_000 * 128 * 4)
+        v.close()
+    if "C3" in only:
+        v = View(8, 1_250_000, 768, _lib.COSINE, _lib.FLOAT32, _lib.DIST_NORMALISH_UNIT)
+        q = qpool(512, 768, _lib.DIST_NORMALISH_UNIT)
+        ms, km = run(v, q, 1, st, wu)
+        emit("C3", v, 1, ms, km, 10_000_000 * 768 * 4)
+        ms, km = run(v, q, 256, st, wu)
+        emit("C3", v, 256, ms, km, 10_000_000 * 768 * 4)
+        if "C5f" in only:
+            rng = np.random.default_rng(44)
+            for sel in [0.01, 0.10, 0.50]:
+                bits = [torch.from_numpy(bits_from_bool(rng.random(1_250_000) < sel).view(np.int64)).cuda()
+                        for _ in range(8)]
+                ptrs = torch.tensor([b.data_ptr() for b in bits], dtype=torch.int64, device="cuda")
+                ms, km = run(v, q, 1, st, wu, accept_ptrs=ptrs)
+                emit(f"C5f-{int(sel * 100)}%", v, 1, ms, km, int(10_000_000 * sel) * 768 * 4 + 10_000_000 // 8,
+                     {"selectivity": sel})
+        v.close()
+    if "C4" in only:
+        v = View(8, 12_500_000, 96, _lib.DOT_PRODUCT, _lib.FLOAT32, _lib.DIST_NORMALISH_UNIT)
+        q = qpool(2048, 96, _lib.DIST_NORMALISH_UNIT)
+        ms, km = run(v, q, 1, st, wu)
+        emit("C4", v, 1, ms, km, 100_000_000 * 96 * 4)
+        ms, km = run(v, q, 1024, max(3, st // 4), 2)
+        emit("C4", v, 1024, ms, km, 100_000_000 * 96 * 4 * 4)
+        v.close()
+    if "C5i" in only:
+        v = View(8, 1_250_000, 768, _lib.EUCLIDEAN, _lib.BYTE, _lib.DIST_INT8)
+        q = torch.from_numpy(synth_host(0, 64, 768, 43, _lib.DIST_INT8)).cuda()
+        ms, km = run(v, q, 1, st, wu)
+        emit("C5i", v, 1, ms, km, 10_000_000 * 768)
+        v.close()
+
+
+if __name__ == "__main__":
+    main()
