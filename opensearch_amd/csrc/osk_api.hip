@@ -11,6 +11,8 @@
 // Every entry point catches all C++ exceptions and returns an error code (see osknn.h).
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <atomic>
+#include <cmath>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -90,13 +92,21 @@ int32_t check_device(int device) {
         set_error("device index out of range");
         return OSK_ERR_INVALID;
     }
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
-        set_error("hipGetDeviceProperties failed");
-        return OSK_ERR_DEVICE;
-    }
-    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
-        set_error(std::string("device is ") + prop.gcnArchName + ", libosknn is built for gfx950");
+    static std::atomic<int> arch_ok[64];   // per device: 0 unknown, 1 gfx950, 2 another arch
+    if (device >= 64 || arch_ok[device].load() == 0) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+            set_error("hipGetDeviceProperties failed");
+            return OSK_ERR_DEVICE;
+        }
+        const bool ok = std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+        if (device < 64) arch_ok[device].store(ok ? 1 : 2);
+        if (!ok) {
+            set_error(std::string("device is ") + prop.gcnArchName + ", libosknn is built for gfx950");
+            return OSK_ERR_NO_DEVICE;
+        }
+    } else if (arch_ok[device].load() == 2) {
+        set_error("device is not gfx950; libosknn is built for gfx950");
         return OSK_ERR_NO_DEVICE;
     }
     if (hipSetDevice(device) != hipSuccess) {
@@ -793,14 +803,8 @@ int32_t view_search_device(osk_view* v, const void* d_queries, int nq, int k,
     OSK_HIP(v->ws_q.reserve((size_t)nq_pad * UP * 16));
     OSK_HIP(v->ws_qnorm.reserve(sizeof(float) * nq_pad));
     // queries → padded unit layout (zeros past dim and for the dummy queries of the last launch)
-    OSK_HIP(hipMemsetAsync(v->ws_q.p, 0, (size_t)nq_pad * UP * 16, st));
-    OSK_HIP(launch_pad_rows(d_queries, (int64_t)v->dim * elem, v->ws_q.p, (int64_t)UP * 16, nq,
-                            (int64_t)v->dim * elem, st));
-    OSK_HIP(hipMemsetAsync(v->ws_qnorm.p, 0, sizeof(float) * nq_pad, st));
-    if (v->enc == ENC_FLOAT32 && v->sim == SIM_COSINE)
-        OSK_HIP(launch_row_norms_f32(v->ws_q.as<float4>(), nq, UP, v->cfg, v->ws_qnorm.as<float>(), st));
-    if (v->enc == ENC_BYTE)
-        OSK_HIP(launch_row_norms_i8(v->ws_q.as<int4>(), nq, UP, v->ws_qnorm.as<int32_t>(), st));
+    // one launch: padded queries (the scan computes |q|² itself, in its own lane layout)
+    OSK_HIP(launch_prep_queries(d_queries, (int64_t)v->dim * elem, nq, v->ws_q.p, UP, nq_pad, st));
 
     if (d_visited) OSK_HIP(hipMemsetAsync(d_visited, 0, sizeof(int64_t) * v->segs.size(), st));
 
@@ -809,8 +813,8 @@ int32_t view_search_device(osk_view* v, const void* d_queries, int nq, int k,
     int32_t rc;
     if (v->profile && (rc = profile_begin(v, st)) != OSK_OK) return rc;
     if (batched) {
-        if (v->enc == ENC_FLOAT32 && v->sim != SIM_COSINE)   // |q|² for the bound / approx L2
-            OSK_HIP(launch_row_norms_f32(v->ws_q.as<float4>(), nq, UP, v->cfg, v->ws_qnorm.as<float>(), st));
+        // |q|² in the device lane layout: approx transforms, the re-score (COSINE) and the bound
+        OSK_HIP(launch_row_norms_f32(v->ws_q.as<float4>(), nq, UP, v->cfg, v->ws_qnorm.as<float>(), st));
         rc = batched_search(v, nq, k, UP, d_accept, d_shard_keys, d_shard_counts, d_visited, st);
     } else {
         rc = stream_search(v, v->ws_q.p, v->ws_qnorm.p, nq, k, UP, d_accept, d_shard_keys, d_shard_counts,

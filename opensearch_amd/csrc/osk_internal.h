@@ -119,6 +119,8 @@ hipError_t launch_row_norms_i8(const int4* rows, int64_t n_rows, int units, int3
                                hipStream_t s);
 hipError_t launch_synth(void* rows, int64_t n_rows, int dim, int units, int enc, uint64_t seed,
                         int dist, int64_t row0, hipStream_t s);
+hipError_t launch_prep_queries(const void* src, int64_t row_bytes, int nq, void* dst, int units, int nq_pad,
+                               hipStream_t s);
 hipError_t launch_pad_rows(const void* src, int64_t src_pitch, void* dst, int64_t dst_pitch,
                            int64_t n_rows, int64_t row_bytes, hipStream_t s);
 hipError_t launch_merge_shards(const uint64_t* cand, int n_tiles, const int32_t* shard_tile_begin,

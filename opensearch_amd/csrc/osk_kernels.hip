@@ -60,6 +60,40 @@ __device__ __forceinline__ void wave_offer(uint64_t key, bool offer, uint64_t& l
     }
 }
 
+// Walk a wave's rows [wb, we) in groups of R (lane group g ↔ one row) and call
+// body(row, in_range, accepted_known).  Filter pushdown: with an accept bitset over a dense field
+// (doc == ord) the rows are taken 64 at a time, the accepted ones are compacted to the front of
+// the wave with one ds_permute, and only they are visited — at 1 % selectivity a wave touches ~1 %
+// of the rows instead of every row.  Otherwise every row is visited and the body checks accept.
+template <int R, class F>
+__device__ __forceinline__ void walk_rows(int64_t wb, int64_t we, const uint64_t* abits,
+                                          const int32_t* ord_to_doc, int lane, int g, F&& body) {
+    if (abits && !ord_to_doc) {
+        for (int64_t w0 = wb; w0 < we; w0 += 64) {
+            const int64_t word = w0 >> 6;
+            const int sh = (int)(w0 & 63);
+            uint64_t m = abits[word] >> sh;
+            if (sh && (word + 1) * 64 < we) m |= abits[word + 1] << (64 - sh);
+            if (we - w0 < 64) m &= (1ull << (we - w0)) - 1ull;
+            const int n = __popcll(m);
+            if (n == 0) continue;
+            // rank of each lane's bit among the set (or the unset) bits → a permutation that puts
+            // the positions of the n accepted rows into lanes 0..n-1
+            const bool bit = (m >> lane) & 1ull;
+            const int below = __popcll(m & ((1ull << lane) - 1ull));
+            const int dst = bit ? below : n + (lane - below);
+            const int pos = __builtin_amdgcn_ds_permute(dst << 2, lane);
+            for (int i0 = 0; i0 < n; i0 += R) {
+                const int idx = i0 + g;
+                const int pr = __shfl(pos, idx < 64 ? idx : 0);
+                body(w0 + pr, idx < n, true);
+            }
+        }
+    } else {
+        for (int64_t r0 = wb; r0 < we; r0 += R) body(r0 + g, r0 + g < we, false);
+    }
+}
+
 // Fold the lists of waves 1..3 (in LDS) into wave 0's list.
 __device__ __forceinline__ void block_fold(const uint64_t* lists /*[4][64]*/, uint64_t& lk,
                                            uint64_t& thr, int lane, int k) {
@@ -112,9 +146,26 @@ __global__ __launch_bounds__(kBlock) void scan_f32(ScanParams p) {
         for (int i = tid; i < NQ * UP; i += kBlock) sq[i] = Q[i];
         __syncthreads();
     }
+    // COSINE: |q|² in the same lane layout as the row norms (identical bits to row_norms_f32 on the
+    // padded query), computed here instead of by a separate launch.
     float qn[NQ];
 #pragma unroll
-    for (int b = 0; b < NQ; ++b) qn[b] = p.qnorm_f ? p.qnorm_f[b] : 0.0f;
+    for (int b = 0; b < NQ; ++b) {
+        qn[b] = 0.0f;
+        if (!L2K && p.sim == SIM_COSINE) {
+            float ax = 0.f, ay = 0.f, az = 0.f, aw = 0.f;
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                const float4 qv = QREG ? qf[QREG ? b : 0][QREG ? j : 0] : sq[b * UP + t + j * L];
+                ax = fmaf(qv.x, qv.x, ax); ay = fmaf(qv.y, qv.y, ay);
+                az = fmaf(qv.z, qv.z, az); aw = fmaf(qv.w, qv.w, aw);
+            }
+            float s = (ax + ay) + (az + aw);
+#pragma unroll
+            for (int m = 1; m < L; m <<= 1) s += __shfl_xor(s, m);
+            qn[b] = s;
+        }
+    }
 
     const int64_t rows = tile.row_end - tile.row_begin;
     const int64_t per_wave = ((rows + 4 * R - 1) / (4 * R)) * R;
@@ -128,13 +179,11 @@ __global__ __launch_bounds__(kBlock) void scan_f32(ScanParams p) {
     for (int b = 0; b < NQ; ++b) { lk[b] = 0ull; thr[b] = 0ull; }
     uint32_t nvis = 0;
 
-    for (int64_t r0 = wb; r0 < we; r0 += R) {
-        const int64_t row = r0 + g;
-        bool valid = row < we;
+    walk_rows<R>(wb, we, abits, seg.ord_to_doc, lane, g, [&](const int64_t row, bool valid, bool accepted_known) {
         int32_t doc = 0;
         if (valid) {
             doc = seg.ord_to_doc ? seg.ord_to_doc[row] : (int32_t)row;
-            if (abits) valid = (abits[doc >> 6] >> (doc & 63)) & 1ull;
+            if (abits && !accepted_known) valid = (abits[doc >> 6] >> (doc & 63)) & 1ull;
         }
         float4 xv[V];
         const float4* xr = X + row * units;
@@ -172,7 +221,7 @@ __global__ __launch_bounds__(kBlock) void scan_f32(ScanParams p) {
             const uint64_t key = valid ? make_key(sc, (uint32_t)(seg.doc_base + doc)) : 0ull;
             wave_offer(key, t == 0, lk[b], thr[b], lane, k);
         }
-    }
+    });
 
     if (p.visited && p.q0 == 0 && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
 
@@ -223,9 +272,20 @@ __global__ __launch_bounds__(kBlock) void scan_i8(ScanParams p) {
         for (int i = tid; i < NQ * UP; i += kBlock) sq[i] = Q[i];
         __syncthreads();
     }
-    int32_t qn[NQ];
+    int32_t qn[NQ];   // Σq² (exact) over this wave's L-lane group
 #pragma unroll
-    for (int b = 0; b < NQ; ++b) qn[b] = p.qnorm_i[b];
+    for (int b = 0; b < NQ; ++b) {
+        int acc = 0;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const int4 qv = QREG ? qf[QREG ? b : 0][QREG ? j : 0] : sq[b * UP + t + j * L];
+            acc = dot4_i8(qv.x, qv.x, acc); acc = dot4_i8(qv.y, qv.y, acc);
+            acc = dot4_i8(qv.z, qv.z, acc); acc = dot4_i8(qv.w, qv.w, acc);
+        }
+#pragma unroll
+        for (int m = 1; m < L; m <<= 1) acc += __shfl_xor(acc, m);
+        qn[b] = acc;
+    }
 
     const int64_t rows = tile.row_end - tile.row_begin;
     const int64_t per_wave = ((rows + 4 * R - 1) / (4 * R)) * R;
@@ -239,13 +299,11 @@ __global__ __launch_bounds__(kBlock) void scan_i8(ScanParams p) {
     for (int b = 0; b < NQ; ++b) { lk[b] = 0ull; thr[b] = 0ull; }
     uint32_t nvis = 0;
 
-    for (int64_t r0 = wb; r0 < we; r0 += R) {
-        const int64_t row = r0 + g;
-        bool valid = row < we;
+    walk_rows<R>(wb, we, abits, seg.ord_to_doc, lane, g, [&](const int64_t row, bool valid, bool accepted_known) {
         int32_t doc = 0;
         if (valid) {
             doc = seg.ord_to_doc ? seg.ord_to_doc[row] : (int32_t)row;
-            if (abits) valid = (abits[doc >> 6] >> (doc & 63)) & 1ull;
+            if (abits && !accepted_known) valid = (abits[doc >> 6] >> (doc & 63)) & 1ull;
         }
         int4 xv[V];
         const int4* xr = X + row * units;
@@ -275,7 +333,7 @@ __global__ __launch_bounds__(kBlock) void scan_i8(ScanParams p) {
             const uint64_t key = valid ? make_key(sc, (uint32_t)(seg.doc_base + doc)) : 0ull;
             wave_offer(key, t == 0, lk[b], thr[b], lane, k);
         }
-    }
+    });
 
     if (p.visited && p.q0 == 0 && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
 
@@ -490,6 +548,33 @@ __global__ __launch_bounds__(kBlock) void pad_rows(const uint8_t* __restrict__ s
     for (int64_t r = wave_global; r < n_rows; r += n_waves)
         for (int64_t b = lane; b < dst_pitch; b += 64)
             dst[r * dst_pitch + b] = b < row_bytes ? src[r * src_pitch + b] : (uint8_t)0;
+}
+
+// Queries → the padded unit layout in one launch: rows [0, nq) copied with zeros past row_bytes,
+// rows [nq, nq_pad) (the dummy queries of the last ≤8-query launch) all zero.
+__global__ __launch_bounds__(kBlock) void prep_queries(const uint8_t* __restrict__ src, int64_t row_bytes,
+                                                       int nq, int4* __restrict__ dst, int units, int nq_pad) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave_global = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) >> 6;
+    for (int64_t r = wave_global; r < nq_pad; r += n_waves) {
+        for (int f = lane; f < units; f += 64) {
+            alignas(16) uint8_t v[16];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int64_t b = (int64_t)f * 16 + e;
+                v[e] = (r < nq && b < row_bytes) ? src[r * row_bytes + b] : (uint8_t)0;
+            }
+            dst[r * units + f] = *reinterpret_cast<const int4*>(v);
+        }
+    }
+}
+
+hipError_t launch_prep_queries(const void* src, int64_t row_bytes, int nq, void* dst, int units, int nq_pad,
+                               hipStream_t s) {
+    hipLaunchKernelGGL(prep_queries, dim3(grid_for(nq_pad)), dim3(kBlock), 0, s, static_cast<const uint8_t*>(src),
+                       row_bytes, nq, static_cast<int4*>(dst), units, nq_pad);
+    return hipGetLastError();
 }
 
 hipError_t launch_pad_rows(const void* src, int64_t src_pitch, void* dst, int64_t dst_pitch,
