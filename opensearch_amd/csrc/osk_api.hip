@@ -187,6 +187,7 @@ struct osk_seg {
     void* d_split = nullptr;
     int split_KS = 0;
     unsigned* d_maxnorm2 = nullptr;
+    float* d_xsqrt = nullptr;          // |x| per row (MFMA path)
     float h_maxnorm2 = 0.0f;
     std::mutex mu;
     osk_view* self_view = nullptr;   // single-segment view behind osk_seg_search
@@ -211,8 +212,8 @@ struct osk_view {
     int n_munits = 0;
     int mfma_KS = 0;
     double mfma_c = 0.0;
-    DevBuf d_munits, d_seg_split, d_seg_vrow, d_shard_unit_begin, d_shard_maxnorm2;
-    DevBuf ws_qsplit, ws_cand_a, ws_akeys, ws_acounts, ws_flags, ws_fbq, ws_fbkeys, ws_fbcounts;
+    DevBuf d_munits, d_seg_split, d_seg_xsqrt, d_seg_vrow, d_shard_unit_begin, d_shard_maxnorm2;
+    DevBuf ws_qsplit, ws_cand_a, ws_akeys, ws_acounts, ws_pkeys, ws_pcounts, ws_flags, ws_fbq, ws_fbkeys, ws_fbcounts;
     HostPinned h_flags;
     int64_t mfma_calls = 0, mfma_fallback_queries = 0;
     std::mutex mu;
@@ -247,6 +248,7 @@ osk_seg::~osk_seg() {
     if (d_ord_to_doc) (void)hipFree(d_ord_to_doc);
     if (d_split) (void)hipFree(d_split);
     if (d_maxnorm2) (void)hipFree(d_maxnorm2);
+    if (d_xsqrt) (void)hipFree(d_xsqrt);
 }
 
 namespace {
@@ -598,7 +600,7 @@ int32_t stream_search(osk_view* v, const void* qpad, const void* qnorm, int nq, 
 int32_t ensure_split(osk_seg* s, hipStream_t st) {
     std::lock_guard<std::mutex> lk(s->mu);
     if (s->d_split) return OSK_OK;
-    const int KS = (s->units + 7) / 8;                      // 32-dim K-steps
+    const int KS = ((s->units + 7) / 8 + kKsAlign - 1) / kKsAlign * kKsAlign;   // 32-dim K-steps (padded)
     const int64_t n_tiles = (s->n_rows + 127) / 128;        // 128-row tiles
     const int64_t n_rb = std::max<int64_t>(1, n_tiles) * 8;
     if (!s->d_xnorm_f) {
@@ -614,6 +616,8 @@ int32_t ensure_split(osk_seg* s, hipStream_t st) {
         return OSK_ERR_OOM;
     }
     OSK_HIP(launch_split_rows(static_cast<const float4*>(s->d_rows), s->n_rows, s->units, KS, n_rb, split, st));
+    OSK_HIP(hipMalloc(&s->d_xsqrt, std::max<int64_t>(1, s->n_rows) * sizeof(float)));
+    if (s->n_rows > 0) OSK_HIP(launch_row_sqrt(s->d_xnorm_f, s->n_rows, s->d_xsqrt, st));
     OSK_HIP(hipMalloc(&s->d_maxnorm2, sizeof(unsigned)));
     OSK_HIP(hipMemsetAsync(s->d_maxnorm2, 0, sizeof(unsigned), st));
     if (s->n_rows > 0) OSK_HIP(launch_max_norm2(s->d_xnorm_f, s->n_rows, s->d_maxnorm2, st));
@@ -631,12 +635,14 @@ int32_t ensure_mfma(osk_view* v, hipStream_t st) {
     if (v->mfma_ready) return OSK_OK;
     const int ns = (int)v->segs.size();
     std::vector<const void*> splits(ns);
+    std::vector<const float*> xsq(ns);
     std::vector<int64_t> vrow(ns);
     int64_t acc = 0, total_tiles = 0;
     for (int i = 0; i < ns; ++i) {
         int32_t rc = ensure_split(v->segs[i], st);
         if (rc) return rc;
         splits[i] = v->segs[i]->d_split;
+        xsq[i] = v->segs[i]->d_xsqrt;
         vrow[i] = acc;
         acc += v->segs[i]->n_rows;
         total_tiles += (v->segs[i]->n_rows + 127) / 128;
@@ -664,18 +670,20 @@ int32_t ensure_mfma(osk_view* v, hipStream_t st) {
     shard_list_begin[v->n_shards] = (int32_t)units.size() * 2;
     v->n_munits = (int)units.size();
     OSK_REQUIRE(v->n_munits > 0 && v->n_munits < 65536, "bad MFMA unit count");
-    v->mfma_KS = (v->units + 7) / 8;
+    v->mfma_KS = ((v->units + 7) / 8 + kKsAlign - 1) / kKsAlign * kKsAlign;
     // |Σ approx − Σ device order| ≤ c·|x||q|: bf16 split (3·2^-16) + fp32 accumulation of the
     // 3·Kpad MFMA products and of the Kpad device-order products (γ_n ≈ n·2^-24), ×1.5 margin.
     const double kpad = 32.0 * v->mfma_KS;
     v->mfma_c = 1.5 * (3.0 * std::ldexp(1.0, -16) + 4.0 * kpad * std::ldexp(1.0, -24));
     OSK_HIP(v->d_munits.reserve(sizeof(MfmaUnit) * units.size()));
     OSK_HIP(v->d_seg_split.reserve(sizeof(void*) * ns));
+    OSK_HIP(v->d_seg_xsqrt.reserve(sizeof(void*) * ns));
     OSK_HIP(v->d_seg_vrow.reserve(sizeof(int64_t) * ns));
     OSK_HIP(v->d_shard_unit_begin.reserve(sizeof(int32_t) * (v->n_shards + 1)));
     OSK_HIP(v->d_shard_maxnorm2.reserve(sizeof(float) * v->n_shards));
     OSK_HIP(hipMemcpyAsync(v->d_munits.p, units.data(), sizeof(MfmaUnit) * units.size(), hipMemcpyHostToDevice, st));
     OSK_HIP(hipMemcpyAsync(v->d_seg_split.p, splits.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
+    OSK_HIP(hipMemcpyAsync(v->d_seg_xsqrt.p, xsq.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
     OSK_HIP(hipMemcpyAsync(v->d_seg_vrow.p, vrow.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice, st));
     OSK_HIP(hipMemcpyAsync(v->d_shard_unit_begin.p, shard_list_begin.data(), sizeof(int32_t) * (v->n_shards + 1),
                            hipMemcpyHostToDevice, st));
@@ -703,6 +711,7 @@ int32_t batched_search(osk_view* v, int nq, int k, int UP, const uint64_t* const
     mp.segs = v->d_segs.as<SegDev>();
     mp.units = v->d_munits.as<MfmaUnit>();
     mp.seg_split = v->d_seg_split.as<const void*>();
+    mp.xsqrt = v->d_seg_xsqrt.as<const float*>();
     mp.accept = d_accept;
     mp.qsplit = v->ws_qsplit.p;
     mp.qnorm = v->ws_qnorm.as<float>();
@@ -714,11 +723,25 @@ int32_t batched_search(osk_view* v, int nq, int k, int UP, const uint64_t* const
     mp.nq_pad = std::min(nq_pad, (int)(v->ws_qnorm.cap / sizeof(float)));
     mp.sim = v->sim;
     mp.ablate = g_tuning.mfma_ablate;
-    OSK_HIP(launch_mfma_cand(mp, n_qb, st));
-    rc = profile_end(v, st);
-    if (rc) return rc;
+    mp.n_shards = S;
     OSK_HIP(v->ws_akeys.reserve(sizeof(uint64_t) * (size_t)nq * S * kKC));
     OSK_HIP(v->ws_acounts.reserve(sizeof(int32_t) * (size_t)nq * S));
+    if (!(g_tuning.mfma_ablate & 16)) {
+        // pilot: the first tile of every unit, merged per (query, shard) → k'-th approx score =
+        // a threshold no row below which can reach the shard's top-k'
+        OSK_HIP(v->ws_pkeys.reserve(sizeof(uint64_t) * (size_t)nq * S * kKC));
+        OSK_HIP(v->ws_pcounts.reserve(sizeof(int32_t) * (size_t)nq * S));
+        MfmaParams pp = mp;
+        pp.visited = nullptr;
+        OSK_HIP(launch_mfma_cand(pp, n_qb, true, st));
+        OSK_HIP(launch_merge_shards(v->ws_cand_a.as<uint64_t>(), v->n_munits * 2, v->d_shard_unit_begin.as<int32_t>(),
+                                    S, nq, kKC, v->ws_pkeys.as<uint64_t>(), v->ws_pcounts.as<int32_t>(), st));
+        mp.thr_keys = v->ws_pkeys.as<uint64_t>();
+        mp.thr_counts = v->ws_pcounts.as<int32_t>();
+    }
+    OSK_HIP(launch_mfma_cand(mp, n_qb, false, st));
+    rc = profile_end(v, st);
+    if (rc) return rc;
     OSK_HIP(launch_merge_shards(v->ws_cand_a.as<uint64_t>(), v->n_munits * 2, v->d_shard_unit_begin.as<int32_t>(),
                                 S, nq, kKC, v->ws_akeys.as<uint64_t>(), v->ws_acounts.as<int32_t>(), st));
     OSK_HIP(v->ws_flags.reserve(sizeof(int) * nq));

@@ -46,6 +46,7 @@ struct ScanParams {
 
 constexpr int kBlock = 256;          // 4 wavefronts per workgroup
 constexpr int kMaxNQ = 8;            // queries per streaming-scan launch
+constexpr int kKsAlign = 4;        // MFMA K-steps (32 dims) per segment split copy: a multiple of this
 constexpr int kKC = 16;              // candidates per (query, shard) of the batched MFMA path (k ≤ kKC − 4)
 
 // ---- batched MFMA path (osk_mfma.hip) ----
@@ -61,11 +62,15 @@ struct MfmaParams {
     const SegDev* segs;
     const MfmaUnit* units;
     const void* const* seg_split;     // per segment: fragment-ordered bf16 hi/lo copy
+    const float* const* xsqrt;        // per segment: |x| per row
     const uint64_t* const* accept;
     const void* qsplit;               // queries in the same fragment order
     const float* qnorm;               // per query |q|² (approx transforms)
     uint64_t* cand;                   // [nq][n_units*2][kKC] approx candidate keys (doc = view row)
     unsigned long long* visited;
+    const uint64_t* thr_keys;         // pilot: [nq][n_shards][kKC] merged keys (main pass), or null
+    const int32_t* thr_counts;        // pilot: [nq][n_shards]
+    int n_shards;
     int n_units;
     int KS;                           // 32-dim K-steps
     int nq;
@@ -95,8 +100,9 @@ struct RescoreParams {
 
 hipError_t launch_split_rows(const float4* rows, int64_t n_rows, int units, int KS, int64_t n_rb,
                              void* out, hipStream_t s);
+hipError_t launch_row_sqrt(const float* xn, int64_t n, float* out, hipStream_t s);
 hipError_t launch_max_norm2(const float* xn, int64_t n, unsigned* out, hipStream_t s);
-hipError_t launch_mfma_cand(const MfmaParams& p, int n_qblocks, hipStream_t s);
+hipError_t launch_mfma_cand(const MfmaParams& p, int n_qblocks, bool pilot, hipStream_t s);
 hipError_t launch_rescore(int cfg, int nq, const RescoreParams& p, hipStream_t s);
 
 int cfg_index(int units);
@@ -107,7 +113,8 @@ struct Tuning {
     int tiles_target = 4096;  // workgroup tiles per view (scan grid size)
     int mfma_min_batch = 16;  // batches ≥ this use the MFMA candidate path (0 = never)
     int mfma_units = 512;     // workgroup units of the MFMA candidate pass per view
-    int mfma_ablate = 0;      // A/B only: 1 skip selection, 2 skip query staging, 4 skip corpus staging
+    int mfma_ablate = 0;      // A/B only: 1 skip the epilogue, 2 skip query staging, 4 skip corpus staging,
+                              // 8 force the full staging epilogue, 16 skip the pilot pass
                               // (results are wrong and the exact fallback is skipped)
 };
 extern Tuning g_tuning;

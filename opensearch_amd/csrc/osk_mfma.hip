@@ -83,6 +83,20 @@ __global__ __launch_bounds__(kBlock) void max_norm2(const float* __restrict__ xn
     if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
 }
 
+// |x| per row (the cosine bound of the candidate epilogue)
+__global__ __launch_bounds__(kBlock) void row_sqrt(const float* __restrict__ xn, int64_t n, float* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
+        out[i] = sqrtf(xn[i]);
+}
+
+hipError_t launch_row_sqrt(const float* xn, int64_t n, float* out, hipStream_t s) {
+    int64_t blocks = (n + kBlock - 1) / kBlock;
+    if (blocks < 1) blocks = 1;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(row_sqrt, dim3((unsigned)blocks), dim3(kBlock), 0, s, xn, n, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_max_norm2(const float* xn, int64_t n, unsigned* out, hipStream_t s) {
     int64_t blocks = (n + kBlock - 1) / kBlock;
     if (blocks < 1) blocks = 1;
@@ -93,18 +107,44 @@ hipError_t launch_max_norm2(const float* xn, int64_t n, unsigned* out, hipStream
 
 // ------------------------------------------------------------------------------------------------
 // candidate pass: 8 waves, 128 rows × 256 queries per tile, K-steps of 32 dims.
+//
+// Wave w owns queries w·32 … +31 of the block against all 128 rows of the tile (acc: 8 row
+// blocks × 2 query blocks of 16×16).  Its query fragments (hi/lo, 4 KiB per K-step) are private:
+// they stream from L2 straight into a register ring kDepth K-steps deep.  The corpus fragments
+// (16 KiB per K-step, shared by all waves) stream by LDS-DMA into a (kDepth+1)-slot LDS ring.
+// The (tile, K-step) sequence of a unit is one flat stream of steps, so the pipeline stays full
+// across tile boundaries.
 // ------------------------------------------------------------------------------------------------
-constexpr int kMB = 512;                       // threads per workgroup
-constexpr int kStageA = 16 * 1024;             // 8 row blocks × hi/lo × 1 KiB
-constexpr int kStageB = 32 * 1024;             // 16 query blocks × hi/lo × 1 KiB
-constexpr int kStage = kStageA + kStageB;      // 48 KiB
-constexpr int kStagePitch = 260;               // fp32 per staged score row (bank-conflict-free writes)
-constexpr int kStaging = 128 * kStagePitch * 4; // 130 KiB of epilogue score staging (aliases the ring)
-constexpr int kLds = 3 * kStage > kStaging ? 3 * kStage : kStaging;   // 144 KiB: 3-slot ring
+constexpr int kMB = 512;                        // threads per workgroup
+constexpr int kDepth = kKsAlign;                // K-steps in flight (KS is a multiple of it)
+constexpr int kStageA = 16 * 1024;              // 8 row blocks × hi/lo × 1 KiB
+constexpr int kRing = (kDepth + 1) * kStageA;   // 80 KiB
+constexpr int kStagePitch = 260;                // fp32 per staged score row (bank-conflict-free writes)
+constexpr int kOffStaged = kRing;               // 64 rows × 260 fp32 (half a tile) = 65 KiB
+constexpr int kStaging = 64 * kStagePitch * 4;
 
+// wait until at most `steps` K-steps of this wave's loads (6 VMEM ops each) are in flight
+// (`steps` is a compile-time constant after unrolling; the switch folds away)
+__device__ __forceinline__ void vm_wait_steps(int steps) {
+    switch (steps) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+    }
+}
+
+// LDS-DMA: 16 B (or 4 B) per lane from a per-lane global address to lds_base + lane·size.
+// AUX = 2: non-temporal (the corpus copy streams through once and must not evict the queries,
+// which every workgroup re-reads from L2 each tile).
+template <int AUX = 0>
 __device__ __forceinline__ void glds16(const void* g, char* lds_base) {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                     (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+                                     (__attribute__((address_space(3))) void*)lds_base, 16, 0, AUX);
+}
+__device__ __forceinline__ void glds4(const void* g, char* lds_base) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                     (__attribute__((address_space(3))) void*)lds_base, 4, 0, 0);
 }
 
 __device__ __forceinline__ float approx_score(int sim, float d, float qn, float xn) {
@@ -119,17 +159,50 @@ __device__ __forceinline__ float approx_score(int sim, float d, float qn, float 
     }
 }
 
+// LDS beyond the ring and the staging: per-query survivor slots of the MAIN epilogue
+constexpr int kSlots = 4;                              // survivors per query per tile before overflow
+constexpr int kOffXn = kOffStaged + kStaging;          // f32 [2][|x|², |x|][128] of the tile (by tile parity)
+constexpr int kOffThr = kOffXn + 2 * 256 * 4;          // u32 [256] sortable score thresholds
+constexpr int kOffCnt = kOffThr + 256 * 4;             // i32 [256] survivor counts
+constexpr int kOffSlot = kOffCnt + 256 * 4;            // u64 [256][kSlots] survivor keys
+constexpr int kOffOvf = kOffSlot + 256 * kSlots * 8;   // i32 overflow flag
+constexpr int kLdsTotal = kOffOvf + 16;
+static_assert(kLdsTotal <= 160 * 1024, "LDS budget");
+
+__device__ __forceinline__ void list_insert(uint64_t (&lst)[kKC], uint64_t key) {
+    if (key > lst[kKC - 1]) {
+        uint64_t cur = key;
+#pragma unroll
+        for (int i = 0; i < kKC; ++i) {
+            const uint64_t a = lst[i];
+            const bool gt = cur > a;
+            lst[i] = gt ? cur : a;
+            cur = gt ? a : cur;
+        }
+    }
+}
+
+// PILOT = true: only the first tile of each unit, every score staged (the lists it leaves are
+// merged per (query, shard) into the thresholds of the main pass).
+template <bool PILOT>
 __global__ __launch_bounds__(kMB) void mfma_cand(MfmaParams p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* staged = reinterpret_cast<float*>(smem + kOffStaged);
+    uint32_t* s_thr = reinterpret_cast<uint32_t*>(smem + kOffThr);
+    int* s_cnt = reinterpret_cast<int*>(smem + kOffCnt);
+    uint64_t* s_slot = reinterpret_cast<uint64_t*>(smem + kOffSlot);
+    int* s_ovf = reinterpret_cast<int*>(smem + kOffOvf);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform → scalar addressing
-    const int wr = wave & 1, wq = wave >> 1;
     const MfmaUnit unit = p.units[blockIdx.x];
     const SegDev seg = p.segs[unit.seg];
     const char* __restrict__ A = static_cast<const char*>(p.seg_split[unit.seg]);
     const int qblock = blockIdx.y;
-    const char* __restrict__ Bq = static_cast<const char*>(p.qsplit) + (size_t)qblock * 16 * p.KS * 2 * 1024;
     const int KS = p.KS, sim = p.sim;
+    // this wave's two 16-query blocks, fragment-ordered [qb][ks][hi/lo][64 lanes][16 B]
+    const char* __restrict__ Bw = static_cast<const char*>(p.qsplit) +
+                                  (size_t)(qblock * 16 + wave * 2) * KS * 2048 + lane * 16;
+    const size_t Bqb = (size_t)KS * 2048;   // bytes per query block
     const uint64_t* abits = p.accept ? p.accept[unit.seg] : nullptr;
 
     // thread-side selection state: thread ↔ (query q_sel of this block, row half h_sel)
@@ -138,135 +211,241 @@ __global__ __launch_bounds__(kMB) void mfma_cand(MfmaParams p) {
 #pragma unroll
     for (int i = 0; i < kKC; ++i) lst[i] = 0ull;
     uint32_t nvis = 0;
+    if (h_sel == 0) {
+        // initial threshold: k'-th approx score of the pilot tiles of this (query, shard), else none
+        uint32_t t0 = 0u;
+        const int qg = qblock * 256 + q_sel;
+        if (!PILOT && p.thr_keys && qg < p.nq) {
+            const size_t o = (size_t)qg * p.n_shards + unit.shard;
+            if (p.thr_counts[o] >= kKC) t0 = (uint32_t)(p.thr_keys[o * kKC + kKC - 1] >> 32);
+        }
+        s_thr[q_sel] = t0;
+        s_cnt[q_sel] = 0;
+    }
+    if (tid == 0) s_ovf[0] = 0;
 
-    // this lane's queries / norms in the MFMA layout: q_local = wq·64 + qb·16 + (lane & 15)
-    float qn_l[4];
+    // this lane's queries / norms in the MFMA layout: q_local = wave·32 + j·16 + (lane & 15)
+    float qn_l[2];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int qg = qblock * 256 + wq * 64 + j * 16 + (lane & 15);
+    for (int j = 0; j < 2; ++j) {
+        const int qg = qblock * 256 + wave * 32 + j * 16 + (lane & 15);
         qn_l[j] = qg < p.nq_pad ? p.qnorm[qg] : 1.0f;
     }
 
-    // Each wave moves 6 of the 48 1-KiB chunks of a stage.  Chunk c of k-step ks lives at a
-    // wave-uniform byte offset; only lane·16 varies per lane.
+    const int64_t tile_last = PILOT ? unit.tile_begin : unit.tile_end - 1;
     const int lane16 = lane * 16;
-    auto issue = [&](const char* tileA, int ks, int buf) {
-        char* base = smem + buf * kStage;
+    // corpus fragments of (tile, k-step ks) → ring slot `slot` (this wave's 2 of the 16 chunks)
+    auto issue_a = [&](int64_t tile, int ks, int slot) {
+        if (p.ablate & 4) return;
+        const char* src = A + ((size_t)tile * 8 * KS + ks) * 2048 + lane16;
+        char* dst = smem + slot * kStageA;
 #pragma unroll
-        for (int c6 = 0; c6 < 6; ++c6) {
-            const int c = wave * 6 + c6;   // uniform
-            const char* src;
-            char* dst;
-            if (c < 16) {
-                const int rb = c >> 1, part = c & 1;
-                src = tileA + (size_t)((rb * KS + ks) * 2 + part) * 1024;
-                dst = base + c * 1024;
-            } else {
-                const int c2 = c - 16, qb = c2 >> 1, part = c2 & 1;
-                src = Bq + (size_t)((qb * KS + ks) * 2 + part) * 1024;
-                dst = base + kStageA + c2 * 1024;
-            }
-            if (!(p.ablate & (c < 16 ? 4 : 2))) glds16(src + lane16, dst);
+        for (int c2 = 0; c2 < 2; ++c2) {
+            const int c = wave * 2 + c2;               // chunk = (row block c >> 1, hi/lo c & 1)
+            glds16<2>(src + ((size_t)(c >> 1) * KS * 2 + (c & 1)) * 1024, dst + c * 1024);
+        }
+        if (ks == 0 && wave < 4) {   // the tile's |x|² and |x| ride along with its first K-step
+            const int64_t row = min(tile * 128 + (wave & 1) * 64 + lane, seg.n_rows - 1);
+            glds4((wave < 2 ? seg.xnorm_f : p.xsqrt[unit.seg]) + row,
+                  smem + kOffXn + (int)(tile & 1) * 1024 + wave * 256);
         }
     };
-
-    for (int64_t tile = unit.tile_begin; tile < unit.tile_end; ++tile) {
-        const int64_t tile_rb0 = tile * 8;
-        f32x4 acc[4][4];
+    bf16x8 bq[kDepth][4];   // register ring: [slot][qb0 hi, qb0 lo, qb1 hi, qb1 lo]
+    auto issue_b = [&](int ks, bf16x8 (&r)[4]) {
+        if (p.ablate & 2) return;
+        const char* src = Bw + (size_t)ks * 2048;
+        r[0] = *reinterpret_cast<const bf16x8*>(src);
+        r[1] = *reinterpret_cast<const bf16x8*>(src + 1024);
+        r[2] = *reinterpret_cast<const bf16x8*>(src + Bqb);
+        r[3] = *reinterpret_cast<const bf16x8*>(src + Bqb + 1024);
+    };
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+    for (int u = 0; u < kDepth; ++u) {
+        if (p.ablate & 2) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-        // 3-slot ring, two K-steps in flight: slot (ks+2)%3 was last read in iteration ks−1, whose
-        // closing barrier every wave has passed before this iteration issues into it.
-        const char* tileA = A + (size_t)tile_rb0 * KS * 2048;
-        issue(tileA, 0, 0);
-        if (KS > 1) issue(tileA, 1, 1);
-        int buf = 0;
-        for (int ks = 0; ks < KS; ++ks) {
-            if (ks + 2 < KS) {
-                const int nb = buf == 0 ? 2 : buf - 1;   // (ks + 2) % 3
-                issue(tileA, ks + 2, nb);
-                asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-            } else if (ks + 1 < KS) {
-                asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            __builtin_amdgcn_s_barrier();
-            const char* sA = smem + buf * kStage;
-            const char* sB = sA + kStageA;
-            bf16x8 bh[4], bl[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int qb = wq * 4 + j;
-                bh[j] = *reinterpret_cast<const bf16x8*>(sB + (qb * 2 + 0) * 1024 + lane * 16);
-                bl[j] = *reinterpret_cast<const bf16x8*>(sB + (qb * 2 + 1) * 1024 + lane * 16);
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int rb = wr * 4 + i;
-                const bf16x8 ah = *reinterpret_cast<const bf16x8*>(sA + (rb * 2 + 0) * 1024 + lane * 16);
-                const bf16x8 al = *reinterpret_cast<const bf16x8*>(sA + (rb * 2 + 1) * 1024 + lane * 16);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[j], acc[i][j], 0, 0, 0);
-                }
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();   // every wave is done reading buf: it may be refilled
-            buf = buf == 2 ? 0 : buf + 1;
+            for (int x = 0; x < 4; ++x) bq[u][x] = bf16x8{};
         }
-        __syncthreads();
-
-        // epilogue: approx scores → staged [128 rows][256 queries] (the accumulators die here) →
-        // thread (q_sel, h_sel) offers rows h_sel·64 … +63 of its query to its top-k' list
-        float* staged = reinterpret_cast<float*>(smem);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row_local = wr * 64 + i * 16 + (lane >> 4) * 4 + r;
-                const int64_t row = tile_rb0 * 16 + row_local;
-                const bool rv = row < seg.n_rows;
-                const float xn = rv ? seg.xnorm_f[row] : 1.0f;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int ql = wq * 64 + j * 16 + (lane & 15);
-                    staged[row_local * kStagePitch + ql] =
-                        rv ? approx_score(sim, acc[i][j][r], qn_l[j], xn) : -__builtin_inff();
-                }
-            }
-        __syncthreads();
-        const int sel_rows = (p.ablate & 1) ? 0 : 64;
-#pragma unroll 2
-        for (int rr = 0; rr < sel_rows; ++rr) {
-            const int row_local = h_sel * 64 + rr;
-            const int64_t ord = tile_rb0 * 16 + row_local;
-            const float s = staged[row_local * kStagePitch + q_sel];
-            if (!(s > -__builtin_inff())) continue;
-            if (abits) {
-                const int32_t doc = seg.ord_to_doc ? seg.ord_to_doc[ord] : (int32_t)ord;
-                if (!((abits[doc >> 6] >> (doc & 63)) & 1ull)) continue;
-            }
-            if (q_sel == 0) ++nvis;
-            const uint64_t key = make_key(s, (uint32_t)(unit.vrow_base + ord));
-            if (key > lst[kKC - 1]) {
-                uint64_t cur = key;
-#pragma unroll
-                for (int i = 0; i < kKC; ++i) {
-                    const uint64_t a = lst[i];
-                    const bool gt = cur > a;
-                    lst[i] = gt ? cur : a;
-                    cur = gt ? a : cur;
-                }
-            }
-        }
-        __syncthreads();
+        issue_a(unit.tile_begin, u, u);
+        issue_b(u, bq[u]);
     }
+
+    f32x4 acc[8][2];
+    int slot = 0;   // ring slot of the current step; step + kDepth goes to slot − 1 (mod kDepth + 1)
+    for (int64_t tile = unit.tile_begin; tile <= tile_last; ++tile) {
+        const int64_t tile_rb0 = tile * 8;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+        for (int ks0 = 0; ks0 < KS; ks0 += kDepth) {
+            // the step kDepth ahead: same tile, or (KS multiple of kDepth) the next tile's k-step u
+            const bool wrap = ks0 + kDepth >= KS;
+            const int64_t tile_n = wrap ? tile + 1 : tile;
+            const int ks_n0 = wrap ? 0 : ks0 + kDepth;
+            const bool more = tile_n <= tile_last;
+#pragma unroll
+            for (int u = 0; u < kDepth; ++u) {
+                // own DMA + query loads of this step done (later steps stay in flight), then every
+                // wave's; past the barrier no wave still reads the previous step's slot
+                vm_wait_steps(more ? kDepth - 1 : kDepth - 1 - u);
+                __builtin_amdgcn_s_barrier();
+                const char* sA = smem + slot * kStageA + lane16;
+                const int slot_n = slot == 0 ? kDepth : slot - 1;
+                if (more) issue_a(tile_n, ks_n0 + u, slot_n);
+                const bf16x8 b0h = bq[u][0], b0l = bq[u][1], b1h = bq[u][2], b1l = bq[u][3];
+#pragma unroll
+                for (int i = 0; i < 8; i += 2) {
+                    const bf16x8 ah0 = *reinterpret_cast<const bf16x8*>(sA + (i * 2 + 0) * 1024);
+                    const bf16x8 al0 = *reinterpret_cast<const bf16x8*>(sA + (i * 2 + 1) * 1024);
+                    const bf16x8 ah1 = *reinterpret_cast<const bf16x8*>(sA + (i * 2 + 2) * 1024);
+                    const bf16x8 al1 = *reinterpret_cast<const bf16x8*>(sA + (i * 2 + 3) * 1024);
+                    // three sweeps over 4 accumulators: consecutive MFMAs never share one
+                    acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah0, b0h, acc[i][0], 0, 0, 0);
+                    acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah0, b1h, acc[i][1], 0, 0, 0);
+                    acc[i + 1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah1, b0h, acc[i + 1][0], 0, 0, 0);
+                    acc[i + 1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah1, b1h, acc[i + 1][1], 0, 0, 0);
+                    acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah0, b0l, acc[i][0], 0, 0, 0);
+                    acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah0, b1l, acc[i][1], 0, 0, 0);
+                    acc[i + 1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah1, b0l, acc[i + 1][0], 0, 0, 0);
+                    acc[i + 1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah1, b1l, acc[i + 1][1], 0, 0, 0);
+                    acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al0, b0h, acc[i][0], 0, 0, 0);
+                    acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al0, b1h, acc[i][1], 0, 0, 0);
+                    acc[i + 1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al1, b0h, acc[i + 1][0], 0, 0, 0);
+                    acc[i + 1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al1, b1h, acc[i + 1][1], 0, 0, 0);
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this step's slot reads retired
+                if (more) issue_b(ks_n0 + u, bq[u]);
+                slot = slot == kDepth ? 0 : slot + 1;
+            }
+        }
+
+        // visited: accepted rows of the tile, counted once (query block 0, one thread per row)
+        if (!PILOT && p.visited && qblock == 0 && tid < 128) {
+            const int64_t row = tile_rb0 * 16 + tid;
+            bool ok = row < seg.n_rows;
+            if (ok && abits) {
+                const int32_t doc = seg.ord_to_doc ? seg.ord_to_doc[row] : (int32_t)row;
+                ok = (abits[doc >> 6] >> (doc & 63)) & 1ull;
+            }
+            nvis += ok ? 1u : 0u;
+        }
+        if (p.ablate & 1) {   // A/B: no epilogue at all (the accumulators stay live)
+            float sink = 0.f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) sink += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+            if (sink == 12345.678f) lst[0] = 1;
+            continue;
+        }
+
+        // ---- epilogue (uses only the staging / slot LDS: the ring keeps streaming) ----
+        const float* xs = reinterpret_cast<const float*>(smem + kOffXn + (int)(tile & 1) * 1024);
+        const float* xr = xs + 128;   // |x|
+        // MAIN: every accumulator is scored in registers and compared with its query's threshold
+        // (pilot k'-th score, raised as the lists fill); the few survivors go to kSlots LDS slots
+        // per query and the query's owner thread merges them into its list.  A tile where some
+        // query has more survivors than slots takes the full path below instead (its
+        // accumulators are still live).
+        // PILOT and overflow: the scores are staged in LDS half a tile at a time and every
+        // (query, row quarter) thread offers its 32 rows of the half to its list.
+        bool full = PILOT || (p.ablate & 8);
+        if (!full) {
+            // Per query a dot-product bound equivalent to "approx score ≥ threshold", loosened by
+            // 2^-16·max(1, |t|) (far above the rounding of either form): d ≥ cq·a_row, a = |x| for
+            // COSINE, else 1.  Only rows past it get the exact approx score and the real test.
+            uint32_t thr_l[2];
+            float cq[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                thr_l[j] = s_thr[wave * 32 + j * 16 + (lane & 15)];
+                const float t = sortable_to_float(thr_l[j]);
+                const float tm = t - 0x1p-16f * fmaxf(1.0f, fabsf(t));
+                float c = -__builtin_inff();
+                if (thr_l[j] != 0u) {
+                    if (sim == SIM_COSINE) c = (2.0f * tm - 1.0f) * sqrtf(qn_l[j]);
+                    else if (sim == SIM_DOT_PRODUCT) c = 2.0f * tm - 1.0f;
+                    else if (sim == SIM_MIP && tm > 0.0f) c = tm >= 1.0f ? tm - 1.0f : 1.0f - 1.0f / tm;
+                }
+                cq[j] = c;
+            }
+            const bool cosine = sim == SIM_COSINE;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row_local = i * 16 + (lane >> 4) * 4 + r;
+                    const float a = cosine ? xr[row_local] : 1.0f;
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        if (!(acc[i][j][r] < cq[j] * a)) {   // (NaN goes to the exact test)
+                            const int64_t row = tile_rb0 * 16 + row_local;
+                            if (row >= seg.n_rows) continue;
+                            const float s = approx_score(sim, acc[i][j][r], qn_l[j], xs[row_local]);
+                            if (float_to_sortable(s) < thr_l[j]) continue;
+                            if (abits) {
+                                const int32_t doc = seg.ord_to_doc ? seg.ord_to_doc[row] : (int32_t)row;
+                                if (!((abits[doc >> 6] >> (doc & 63)) & 1ull)) continue;
+                            }
+                            const int ql = wave * 32 + j * 16 + (lane & 15);
+                            const int slot = atomicAdd(&s_cnt[ql], 1);
+                            if (slot < kSlots) s_slot[ql * kSlots + slot] = make_key(s, (uint32_t)(unit.vrow_base + row));
+                            else s_ovf[0] = 1;
+                        }
+                    }
+                }
+            __syncthreads();
+            full = s_ovf[0] != 0;   // uniform
+            if (h_sel == 0) {
+                if (!full) {
+                    const int n = min(s_cnt[q_sel], kSlots);
+                    for (int e = 0; e < n; ++e) list_insert(lst, s_slot[q_sel * kSlots + e]);
+                    if (lst[kKC - 1]) atomicMax(&s_thr[q_sel], (uint32_t)(lst[kKC - 1] >> 32));
+                }
+                s_cnt[q_sel] = 0;
+            }
+            __syncthreads();        // every thread has read s_ovf
+            if (tid == 0) s_ovf[0] = 0;
+        }
+        if (full) {
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+#pragma unroll
+                for (int i = half * 4; i < half * 4 + 4; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int row_local = i * 16 + (lane >> 4) * 4 + r;
+                        const int64_t row = tile_rb0 * 16 + row_local;
+                        const bool rv = row < seg.n_rows;
+                        const float xn = rv ? xs[row_local] : 1.0f;
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            const int ql = wave * 32 + j * 16 + (lane & 15);
+                            staged[(row_local - half * 64) * kStagePitch + ql] =
+                                rv ? approx_score(sim, acc[i][j][r], qn_l[j], xn) : -__builtin_inff();
+                        }
+                    }
+                __syncthreads();
+#pragma unroll 2
+                for (int rr = 0; rr < 32; ++rr) {
+                    const int row_half = h_sel * 32 + rr;
+                    const int64_t ord = tile_rb0 * 16 + half * 64 + row_half;
+                    const float s = staged[row_half * kStagePitch + q_sel];
+                    if (!(s > -__builtin_inff())) continue;
+                    if (abits) {
+                        const int32_t doc = seg.ord_to_doc ? seg.ord_to_doc[ord] : (int32_t)ord;
+                        if (!((abits[doc >> 6] >> (doc & 63)) & 1ull)) continue;
+                    }
+                    list_insert(lst, make_key(s, (uint32_t)(unit.vrow_base + ord)));
+                }
+                __syncthreads();
+            }
+            if (!PILOT && lst[kKC - 1]) atomicMax(&s_thr[q_sel], (uint32_t)(lst[kKC - 1] >> 32));
+            __syncthreads();
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may outlive the workgroup
 
     const int qg = qblock * 256 + q_sel;
     if (qg < p.nq) {
@@ -274,17 +453,24 @@ __global__ __launch_bounds__(kMB) void mfma_cand(MfmaParams p) {
 #pragma unroll
         for (int i = 0; i < kKC; ++i) o[i] = lst[i];
     }
-    if (p.visited && qblock == 0 && q_sel == 0) atomicAdd(&p.visited[unit.seg], (unsigned long long)nvis);
+    if (!PILOT && p.visited && qblock == 0 && tid < 128 && nvis)
+        atomicAdd(&p.visited[unit.seg], (unsigned long long)nvis);
 }
 
-hipError_t launch_mfma_cand(const MfmaParams& p, int n_qblocks, hipStream_t s) {
+hipError_t launch_mfma_cand(const MfmaParams& p, int n_qblocks, bool pilot, hipStream_t s) {
+    if (p.KS % kDepth != 0) return hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)mfma_cand, hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+        hipError_t e = hipFuncSetAttribute((const void*)mfma_cand<false>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTotal);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)mfma_cand<true>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTotal);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    hipLaunchKernelGGL(mfma_cand, dim3(p.n_units, n_qblocks), dim3(kMB), kLds, s, p);
+    if (pilot) hipLaunchKernelGGL(mfma_cand<true>, dim3(p.n_units, n_qblocks), dim3(kMB), kLdsTotal, s, p);
+    else hipLaunchKernelGGL(mfma_cand<false>, dim3(p.n_units, n_qblocks), dim3(kMB), kLdsTotal, s, p);
     return hipGetLastError();
 }
 

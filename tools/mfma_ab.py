@@ -3,7 +3,7 @@
 
   python tools/mfma_ab.py [--rows-per-shard N] [--batch 256] [--ablate 0,1,2,4,6] [--units 512]
 
-ablate bits: 1 = skip the top-k' selection, 2 = skip query (B) staging, 4 = skip corpus (A) staging.
+ablate bits: 1 = skip the epilogue (scores + selection), 2 = skip query (B) staging, 4 = skip corpus (A) staging.
 Ablated runs produce wrong candidates; only the kernel time (HIP events, osk_view_profile) matters.
 """
 import argparse
