@@ -50,15 +50,16 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md; 6.29 TB/s meas
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_traffic_c3_b1.json")
 
 
-def pmc_traffic(rows_local: int, batch: int):
+def pmc_traffic(rows_local: int, batch: int, prefilter: bool):
     """HBM bytes per scan launch from the committed rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes of this
     same command (tools/pmc_traffic.py; gfx950 ×2 FETCH correction applied), scaled to this rank's rows.
     The passes were taken at N=1 (10M rows, batch 1).  None when absent or for another batch size."""
     if batch != 1 or not os.path.exists(PMC_SUMMARY):
         return None, None
     data = json.load(open(PMC_SUMMARY))
+    want = "sq8_scan<16, 3, 1, 4>" if prefilter else "scan_f32<16, 12, 1, false"
     for name, v in data.items():
-        if "scan_f32<16, 12, 1, false" in name:
+        if want in name:
             return v["hbm_bytes"] * rows_local / (N_SHARDS * ROWS_PER_SHARD), os.path.relpath(PMC_SUMMARY, ROOT)
     return None, None
 
@@ -98,6 +99,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--rows-per-shard", type=int, default=ROWS_PER_SHARD)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sq8", action="store_true", help="measure the fp32 streaming scan as the main path")
     ap.add_argument("--cpu-sample-rows", type=int, default=262_144)
     ap.add_argument("--cpu-queries", type=int, default=32)
     a = ap.parse_args()
@@ -124,6 +126,9 @@ def main():
     keys = torch.empty((B, shards.s_pad, K), dtype=torch.int64, device="cuda")
     counts = torch.empty((B, shards.s_pad), dtype=torch.int32, device="cuda")
     gsi = shards.global_shard_index.cuda()
+    # One explicit stream for the library calls and torch's own ops (gather copy, events): the null
+    # stream's handle is 0, which the C-ABI reads as "the library's own (non-blocking) stream".
+    torch.cuda.set_stream(torch.cuda.Stream())
     stream = torch.cuda.current_stream().cuda_stream
 
     def step(i):
@@ -132,51 +137,109 @@ def main():
         gk, gc = D.gather_shard_topk(keys, counts, world)
         return D.merge_gathered(gk, gc, gsi, K, FROM, SIZE, local_rank, stream)
 
-    for i in range(a.warmup):
-        out = step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    _lib.check(_lib.lib().osk_view_profile(shards.view, 1))
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t_start = time.perf_counter()
-    ev0.record()
-    for i in range(a.steps):
-        out = step(a.warmup + i)
-        if (i + 1) % 200 == 0:
-            log(f"rank {rank}: step {i + 1}/{a.steps}")
-    ev1.record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
-    scan_ms, calls = C.c_double(), C.c_int64()
-    _lib.check(_lib.lib().osk_view_scan_time(shards.view, C.byref(scan_ms), C.byref(calls)))
-    _lib.check(_lib.lib().osk_view_profile(shards.view, 0))
-    ev_ms = ev0.elapsed_time(ev1)
+    def timed(steps, warmup, offset=0):
+        """W untimed steps, then K steps between barrier + synchronize; returns the max-over-ranks wall
+        time, the mean scan-launch duration (HIP events on the launch stream), the GPU event time and
+        the last step's output."""
+        out = None
+        for i in range(warmup):
+            out = step(offset + i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        _lib.check(_lib.lib().osk_view_profile(shards.view, 1))
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t_start = time.perf_counter()
+        ev0.record()
+        for i in range(steps):
+            out = step(offset + warmup + i)
+            if (i + 1) % 200 == 0:
+                log(f"rank {rank}: step {i + 1}/{steps}")
+        ev1.record()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t_start
+        scan_ms, calls = C.c_double(), C.c_int64()
+        _lib.check(_lib.lib().osk_view_scan_time(shards.view, C.byref(scan_ms), C.byref(calls)))
+        _lib.check(_lib.lib().osk_view_profile(shards.view, 0))
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item()), scan_ms.value / max(1, calls.value), ev0.elapsed_time(ev1), out
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed_max = float(t.item())
+    def counter(name):
+        v = C.c_int64()
+        _lib.check(_lib.lib().osk_view_counter(shards.view, name.encode(), C.byref(v)))
+        return v.value
 
+    prefilter = B < 16 and K <= 16 and not a.no_sq8
+    batched = B >= 16 and K <= 12           # the library's batched MFMA path (osk_tune "mfma_min_batch")
+    _lib.tune("sq8", 0 if a.no_sq8 else 1)
+    fb0, rs0, calls0 = counter("sq8_fallback_queries"), counter("sq8_rescored_rows"), counter("sq8_calls")
+    elapsed_max, scan_avg_ms, ev_ms, out = timed(a.steps, a.warmup)
     # sanity on the last step: every query got `SIZE` hits from the 10M corpus
     cnt = out[3].cpu().numpy()
     assert np.all(cnt == SIZE), cnt
 
-    scan_avg_ms = scan_ms.value / max(1, calls.value)
-    batched = B >= 16 and K <= 12           # the library's batched MFMA path (osk_tune "mfma_min_batch")
-    passes = (B + 255) // 256 if batched else (B + 7) // 8
-    bytes_per_launch = rows_local * DIM * 4 * passes
+    u8 = (DIM + 15) // 16
+    if prefilter:
+        passes = (B + 7) // 8
+        bytes_per_launch = rows_local * (u8 * 16 + 16) * passes
+        kernel_name = (f"sq8_scan<L=16,V=3,NQ={min(8, 1 << max(0, (B - 1).bit_length()))}> certified int8 prefilter "
+                       "(bytes = int8 rows + 16-B bound terms per row, once per launch of ≤ 8 queries)")
+    elif batched:
+        passes = (B + 255) // 256
+        bytes_per_launch = rows_local * DIM * 4 * passes
+        kernel_name = "mfma_cand (bf16x3 split MFMA candidates; bytes = the hi/lo copy read once per 256 queries)"
+    else:
+        passes = (B + 7) // 8
+        bytes_per_launch = rows_local * DIM * 4 * passes
+        kernel_name = "scan_f32<L=16,V=12,NQ=min(B,8),dot,nt>"
     achieved = bytes_per_launch / (scan_avg_ms * 1e-3) / 1e9
-    kernel_name = ("mfma_cand (bf16x3 split MFMA candidates; bytes = the hi/lo copy read once per 256 queries)"
-                   if batched else "scan_f32<L=16,V=12,NQ=min(B,8),dot,nt>")
     mfma_tflops = (3 * 2 * B * rows_local * DIM) / (scan_avg_ms * 1e-3) / 1e12 if batched else None
 
-    traffic, traffic_src = pmc_traffic(rows_local, B)
+    extra = {}
+    if prefilter:
+        n_calls = counter("sq8_calls") - calls0
+        extra["prefilter"] = {
+            "fallback_queries": counter("sq8_fallback_queries") - fb0,
+            "rescored_rows_per_query": (counter("sq8_rescored_rows") - rs0) / max(1, n_calls * B),
+            "searches": n_calls,
+        }
+        # the fp32 streaming scan on the same queries, same run: its own roofline, and the results
+        # of both paths compared bit for bit (docs, scores, shard indices) on a sample of batches
+        _lib.tune("sq8", 0)
+        s_el, s_scan, _, _ = timed(min(a.steps, 50), 2)
+        mism = 0
+        for i in range(min(8, n_pool)):
+            ref = step(i)
+            _lib.tune("sq8", 1)
+            got = step(i)
+            _lib.tune("sq8", 0)
+            for j, (x, y) in enumerate(zip(got, ref)):
+                same = torch.equal(x.view(torch.int32) if x.dtype == torch.float32 else x,
+                                   y.view(torch.int32) if y.dtype == torch.float32 else y)
+                if not same:
+                    mism += 1
+                    if mism <= 4:
+                        log(f"mismatch batch {i} output {j}: prefilter {x.flatten()[:10].tolist()} "
+                            f"fp32 {y.flatten()[:10].tolist()}")
+        _lib.tune("sq8", 1)
+        s_bytes = rows_local * DIM * 4 * passes
+        extra["fp32_stream"] = {
+            "value": min(a.steps, 50) * B / s_el, "scan_ms_avg": s_scan,
+            "roofline_achieved_GBps": s_bytes / (s_scan * 1e-3) / 1e9,
+            "roofline_frac": s_bytes / (s_scan * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "kernel": "scan_f32<L=16,V=12,NQ=min(B,8),dot,nt>",
+            "identical_to_prefilter_on_8_batches": mism == 0,
+        }
+        assert mism == 0, f"prefilter and fp32 scan results differ in {mism} tensors"
+
+    traffic, traffic_src = pmc_traffic(rows_local, B, prefilter)
     if rank == 0:
         res = {
             "metric": "exact k-NN QPS@k=10 (recall=1.0), 10M×768 fp32, 1/2/4/8 GPUs; % HBM roofline",
@@ -193,6 +256,7 @@ def main():
             "data": "synthetic (device counter generator: Irwin-Hall(4)≈N(0,1), rows L2-normalised; seed 42/43)",
             "config": {"workload": "C3 Cohere-shaped exact k-NN: 10M×768 fp32 COSINE, 8 shards, k=10, from=0, size=10",
                        "batch": B, "rows": N_SHARDS * a.rows_per_shard, "dim": DIM, "shards": N_SHARDS,
+                       "path": "prefilter" if prefilter else "mfma" if batched else "fp32_stream",
                        "parallelism": f"shards over {world} GPU(s), RCCL all-gather + device merge"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
@@ -201,6 +265,7 @@ def main():
                          "bf16_mfma_tflops": mfma_tflops},
             "gpu_event_ms_per_step": ev_ms / a.steps,
         }
+        res.update(extra)
         if world == 1 and not a.no_cpu_baseline:
             threads = min(16, os.cpu_count() or 1)
             res["cpu_baseline"] = cpu_baseline(a.cpu_sample_rows, a.cpu_queries, threads)

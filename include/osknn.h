@@ -171,14 +171,22 @@ int32_t osk_view_scan_time(osk_view* view, double* total_ms, int64_t* calls);
  *   "tiles_target"    workgroup tiles per view for the streaming scan (default 4096; at view create)
  *   "mfma_min_batch"  batches of at least this many float32 queries (and k ≤ 12) take the batched
  *                     MFMA path (default 16; 0 = never)
- *   "mfma_units"      workgroup units of the MFMA candidate pass per view (default 512) */
+ *   "mfma_units"      workgroup units of the MFMA candidate pass per view (default 512)
+ *   "sq8"             0|1 certified int8 prefilter for float32 searches below mfma_min_batch with
+ *                     k ≤ 16 (default 1; results are bit-identical either way)
+ *   "sq8_force_fallback"  tests: every prefiltered query takes the exact fallback scan */
 int32_t osk_tune_set(const char* key, int64_t value);
 
 /* Batched-path counters of a view: searches that took the MFMA path, and queries among them whose
  * certificate failed and were recomputed by the exact streaming scan. */
 int32_t osk_view_stats(osk_view* view, int64_t* batched_calls, int64_t* fallback_queries);
+/* Named counters of a view: "mfma_calls", "mfma_fallback_queries" (as osk_view_stats),
+ * "sq8_calls" (prefiltered searches), "sq8_fallback_queries" (queries whose certificate failed and
+ * were answered by the exact scan), "sq8_rescored_rows" (rows re-scored exactly, all calls). */
+int32_t osk_view_counter(osk_view* view, const char* name, int64_t* value);
 /* Tests / debugging only: copy `bytes` of an internal buffer of the view's last search
- * ("akeys", "cand_a", "flags", "qsplit", "qnorm") to host memory. */
+ * ("akeys", "cand_a", "flags", "qsplit", "qnorm", "sq8cand",
+ * "sq8lb", "qc") to host memory. */
 int32_t osk_view_debug_copy(osk_view* view, const char* name, void* host, int64_t bytes);
 
 /* Host-buffer convenience: shard search + coordinator merge on one device, synchronous.

@@ -65,6 +65,7 @@ SIGNATURES = {
     "osk_view_profile": (_I32, [_P, _I32]),
     "osk_tune_set": (_I32, [C.c_char_p, _I64]),
     "osk_view_stats": (_I32, [_P, _PI64, _PI64]),
+    "osk_view_counter": (_I32, [_P, C.c_char_p, _PI64]),
     "osk_view_debug_copy": (_I32, [_P, C.c_char_p, _P, _I64]),
     "osk_view_scan_time": (_I32, [_P, C.POINTER(C.c_double), _PI64]),
 }

@@ -22,8 +22,8 @@ INCLUDE = ROOT / "include"
 LIB = PKG / "libosknn.so"
 OBJDIR = ROOT / "build" / "osknn"
 
-SOURCES = ["osk_kernels.hip", "osk_mfma.hip", "osk_api.hip", "osk_host.cpp"]
-HEADERS = ["osk_common.h", "osk_internal.h"]
+SOURCES = ["osk_kernels.hip", "osk_mfma.hip", "osk_sq8.hip", "osk_api.hip", "osk_host.cpp"]
+HEADERS = ["osk_common.h", "osk_internal.h", "osk_wave.h"]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"

@@ -189,6 +189,10 @@ struct osk_seg {
     unsigned* d_maxnorm2 = nullptr;
     float* d_xsqrt = nullptr;          // |x| per row (MFMA path)
     float h_maxnorm2 = 0.0f;
+    // certified int8 prefilter (built on first prefiltered search): int8 rows + per-row bound terms
+    void* d_q8 = nullptr;
+    float4* d_q8aux = nullptr;
+    int units8 = 0;
     std::mutex mu;
     osk_view* self_view = nullptr;   // single-segment view behind osk_seg_search
     ~osk_seg();
@@ -216,6 +220,13 @@ struct osk_view {
     DevBuf ws_qsplit, ws_cand_a, ws_akeys, ws_acounts, ws_pkeys, ws_pcounts, ws_flags, ws_fbq, ws_fbkeys, ws_fbcounts;
     HostPinned h_flags;
     int64_t mfma_calls = 0, mfma_fallback_queries = 0;
+    // certified int8 prefilter
+    bool sq8_ready = false;
+    int units8 = 0;
+    float sq8_gam = 0.f, sq8_g2 = 0.f, sq8_cos_slack = 0.f;
+    DevBuf d_sq8_rows, d_sq8_aux, d_counters;   // counters: [0] fallback queries, [1] rows re-scored
+    DevBuf ws_q8, ws_qc, ws_sq8cand, ws_sq8lb;
+    int64_t sq8_calls = 0;
     std::mutex mu;
     // scan-kernel timing (osk_view_profile): events bracket the scan launches on the search stream
     bool profile = false;
@@ -249,6 +260,8 @@ osk_seg::~osk_seg() {
     if (d_split) (void)hipFree(d_split);
     if (d_maxnorm2) (void)hipFree(d_maxnorm2);
     if (d_xsqrt) (void)hipFree(d_xsqrt);
+    if (d_q8) (void)hipFree(d_q8);
+    if (d_q8aux) (void)hipFree(d_q8aux);
 }
 
 namespace {
@@ -334,6 +347,10 @@ int32_t osk_tune_set(const char* key, int64_t value) {
     } else if (k == "mfma_units") {
         OSK_REQUIRE(value >= 1 && value <= 32768, "mfma_units out of range");
         g_tuning.mfma_units = (int)value;
+    } else if (k == "sq8") {
+        g_tuning.sq8 = value != 0;
+    } else if (k == "sq8_force_fallback") {
+        g_tuning.sq8_force_fallback = value != 0;
     } else if (k == "tiles_target") {
         OSK_REQUIRE(value >= 1 && value <= (1 << 22), "tiles_target out of range");
         g_tuning.tiles_target = (int)value;
@@ -510,12 +527,23 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
 
     v->seg_doc_base.resize(n_segs);
     for (int i = 0; i < n_segs; ++i) v->seg_doc_base[i] = seg_doc_base ? seg_doc_base[i] : 0;
+    std::vector<int64_t> vrow(n_segs);   // view-global row of each segment's ord 0
+    int64_t vacc = 0;
+    for (int i = 0; i < n_segs; ++i) {
+        vrow[i] = vacc;
+        vacc += segs[i]->n_rows;
+    }
+    OSK_REQUIRE(total < 0xFFFFFFFFll, "a view holds < 2^32 rows");
     std::vector<SegDev> sd = seg_devs(v.get());
     hipStream_t st = device_stream(v->device);
     OSK_HIP(v->d_segs.reserve(sizeof(SegDev) * n_segs));
     OSK_HIP(v->d_tiles.reserve(sizeof(TileDev) * std::max<size_t>(1, tiles.size())));
     OSK_HIP(v->d_shard_tile_begin.reserve(sizeof(int32_t) * (n_shards + 1)));
     OSK_HIP(v->d_shard_index.reserve(sizeof(int32_t) * n_shards));
+    OSK_HIP(v->d_seg_vrow.reserve(sizeof(int64_t) * n_segs));
+    OSK_HIP(v->d_counters.reserve(sizeof(unsigned long long) * 4));
+    OSK_HIP(hipMemsetAsync(v->d_counters.p, 0, sizeof(unsigned long long) * 4, st));
+    OSK_HIP(hipMemcpyAsync(v->d_seg_vrow.p, vrow.data(), sizeof(int64_t) * n_segs, hipMemcpyHostToDevice, st));
     OSK_HIP(hipMemcpyAsync(v->d_segs.p, sd.data(), sizeof(SegDev) * n_segs, hipMemcpyHostToDevice, st));
     if (!tiles.empty())
         OSK_HIP(hipMemcpyAsync(v->d_tiles.p, tiles.data(), sizeof(TileDev) * tiles.size(),
@@ -678,13 +706,11 @@ int32_t ensure_mfma(osk_view* v, hipStream_t st) {
     OSK_HIP(v->d_munits.reserve(sizeof(MfmaUnit) * units.size()));
     OSK_HIP(v->d_seg_split.reserve(sizeof(void*) * ns));
     OSK_HIP(v->d_seg_xsqrt.reserve(sizeof(void*) * ns));
-    OSK_HIP(v->d_seg_vrow.reserve(sizeof(int64_t) * ns));
     OSK_HIP(v->d_shard_unit_begin.reserve(sizeof(int32_t) * (v->n_shards + 1)));
     OSK_HIP(v->d_shard_maxnorm2.reserve(sizeof(float) * v->n_shards));
     OSK_HIP(hipMemcpyAsync(v->d_munits.p, units.data(), sizeof(MfmaUnit) * units.size(), hipMemcpyHostToDevice, st));
     OSK_HIP(hipMemcpyAsync(v->d_seg_split.p, splits.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
     OSK_HIP(hipMemcpyAsync(v->d_seg_xsqrt.p, xsq.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
-    OSK_HIP(hipMemcpyAsync(v->d_seg_vrow.p, vrow.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice, st));
     OSK_HIP(hipMemcpyAsync(v->d_shard_unit_begin.p, shard_list_begin.data(), sizeof(int32_t) * (v->n_shards + 1),
                            hipMemcpyHostToDevice, st));
     OSK_HIP(hipMemcpyAsync(v->d_shard_maxnorm2.p, shard_max.data(), sizeof(float) * v->n_shards,
@@ -803,6 +829,154 @@ int32_t batched_search(osk_view* v, int nq, int k, int UP, const uint64_t* const
     return OSK_OK;
 }
 
+// The segment's int8 copy + per-row bound terms for the certified prefilter.  Built once.
+int32_t ensure_sq8_seg(osk_seg* s, hipStream_t st) {
+    std::lock_guard<std::mutex> lk(s->mu);
+    if (s->d_q8) return OSK_OK;
+    const int u8 = (s->dim + 15) / 16;
+    void* q8 = nullptr;
+    hipError_t e = hipMalloc(&q8, (size_t)std::max<int64_t>(1, s->n_rows) * u8 * 16);
+    if (e != hipSuccess) {
+        set_error(std::string("hipMalloc of the int8 prefilter copy failed: ") + hipGetErrorString(e));
+        return OSK_ERR_OOM;
+    }
+    float4* aux = nullptr;
+    e = hipMalloc(&aux, (size_t)std::max<int64_t>(1, s->n_rows) * sizeof(float4));
+    if (e != hipSuccess) {
+        (void)hipFree(q8);
+        set_error(std::string("hipMalloc of the prefilter bound terms failed: ") + hipGetErrorString(e));
+        return OSK_ERR_OOM;
+    }
+    OSK_HIP(launch_sq8_quantize(static_cast<const float4*>(s->d_rows), s->n_rows, s->units, s->units, u8, q8, aux,
+                                0, st));
+    OSK_HIP(hipStreamSynchronize(st));
+    s->d_q8 = q8;
+    s->d_q8aux = aux;
+    s->units8 = u8;
+    return OSK_OK;
+}
+
+int32_t ensure_sq8(osk_view* v, hipStream_t st) {
+    if (v->sq8_ready) return OSK_OK;
+    const int ns = (int)v->segs.size();
+    std::vector<const void*> rows(ns);
+    std::vector<const float4*> aux(ns);
+    for (int i = 0; i < ns; ++i) {
+        int32_t rc = ensure_sq8_seg(v->segs[i], st);
+        if (rc) return rc;
+        rows[i] = v->segs[i]->d_q8;
+        aux[i] = v->segs[i]->d_q8aux;
+    }
+    v->units8 = (v->dim + 15) / 16;
+    // rounding bounds of the fp32 device order over n = 4·units products: γ_n ≤ n·2^-24
+    // (any summation tree); gam = γ_n/2 with a 2× margin, g2 ≥ γ_{n+2} with margin.
+    const double n = 4.0 * v->units;
+    v->sq8_gam = (float)((n + 8.0) * std::ldexp(1.0, -24));
+    v->sq8_g2 = (float)((n + 8.0) * std::ldexp(1.0, -23));
+    v->sq8_cos_slack = (float)((n + 8.0) * std::ldexp(1.0, -23) + std::ldexp(1.0, -18));
+    OSK_HIP(v->d_sq8_rows.reserve(sizeof(void*) * ns));
+    OSK_HIP(v->d_sq8_aux.reserve(sizeof(void*) * ns));
+    OSK_HIP(hipMemcpyAsync(v->d_sq8_rows.p, rows.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
+    OSK_HIP(hipMemcpyAsync(v->d_sq8_aux.p, aux.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
+    OSK_HIP(hipStreamSynchronize(st));
+    v->sq8_ready = true;
+    return OSK_OK;
+}
+
+// Certified int8 prefilter search (float32, k ≤ kKQ): int8 scan → settle (exact re-score +
+// certificate) → exact fp32 scan of the queries whose certificate failed, gated on the device so
+// that nothing waits on the host (every fallback workgroup exits at once when no query failed).
+// ws_q / ws_qnorm hold the padded fp32 queries and |q|² (device order).
+int32_t sq8_search(osk_view* v, int nq, int k, int UP, const uint64_t* const* d_accept, uint64_t* d_shard_keys,
+                   int32_t* d_shard_counts, int64_t* d_visited, hipStream_t st) {
+    int32_t rc = ensure_sq8(v, st);
+    if (rc) return rc;
+    const int u8 = v->units8, S = v->n_shards;
+    const int nq_pad = (nq + kMaxNQ - 1) / kMaxNQ * kMaxNQ;
+    OSK_HIP(v->ws_q8.reserve((size_t)nq_pad * u8 * 16));
+    OSK_HIP(v->ws_qc.reserve(sizeof(float4) * nq_pad));
+    OSK_HIP(launch_sq8_quantize(v->ws_q.as<float4>(), nq_pad, v->units, UP, u8, v->ws_q8.p, v->ws_qc.as<float4>(),
+                                1, st));
+    if (v->sim == SIM_COSINE)
+        OSK_HIP(launch_row_norms_f32(v->ws_q.as<float4>(), nq_pad, UP, v->cfg, v->ws_qnorm.as<float>(), st));
+    const size_t nl = (size_t)nq * v->n_tiles * kKQ;
+    OSK_HIP(v->ws_sq8cand.reserve(sizeof(uint64_t) * nl));
+    OSK_HIP(v->ws_sq8lb.reserve(sizeof(uint32_t) * nl));
+    Sq8Params p{};
+    p.segs = v->d_segs.as<SegDev>();
+    p.tiles = v->d_tiles.as<TileDev>();
+    p.accept = d_accept;
+    p.rows8 = v->d_sq8_rows.as<const int4*>();
+    p.aux = v->d_sq8_aux.as<const float4*>();
+    p.seg_vrow = v->d_seg_vrow.as<int64_t>();
+    p.cand = v->ws_sq8cand.as<uint64_t>();
+    p.cand_lb = v->ws_sq8lb.as<uint32_t>();
+    p.visited = reinterpret_cast<unsigned long long*>(d_visited);
+    p.n_tiles = v->n_tiles;
+    p.units8 = u8;
+    p.sim = v->sim;
+    p.gam = v->sq8_gam;
+    p.g2 = v->sq8_g2;
+    p.cos_slack = v->sq8_cos_slack;
+    for (int q0 = 0; q0 < nq; q0 += kMaxNQ) {
+        p.q0 = q0;
+        p.q_count = std::min(kMaxNQ, nq - q0);
+        p.q8 = v->ws_q8.as<int4>() + (size_t)q0 * u8;
+        p.qc = v->ws_qc.as<float4>() + q0;
+        p.qn_dev = v->ws_qnorm.as<float>() + q0;
+        OSK_HIP(launch_sq8_scan(p.q_count, p, st));
+    }
+    rc = profile_end(v, st);
+    if (rc) return rc;
+    OSK_HIP(v->ws_flags.reserve(sizeof(int) * nq));
+    OSK_HIP(hipMemsetAsync(v->ws_flags.p, 0, sizeof(int) * nq, st));
+    SettleParams sp{};
+    sp.segs = v->d_segs.as<SegDev>();
+    sp.seg_vrow = v->d_seg_vrow.as<int64_t>();
+    sp.shard_tile_begin = v->d_shard_tile_begin.as<int32_t>();
+    sp.cand = p.cand;
+    sp.cand_lb = p.cand_lb;
+    sp.q = v->ws_q.p;
+    sp.qnorm = v->ws_qnorm.as<float>();
+    sp.shard_keys = d_shard_keys;
+    sp.shard_counts = d_shard_counts;
+    sp.flags = v->ws_flags.as<int>();
+    sp.counters = v->d_counters.as<unsigned long long>();
+    sp.n_tiles = v->n_tiles;
+    sp.n_shards = S;
+    sp.n_segs = (int)v->segs.size();
+    sp.units = v->units;
+    sp.k = k;
+    sp.sim = v->sim;
+    sp.force_fail = g_tuning.sq8_force_fallback;
+    OSK_HIP(launch_sq8_settle(v->cfg, nq, sp, st));
+    v->sq8_calls += 1;
+    // exact fallback, gated per query on the device
+    OSK_HIP(v->ws_cand.reserve(sizeof(uint64_t) * (size_t)nq * v->n_tiles * k));
+    ScanParams fp{};
+    fp.segs = v->d_segs.as<SegDev>();
+    fp.tiles = v->d_tiles.as<TileDev>();
+    fp.accept = d_accept;
+    fp.cand = v->ws_cand.as<uint64_t>();
+    fp.visited = nullptr;
+    fp.n_tiles = v->n_tiles;
+    fp.units = v->units;
+    fp.k = k;
+    fp.sim = v->sim;
+    fp.dim = v->dim;
+    fp.gate = v->ws_flags.as<int>();
+    for (int q0 = 0; q0 < nq; q0 += kMaxNQ) {
+        fp.q0 = q0;
+        fp.q_count = std::min(kMaxNQ, nq - q0);
+        fp.q = v->ws_q.as<char>() + (size_t)q0 * UP * 16;
+        fp.qnorm_f = v->ws_qnorm.as<float>() + q0;
+        OSK_HIP(launch_scan(ENC_FLOAT32, v->cfg, fp.q_count, fp, st));
+    }
+    OSK_HIP(launch_merge_shards(v->ws_cand.as<uint64_t>(), v->n_tiles, v->d_shard_tile_begin.as<int32_t>(), S, nq,
+                                k, d_shard_keys, d_shard_counts, st, v->ws_flags.as<int>()));
+    return OSK_OK;
+}
+
 // Core of osk_view_search_device (caller holds no lock; device already set).
 int32_t view_search_device(osk_view* v, const void* d_queries, int nq, int k,
                            const uint64_t* const* d_accept, uint64_t* d_shard_keys,
@@ -833,9 +1007,13 @@ int32_t view_search_device(osk_view* v, const void* d_queries, int nq, int k,
 
     const bool batched = v->enc == ENC_FLOAT32 && g_tuning.mfma_min_batch > 0 &&
                          nq >= g_tuning.mfma_min_batch && k <= kKC - 4;
+    const bool prefilter = !batched && v->enc == ENC_FLOAT32 && g_tuning.sq8 && k <= kKQ;
     int32_t rc;
+    if (prefilter && (rc = ensure_sq8(v, st)) != OSK_OK) return rc;   // one-time build, outside the timing
     if (v->profile && (rc = profile_begin(v, st)) != OSK_OK) return rc;
-    if (batched) {
+    if (prefilter) {
+        rc = sq8_search(v, nq, k, UP, d_accept, d_shard_keys, d_shard_counts, d_visited, st);
+    } else if (batched) {
         // |q|² in the device lane layout: approx transforms, the re-score (COSINE) and the bound
         OSK_HIP(launch_row_norms_f32(v->ws_q.as<float4>(), nq, UP, v->cfg, v->ws_qnorm.as<float>(), st));
         rc = batched_search(v, nq, k, UP, d_accept, d_shard_keys, d_shard_counts, d_visited, st);
@@ -920,7 +1098,9 @@ int32_t osk_view_debug_copy(osk_view* v, const char* name, void* host, int64_t b
     std::lock_guard<std::mutex> lk(v->mu);
     const std::string n(name);
     const DevBuf* b = n == "akeys" ? &v->ws_akeys : n == "cand_a" ? &v->ws_cand_a : n == "flags" ? &v->ws_flags
-                    : n == "qsplit" ? &v->ws_qsplit : n == "qnorm" ? &v->ws_qnorm : nullptr;
+                    : n == "qsplit" ? &v->ws_qsplit : n == "qnorm" ? &v->ws_qnorm
+                    : n == "sq8cand" ? &v->ws_sq8cand : n == "sq8lb" ? &v->ws_sq8lb : n == "qc" ? &v->ws_qc
+                    : nullptr;
     OSK_REQUIRE(b != nullptr, "unknown buffer");
     OSK_REQUIRE((size_t)bytes <= b->cap, "bytes exceed the buffer");
     OSK_HIP(hipMemcpy(host, b->p, bytes, hipMemcpyDeviceToHost));
@@ -934,6 +1114,28 @@ int32_t osk_view_stats(osk_view* v, int64_t* batched_calls, int64_t* fallback_qu
     std::lock_guard<std::mutex> lk(v->mu);
     *batched_calls = v->mfma_calls;
     *fallback_queries = v->mfma_fallback_queries;
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
+    OSK_GUARD_BEGIN
+    OSK_REQUIRE(v != nullptr && name != nullptr && value != nullptr, "null argument");
+    int32_t rc = check_device(v->device);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(v->mu);
+    const std::string n(name);
+    if (n == "mfma_calls") *value = v->mfma_calls;
+    else if (n == "mfma_fallback_queries") *value = v->mfma_fallback_queries;
+    else if (n == "sq8_calls") *value = v->sq8_calls;
+    else if (n == "sq8_fallback_queries" || n == "sq8_rescored_rows") {
+        unsigned long long c[4];
+        OSK_HIP(hipMemcpy(c, v->d_counters.p, sizeof(c), hipMemcpyDeviceToHost));
+        *value = (int64_t)(n == "sq8_fallback_queries" ? c[0] : c[1]);
+    } else {
+        set_error("unknown counter: " + n);
+        return OSK_ERR_INVALID;
+    }
     return OSK_OK;
     OSK_GUARD_END
 }

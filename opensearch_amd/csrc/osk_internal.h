@@ -42,6 +42,7 @@ struct ScanParams {
     int k;
     int sim;
     int dim;
+    const int* gate;                 // fallback re-scan: skip the launch unless some query's flag is set
 };
 
 constexpr int kBlock = 256;          // 4 wavefronts per workgroup
@@ -105,6 +106,64 @@ hipError_t launch_max_norm2(const float* xn, int64_t n, unsigned* out, hipStream
 hipError_t launch_mfma_cand(const MfmaParams& p, int n_qblocks, bool pilot, hipStream_t s);
 hipError_t launch_rescore(int cfg, int nq, const RescoreParams& p, hipStream_t s);
 
+// ---- certified int8 prefilter (osk_sq8.hip) ----
+// A float32 segment keeps an int8 copy (per-row symmetric scale) and per-row bound terms.  The
+// prefilter scan streams the int8 copy (¼ of the bytes), bounds every row's device-order fp32 score
+// from above and below, and keeps per tile the kKQ rows with the highest upper bound; the settle
+// kernel re-scores exactly the rows that can still reach the shard's top k and proves the rest
+// cannot.  Results are bit-identical to the fp32 streaming scan.
+constexpr int kKQ = 16;              // per-tile candidate list of the prefilter (k ≤ kKQ)
+constexpr int kSettleCap = 4096;     // candidates re-scored per (query, shard) before the fallback
+
+struct Sq8Params {
+    const SegDev* segs;
+    const TileDev* tiles;
+    const uint64_t* const* accept;
+    const int4* const* rows8;        // per segment: int8 rows [n_rows][units8] 16-B units
+    const float4* const* aux;        // per segment: {scale, scale·|q8|, |x − scale·q8|, |x|²} per row
+    const int64_t* seg_vrow;         // view row of each segment's ord 0
+    const int4* q8;                  // this launch's int8 queries [NQ][units8]
+    const float4* qc;                // this launch's query terms {scale, |b − s·q8|, s·|q8| + |b − s·q8|, |b|²}
+    const float* qn_dev;             // this launch's |q|² in the device lane order (COSINE)
+    uint64_t* cand;                  // [nq][n_tiles][kKQ] keys (upper-bound score, view row)
+    uint32_t* cand_lb;               // [nq][n_tiles][kKQ] sortable lower-bound scores
+    unsigned long long* visited;
+    int n_tiles;
+    int q0;
+    int q_count;
+    int units8;
+    int sim;
+    float gam;                       // fp32 dot rounding: |dot_dev − x·b| ≤ gam·(|x|² + |b|²)
+    float g2;                        // fp32 d² rounding:  |d²_dev − d²| ≤ g2·d²
+    float cos_slack;                 // COSINE quick test: norm-order slack
+};
+
+struct SettleParams {
+    const SegDev* segs;
+    const int64_t* seg_vrow;
+    const int32_t* shard_tile_begin;
+    const uint64_t* cand;
+    const uint32_t* cand_lb;
+    const void* q;                   // padded fp32 queries [nq][UP] float4
+    const float* qnorm;              // |q|² device order (COSINE)
+    uint64_t* shard_keys;            // [nq][n_shards][k]
+    int32_t* shard_counts;
+    int* flags;                      // [nq] set when the query needs the exact fallback
+    unsigned long long* counters;    // [0] fallback queries, [1] rows re-scored
+    int n_tiles;
+    int n_shards;
+    int n_segs;
+    int units;
+    int k;
+    int sim;
+    int force_fail;                  // tests: send every query to the fallback
+};
+
+hipError_t launch_sq8_quantize(const float4* x, int64_t n, int units, int pitch, int units8, void* out8,
+                               float4* aux, int mode, hipStream_t s);
+hipError_t launch_sq8_scan(int nq, const Sq8Params& p, hipStream_t s);
+hipError_t launch_sq8_settle(int cfg, int nq, const SettleParams& p, hipStream_t s);
+
 int cfg_index(int units);
 
 // Process-wide tuning knobs (osk_tune_set; benchmarks and A/B runs only).
@@ -113,6 +172,8 @@ struct Tuning {
     int tiles_target = 4096;  // workgroup tiles per view (scan grid size)
     int mfma_min_batch = 16;  // batches ≥ this use the MFMA candidate path (0 = never)
     int mfma_units = 512;     // workgroup units of the MFMA candidate pass per view
+    int sq8 = 1;              // certified int8 prefilter for float32 batches below mfma_min_batch
+    int sq8_force_fallback = 0;   // tests: every prefiltered query takes the exact fallback
     int mfma_ablate = 0;      // A/B only: 1 skip the epilogue, 2 skip query staging, 4 skip corpus staging,
                               // 8 force the full staging epilogue, 16 skip the pilot pass
                               // (results are wrong and the exact fallback is skipped)
@@ -132,7 +193,7 @@ hipError_t launch_pad_rows(const void* src, int64_t src_pitch, void* dst, int64_
                            int64_t n_rows, int64_t row_bytes, hipStream_t s);
 hipError_t launch_merge_shards(const uint64_t* cand, int n_tiles, const int32_t* shard_tile_begin,
                                int n_shards, int nq, int k, uint64_t* shard_keys,
-                               int32_t* shard_counts, hipStream_t s);
+                               int32_t* shard_counts, hipStream_t s, const int* gate = nullptr);
 hipError_t launch_merge_coord(const uint64_t* shard_keys, const int32_t* shard_counts,
                               const int32_t* shard_index, int nq, int n_shards, int k, int from,
                               int size, float* scores, int32_t* docs, int32_t* shard_out,

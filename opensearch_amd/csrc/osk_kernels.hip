@@ -18,90 +18,9 @@
 //     0..k-1 of a register and a wave-uniform threshold; a row-group only costs a ballot unless a
 //     score beats the threshold (rare after the first few hundred rows).
 #include "osk_internal.h"
+#include "osk_wave.h"
 
 namespace osk {
-
-// ------------------------------------------------------------------------------------------------
-// wavefront helpers
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
-    uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, l);
-    uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
-    return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ uint64_t shfl_up1_64(uint64_t v) {
-    int lo = __shfl_up((int)(uint32_t)v, 1);
-    int hi = __shfl_up((int)(uint32_t)(v >> 32), 1);
-    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
-}
-
-// Insert key K (known to beat thr = lk[k-1]) into the wave's sorted-descending list held in
-// lanes 0..k-1 of lk.  Entries better than K form a prefix; K goes to lane `pos`, the tail
-// shifts down one lane and the old k-th entry falls off.
-__device__ __forceinline__ void wave_insert(uint64_t& lk, uint64_t& thr, uint64_t K, int lane,
-                                            int k) {
-    const uint64_t better = __ballot(lane < k && lk > K);
-    const int pos = __popcll(better);
-    const uint64_t up = shfl_up1_64(lk);
-    lk = lane < pos ? lk : (lane == pos ? K : up);
-    thr = readlane64(lk, k - 1);
-}
-
-// Offer each lane's key where `offer` holds; wave-uniform loop over the (few) lanes that beat thr.
-__device__ __forceinline__ void wave_offer(uint64_t key, bool offer, uint64_t& lk, uint64_t& thr,
-                                           int lane, int k) {
-    uint64_t m = __ballot(offer && key > thr);
-    while (m) {
-        const int src = __builtin_ctzll(m);
-        const uint64_t K = readlane64(key, src);
-        wave_insert(lk, thr, K, lane, k);
-        m &= ~(1ull << src);
-        m &= __ballot(offer && key > thr);
-    }
-}
-
-// Walk a wave's rows [wb, we) in groups of R (lane group g ↔ one row) and call
-// body(row, in_range, accepted_known).  Filter pushdown: with an accept bitset over a dense field
-// (doc == ord) the rows are taken 64 at a time, the accepted ones are compacted to the front of
-// the wave with one ds_permute, and only they are visited — at 1 % selectivity a wave touches ~1 %
-// of the rows instead of every row.  Otherwise every row is visited and the body checks accept.
-template <int R, class F>
-__device__ __forceinline__ void walk_rows(int64_t wb, int64_t we, const uint64_t* abits,
-                                          const int32_t* ord_to_doc, int lane, int g, F&& body) {
-    if (abits && !ord_to_doc) {
-        for (int64_t w0 = wb; w0 < we; w0 += 64) {
-            const int64_t word = w0 >> 6;
-            const int sh = (int)(w0 & 63);
-            uint64_t m = abits[word] >> sh;
-            if (sh && (word + 1) * 64 < we) m |= abits[word + 1] << (64 - sh);
-            if (we - w0 < 64) m &= (1ull << (we - w0)) - 1ull;
-            const int n = __popcll(m);
-            if (n == 0) continue;
-            // rank of each lane's bit among the set (or the unset) bits → a permutation that puts
-            // the positions of the n accepted rows into lanes 0..n-1
-            const bool bit = (m >> lane) & 1ull;
-            const int below = __popcll(m & ((1ull << lane) - 1ull));
-            const int dst = bit ? below : n + (lane - below);
-            const int pos = __builtin_amdgcn_ds_permute(dst << 2, lane);
-            for (int i0 = 0; i0 < n; i0 += R) {
-                const int idx = i0 + g;
-                const int pr = __shfl(pos, idx < 64 ? idx : 0);
-                body(w0 + pr, idx < n, true);
-            }
-        }
-    } else {
-        for (int64_t r0 = wb; r0 < we; r0 += R) body(r0 + g, r0 + g < we, false);
-    }
-}
-
-// Fold the lists of waves 1..3 (in LDS) into wave 0's list.
-__device__ __forceinline__ void block_fold(const uint64_t* lists /*[4][64]*/, uint64_t& lk,
-                                           uint64_t& thr, int lane, int k) {
-    for (int w = 1; w < 4; ++w) {
-        const uint64_t key = lane < k ? lists[w * 64 + lane] : 0ull;
-        wave_offer(key, true, lk, thr, lane, k);
-    }
-}
 
 // ------------------------------------------------------------------------------------------------
 // streaming scan, float32
@@ -124,6 +43,11 @@ __global__ __launch_bounds__(kBlock) void scan_f32(ScanParams p) {
     constexpr int R = 64 / L;                 // rows per wave-iteration
     constexpr int UP = L * V;                 // padded float4s per query
     constexpr bool QREG = NQ * V * 4 <= 64;   // query fragments in VGPRs, else read from LDS
+    if (p.gate) {   // exact fallback of the prefilter: run only if one of this launch's queries failed
+        bool any = false;
+        for (int b = 0; b < p.q_count; ++b) any |= p.gate[p.q0 + b] != 0;
+        if (!any) return;
+    }
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float4* sq = reinterpret_cast<float4*>(smem);
     uint64_t* slist = reinterpret_cast<uint64_t*>(smem + (QREG ? 0 : NQ * UP * 16));
@@ -250,6 +174,11 @@ __global__ __launch_bounds__(kBlock) void scan_i8(ScanParams p) {
     constexpr int R = 64 / L;
     constexpr int UP = L * V;
     constexpr bool QREG = NQ * V * 4 <= 64;
+    if (p.gate) {   // exact fallback of the prefilter: run only if one of this launch's queries failed
+        bool any = false;
+        for (int b = 0; b < p.q_count; ++b) any |= p.gate[p.q0 + b] != 0;
+        if (!any) return;
+    }
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int4* sq = reinterpret_cast<int4*>(smem);
     uint64_t* slist = reinterpret_cast<uint64_t*>(smem + (QREG ? 0 : NQ * UP * 16));
@@ -592,9 +521,11 @@ __global__ __launch_bounds__(kBlock) void merge_shards(const uint64_t* __restric
                                                        const int32_t* __restrict__ shard_tile_begin,
                                                        int n_shards, int k,
                                                        uint64_t* __restrict__ shard_keys,
-                                                       int32_t* __restrict__ shard_counts) {
+                                                       int32_t* __restrict__ shard_counts,
+                                                       const int* __restrict__ gate) {
     __shared__ uint64_t lists[4 * 64];
     const int s = blockIdx.x, b = blockIdx.y;
+    if (gate && !gate[b]) return;   // prefilter fallback: only the queries that failed
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int t0 = shard_tile_begin[s], t1 = shard_tile_begin[s + 1];
     const uint64_t* c = cand + ((size_t)b * n_tiles + t0) * k;
@@ -618,9 +549,9 @@ __global__ __launch_bounds__(kBlock) void merge_shards(const uint64_t* __restric
 
 hipError_t launch_merge_shards(const uint64_t* cand, int n_tiles, const int32_t* shard_tile_begin,
                                int n_shards, int nq, int k, uint64_t* shard_keys,
-                               int32_t* shard_counts, hipStream_t s) {
+                               int32_t* shard_counts, hipStream_t s, const int* gate) {
     hipLaunchKernelGGL(merge_shards, dim3(n_shards, nq), dim3(kBlock), 0, s, cand, n_tiles,
-                       shard_tile_begin, n_shards, k, shard_keys, shard_counts);
+                       shard_tile_begin, n_shards, k, shard_keys, shard_counts, gate);
     return hipGetLastError();
 }
 

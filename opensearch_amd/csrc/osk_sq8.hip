@@ -1,0 +1,480 @@
+// osk_sq8.hip — certified int8 prefilter for exact k-NN over float32 fields (batches below the MFMA
+// path).  Lucene analogue: a scalar-quantized copy next to the raw vectors, with the raw vectors
+// re-scored ([L] Lucene99ScalarQuantizedVectorsFormat + rescoring); here the re-scoring is exact and
+// a per-(query, shard) certificate proves that no row outside the re-scored set can enter the top k,
+// so the result is bit-identical to the fp32 streaming scan (osk_kernels.hip scan_f32) — the same
+// docs, the same score bits, the same tie order.
+//
+//   sq8_quantize  fp32 rows (or queries) → int8 (per-row symmetric scale s = max|x|/127) + the
+//                 per-row bound terms {s, s·|q|, |x − s·q|, |x|²}, computed in double, rounded up.
+//   sq8_scan      streams the int8 copy (¼ of the fp32 bytes): Σ q8_row·q8_query in exact int32
+//                 (v_dot4_i32_i8), then for every row an interval [lo, hi] that provably contains the
+//                 score the fp32 streaming scan computes for that row (quantisation error bound +
+//                 the fp32 rounding bound of the device summation order).  Per tile it keeps the
+//                 kKQ rows with the highest upper bound (keys) and their lower bounds.
+//   sq8_settle    per (query, shard): L = k-th best lower bound; every listed row whose upper bound
+//                 reaches L is re-scored with the streaming scan's exact arithmetic; a tile whose
+//                 list is full and whose last upper bound reaches L (a dropped row might qualify), or
+//                 more than kSettleCap candidates, sends the query to the exact fallback scan.
+//
+// Soundness: every non-re-scored row r has score(r) ≤ ub(r) < L ≤ T, where T is the
+// k-th exact score among the re-scored rows (the k rows that define L are all re-scored, and each
+// scores ≥ its lower bound ≥ L).  Strictness (ub < L) makes doc-order ties irrelevant.
+#include "osk_internal.h"
+#include "osk_wave.h"
+
+namespace osk {
+
+__device__ __forceinline__ float f32_round_up(double d) {   // d ≥ 0: smallest float ≥ d
+    float f = (float)d;
+    if ((double)f < d) f = __uint_as_float(__float_as_uint(f) + 1u);
+    return f;
+}
+
+// ------------------------------------------------------------------------------------------------
+// quantisation (one wave per row).  mode 0 (segment rows): aux = {s, s·|q|, |x − s·q|, |x|²};
+// mode 1 (queries): aux = {s, |b − s·q|, s·|q| + |b − s·q|, |b|²}.  |·| are real (double) norms
+// rounded up; |x|² is rounded to nearest (the kernels add slack for it).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void sq8_quantize(const float4* __restrict__ X, int64_t n, int units,
+                                                       int pitch, int units8, uint32_t* __restrict__ out8,
+                                                       float4* __restrict__ aux, int mode) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave_global = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) >> 6;
+    const int dw = units8 * 4;   // int8 dwords per row (≥ units: one dword per fp32 float4)
+    for (int64_t r = wave_global; r < n; r += n_waves) {
+        const float4* xr = X + r * pitch;
+        float m = 0.0f;
+        for (int f = lane; f < units; f += 64) {
+            const float4 x = xr[f];
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
+        }
+        for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+        const float s = m / 127.0f;
+        long long sq = 0;
+        double se = 0.0, sx = 0.0;
+        for (int d = lane; d < dw; d += 64) {
+            uint32_t packed = 0u;
+            if (d < units) {
+                const float4 x = xr[d];
+                const float xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    int qi = 0;
+                    if (s > 0.0f) qi = (int)fminf(fmaxf(rintf(xs[e] / s), -127.0f), 127.0f);
+                    packed |= ((uint32_t)qi & 0xFFu) << (8 * e);
+                    sq += (long long)(qi * qi);
+                    const double rr = (double)xs[e] - (double)s * (double)qi;   // exact in double
+                    se += rr * rr;
+                    sx += (double)xs[e] * (double)xs[e];
+                }
+            }
+            out8[r * dw + d] = packed;
+        }
+        for (int o = 32; o >= 1; o >>= 1) {
+            sq += __shfl_xor(sq, o);
+            se += __shfl_xor(se, o);
+            sx += __shfl_xor(sx, o);
+        }
+        if (lane == 0) {
+            const double A = (double)s * sqrt((double)sq) * (1.0 + 1e-12);
+            const double B = sqrt(se) * (1.0 + 1e-12);
+            aux[r] = mode == 0 ? make_float4(s, f32_round_up(A), f32_round_up(B), (float)sx)
+                               : make_float4(s, f32_round_up(B), f32_round_up((A + B) * (1.0 + 1e-12)), (float)sx);
+        }
+    }
+}
+
+hipError_t launch_sq8_quantize(const float4* x, int64_t n, int units, int pitch, int units8, void* out8,
+                               float4* aux, int mode, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    int64_t blocks = (n + 3) / 4;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(sq8_quantize, dim3((unsigned)blocks), dim3(kBlock), 0, s, x, n, units, pitch, units8,
+                       static_cast<uint32_t*>(out8), aux, mode);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// bounds
+// ------------------------------------------------------------------------------------------------
+// [lo, hi] ∋ the raw value the fp32 streaming scan computes for (row, query): its dot product
+// (DOT_PRODUCT / COSINE / MAXIMUM_INNER_PRODUCT) or its squared distance (EUCLIDEAN).
+//   x·b = s_x·s_b·I + e,  |e| ≤ s_x|q_x|·|δ_b| + |δ_x|·(s_b|q_b| + |δ_b|) = ax.y·qc.y + ax.z·qc.z
+//   dot:  |dot_dev − x·b| ≤ γ_n·|x||b| ≤ gam·(|x|² + |b|²)
+//   d²:   d² = |x|² + |b|² − 2x·b,  |d²_dev − d²| ≤ g2·d²
+// Every float operation below rounds by ≤ 2^-24 relative; the 2^-20 slack covers all of them.
+__device__ __forceinline__ void sq8_bounds(int sim, int I, float4 ax, float4 qc, float gam, float g2,
+                                           float& lo, float& hi) {
+    const float approx = (float)I * (ax.x * qc.x);
+    const float eq = fmaf(ax.y, qc.y, ax.z * qc.z);
+    if (sim == SIM_EUCLIDEAN) {
+        const float base = ax.w + qc.w;
+        const float sl = 0x1p-20f * (base + 2.0f * (fabsf(approx) + eq));
+        const float d2lo = base - 2.0f * (approx + eq) - sl;
+        const float d2hi = base - 2.0f * (approx - eq) + sl;
+        lo = fmaxf(d2lo, 0.0f) * (1.0f - g2);
+        hi = d2hi * (1.0f + g2);
+    } else {
+        const float e = eq + gam * (ax.w + qc.w);
+        const float sl = 0x1p-20f * (fabsf(approx) + e);
+        hi = approx + e + sl;
+        lo = approx - e - sl;
+    }
+}
+
+// Quick-reject threshold of a wave list whose worst upper-bound key is `thr` (0 = list not full):
+// a row whose bound fails sq8_pass has upper-bound score ≤ the list's worst score, so it cannot
+// enter the list (the precise test below decides the rest).
+//   EUCLIDEAN: d² threshold; COSINE: dot threshold per |x|; others: dot threshold.
+__device__ __forceinline__ float sq8_quick(int sim, uint64_t thr, float sqn, float cos_slack) {
+    if (thr == 0ull) return sim == SIM_EUCLIDEAN ? __builtin_inff() : -__builtin_inff();
+    const float t = key_score(thr);
+    switch (sim) {
+        case SIM_EUCLIDEAN: {
+            const float tm = t * (1.0f - 0x1p-16f);
+            return tm > 0.0f ? 1.0f / tm - 1.0f : __builtin_inff();
+        }
+        case SIM_MIP: {
+            const float tm = t * (1.0f - 0x1p-16f);
+            if (!(tm > 0.0f)) return -__builtin_inff();
+            return tm >= 1.0f ? tm - 1.0f : 1.0f - 1.0f / tm;
+        }
+        case SIM_DOT_PRODUCT: {
+            const float tm = t - 0x1p-16f * fabsf(t) - 0x1p-20f;
+            return 2.0f * tm - 1.0f;
+        }
+        default: {   // COSINE
+            const float tm = t - 0x1p-16f * fabsf(t) - 0x1p-20f;
+            return (2.0f * tm - 1.0f - cos_slack) * sqn;
+        }
+    }
+}
+__device__ __forceinline__ bool sq8_pass(int sim, float lo, float hi, float tq, float sx) {
+    if (sim == SIM_EUCLIDEAN) return !(lo > tq);
+    if (sim == SIM_COSINE) return !(hi < tq * sx);
+    return !(hi < tq);
+}
+
+__device__ __forceinline__ int4 load_i4_nt(const int4* p) {
+    typedef int i4v __attribute__((ext_vector_type(4)));
+    const i4v v = __builtin_nontemporal_load(reinterpret_cast<const i4v*>(p));
+    return make_int4(v.x, v.y, v.z, v.w);
+}
+
+// ------------------------------------------------------------------------------------------------
+// prefilter scan: a row is L lanes × V 16-byte int8 units; U row groups per wave-iteration are
+// loaded before any is reduced (≈ U·V·1 KiB in flight per wave).
+// ------------------------------------------------------------------------------------------------
+template <int L, int V, int NQ, int U>
+__global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
+    constexpr int R = 64 / L;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    uint64_t* slist = reinterpret_cast<uint64_t*>(smem);                      // [NQ][4][64]
+    uint32_t* splb = reinterpret_cast<uint32_t*>(smem + NQ * 4 * 64 * 8);    // [NQ][4][64]
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int t = lane & (L - 1), g = lane / L;
+    const TileDev tile = p.tiles[blockIdx.x];
+    const SegDev seg = p.segs[tile.seg];
+    const int4* __restrict__ X = p.rows8[tile.seg];
+    const float4* __restrict__ AX = p.aux[tile.seg];
+    const uint32_t vbase = (uint32_t)p.seg_vrow[tile.seg];
+    const int u8 = p.units8, sim = p.sim;
+
+    int4 qf[NQ][V];
+    float4 qc[NQ];
+    float qnd[NQ], sqn[NQ];
+#pragma unroll
+    for (int b = 0; b < NQ; ++b) {
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const int f = t + j * L;
+            qf[b][j] = f < u8 ? p.q8[b * u8 + f] : make_int4(0, 0, 0, 0);
+        }
+        qc[b] = p.qc[b];
+        qnd[b] = sim == SIM_COSINE ? p.qn_dev[b] : 0.0f;
+        sqn[b] = sqrtf(qnd[b]);
+    }
+
+    const int64_t rows = tile.row_end - tile.row_begin;
+    const int64_t per_wave = ((rows + 4 * R - 1) / (4 * R)) * R;
+    const int64_t wb = tile.row_begin + wave * per_wave;
+    const int64_t we = min(wb + per_wave, tile.row_end);
+    const uint64_t* abits = p.accept ? p.accept[tile.seg] : nullptr;
+
+    uint64_t lk[NQ], thr[NQ];
+    uint32_t lp[NQ];
+    float tq[NQ];
+#pragma unroll
+    for (int b = 0; b < NQ; ++b) {
+        lk[b] = 0ull;
+        thr[b] = 0ull;
+        lp[b] = 0u;
+        tq[b] = sq8_quick(sim, 0ull, 0.0f, 0.0f);
+    }
+    uint32_t nvis = 0;
+
+    auto process = [&](const int64_t (&row)[U], bool (&valid)[U], bool known) {
+        int4 xv[U][V];
+        float4 ax[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (valid[u] && abits && !known) {
+                const int32_t doc = seg.ord_to_doc ? seg.ord_to_doc[row[u]] : (int32_t)row[u];
+                valid[u] = (abits[doc >> 6] >> (doc & 63)) & 1ull;
+            }
+            const int4* xr = X + row[u] * u8;
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                const int f = t + j * L;
+                xv[u][j] = (valid[u] && f < u8) ? load_i4_nt(xr + f) : make_int4(0, 0, 0, 0);
+            }
+            ax[u] = valid[u] ? AX[row[u]] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            nvis += __popcll(__ballot(t == 0 && valid[u]));
+            const float sx = sim == SIM_COSINE ? sqrtf(ax[u].w) : 0.0f;
+#pragma unroll
+            for (int b = 0; b < NQ; ++b) {
+                int acc = 0;
+#pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    acc = __builtin_amdgcn_sdot4(xv[u][j].x, qf[b][j].x, acc, false);
+                    acc = __builtin_amdgcn_sdot4(xv[u][j].y, qf[b][j].y, acc, false);
+                    acc = __builtin_amdgcn_sdot4(xv[u][j].z, qf[b][j].z, acc, false);
+                    acc = __builtin_amdgcn_sdot4(xv[u][j].w, qf[b][j].w, acc, false);
+                }
+#pragma unroll
+                for (int m = 1; m < L; m <<= 1) acc += __shfl_xor(acc, m);
+                float lo, hi;
+                sq8_bounds(sim, acc, ax[u], qc[b], p.gam, p.g2, lo, hi);
+                const bool pass = valid[u] && sq8_pass(sim, lo, hi, tq[b], sx);
+                if (__ballot(pass && t == 0)) {   // wave-uniform: rare once the list has filled
+                    float xnd = 0.0f;
+                    if (sim == SIM_COSINE && pass) xnd = seg.xnorm_f[row[u]];
+                    const float ub = sim == SIM_EUCLIDEAN ? score_f32_l2(lo) : score_f32(sim, hi, qnd[b], xnd);
+                    const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qnd[b], xnd);
+                    const uint64_t key = pass ? make_key(ub, vbase + (uint32_t)row[u]) : 0ull;
+                    wave_offer2(key, float_to_sortable(lb), pass && t == 0, lk[b], lp[b], thr[b], lane, kKQ);
+                    tq[b] = sq8_quick(sim, thr[b], sqn[b], p.cos_slack);
+                }
+            }
+        }
+    };
+
+    if (abits && !seg.ord_to_doc) {
+        // filter pushdown: accepted rows of 64 compacted to the front of the wave (see walk_rows)
+        for (int64_t w0 = wb; w0 < we; w0 += 64) {
+            const int64_t word = w0 >> 6;
+            const int sh = (int)(w0 & 63);
+            uint64_t m = abits[word] >> sh;
+            if (sh && (word + 1) * 64 < we) m |= abits[word + 1] << (64 - sh);
+            if (we - w0 < 64) m &= (1ull << (we - w0)) - 1ull;
+            const int n = __popcll(m);
+            if (n == 0) continue;
+            const bool bit = (m >> lane) & 1ull;
+            const int below = __popcll(m & ((1ull << lane) - 1ull));
+            const int dst = bit ? below : n + (lane - below);
+            const int pos = __builtin_amdgcn_ds_permute(dst << 2, lane);
+            for (int i0 = 0; i0 < n; i0 += R * U) {
+                int64_t rr[U];
+                bool vv[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int idx = i0 + u * R + g;
+                    const int pr = __shfl(pos, idx < 64 ? idx : 0);
+                    rr[u] = w0 + pr;
+                    vv[u] = idx < n;
+                }
+                process(rr, vv, true);
+            }
+        }
+    } else {
+        for (int64_t r0 = wb; r0 < we; r0 += R * U) {
+            int64_t rr[U];
+            bool vv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                rr[u] = r0 + u * R + g;
+                vv[u] = rr[u] < we;
+            }
+            process(rr, vv, false);
+        }
+    }
+
+    if (p.visited && p.q0 == 0 && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
+
+#pragma unroll
+    for (int b = 0; b < NQ; ++b) {
+        slist[(b * 4 + wave) * 64 + lane] = lane < kKQ ? lk[b] : 0ull;
+        splb[(b * 4 + wave) * 64 + lane] = lp[b];
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+        for (int b = 0; b < NQ; ++b) {
+            for (int w = 1; w < 4; ++w) {
+                const uint64_t key = lane < kKQ ? slist[(b * 4 + w) * 64 + lane] : 0ull;
+                wave_offer2(key, splb[(b * 4 + w) * 64 + lane], true, lk[b], lp[b], thr[b], lane, kKQ);
+            }
+            if (b < p.q_count && lane < kKQ) {
+                const size_t o = ((size_t)(p.q0 + b) * p.n_tiles + blockIdx.x) * kKQ + lane;
+                p.cand[o] = lk[b];
+                p.cand_lb[o] = lp[b];
+            }
+        }
+    }
+}
+
+// int8 lane configs by 16-byte units per row: {L, V} (the int32 sums are exact: any order)
+static int sq8_cfg(int u8) {
+    return u8 <= 4 ? 0 : u8 <= 8 ? 1 : u8 <= 16 ? 2 : u8 <= 32 ? 3 : u8 <= 48 ? 4 : u8 <= 64 ? 5 : u8 <= 128 ? 6 : 7;
+}
+using Sq8Fn = void (*)(Sq8Params);
+#define OSK_SQ8_ROW(L, V) {sq8_scan<L, V, 1, 4>, sq8_scan<L, V, 2, 4>, sq8_scan<L, V, 4, 2>, sq8_scan<L, V, 8, 1>}
+static const Sq8Fn kSq8[8][4] = {OSK_SQ8_ROW(4, 1),  OSK_SQ8_ROW(8, 1),  OSK_SQ8_ROW(16, 1), OSK_SQ8_ROW(16, 2),
+                                 OSK_SQ8_ROW(16, 3), OSK_SQ8_ROW(16, 4), OSK_SQ8_ROW(32, 4), OSK_SQ8_ROW(64, 4)};
+
+hipError_t launch_sq8_scan(int nq, const Sq8Params& p, hipStream_t s) {
+    const int slot = nq <= 1 ? 0 : nq <= 2 ? 1 : nq <= 4 ? 2 : 3;
+    const int NQ = 1 << slot;
+    const size_t lds = (size_t)NQ * 4 * 64 * 12;
+    hipLaunchKernelGGL(kSq8[sq8_cfg(p.units8)][slot], dim3(p.n_tiles), dim3(kBlock), lds, s, p);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// settle: one 512-thread workgroup per (shard, query)
+// ------------------------------------------------------------------------------------------------
+constexpr int kSettleThreads = 512;
+
+template <int L, int V, bool L2K>
+__global__ __launch_bounds__(kSettleThreads) void sq8_settle(SettleParams p) {
+    constexpr int NW = kSettleThreads / 64, R = 64 / L, UP = L * V;
+    __shared__ uint64_t s_lists[NW * 64];
+    __shared__ uint32_t s_cand[kSettleCap];
+    __shared__ int s_nc, s_fail;
+    __shared__ uint32_t s_L;
+    const int s = blockIdx.x, q = blockIdx.y, S = p.n_shards;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int t = lane & (L - 1), g = lane / L;
+    const int k = p.k, sim = p.sim;
+    const int t0 = p.shard_tile_begin[s], t1 = p.shard_tile_begin[s + 1];
+    const size_t base = ((size_t)q * p.n_tiles + t0) * kKQ;
+    const uint64_t* __restrict__ E = p.cand + base;
+    const uint32_t* __restrict__ LB = p.cand_lb + base;
+    const int n = (t1 - t0) * kKQ;
+    if (tid == 0) {
+        s_nc = 0;
+        s_fail = p.force_fail;
+    }
+
+    // (a) L = the k-th best lower bound among the listed rows (0 when fewer than k are listed)
+    uint64_t lk = 0ull, thr = 0ull;
+    for (int b0 = wave * 64; b0 < n; b0 += kSettleThreads) {
+        const int i = b0 + lane;
+        const uint64_t key = i < n ? E[i] : 0ull;
+        const uint64_t lkey = key ? (((uint64_t)LB[i] << 32) | (uint32_t)i) : 0ull;
+        wave_offer(lkey, true, lk, thr, lane, k);
+    }
+    s_lists[wave * 64 + lane] = lane < k ? lk : 0ull;
+    __syncthreads();
+    if (wave == 0) {
+        for (int w = 1; w < NW; ++w) {
+            const uint64_t key = lane < k ? s_lists[w * 64 + lane] : 0ull;
+            wave_offer(key, true, lk, thr, lane, k);
+        }
+        if (lane == 0) s_L = (uint32_t)(thr >> 32);
+    }
+    __syncthreads();
+    const uint32_t Lb = s_L;
+
+    // (b) candidates: listed rows whose upper bound reaches L.  A full tile list whose last entry
+    // reaches L may have dropped a qualifying row → no certificate.
+    for (int i = tid; i < n; i += kSettleThreads) {
+        const uint64_t key = E[i];
+        if (!key || (uint32_t)(key >> 32) < Lb) continue;
+        if ((i % kKQ) == kKQ - 1) s_fail = 1;
+        const int slot = atomicAdd(&s_nc, 1);
+        if (slot < kSettleCap) s_cand[slot] = 0xFFFFFFFFu - (uint32_t)key;
+    }
+    __syncthreads();
+    const int nc = s_nc;
+    if (s_fail || nc > kSettleCap) {
+        if (tid == 0 && atomicOr(&p.flags[q], 1) == 0) atomicAdd(&p.counters[0], 1ull);
+        return;
+    }
+    if (tid == 0 && nc) atomicAdd(&p.counters[1], (unsigned long long)nc);
+
+    // (c) exact re-score with the streaming scan's arithmetic (same lane layout and fma order)
+    const float4* __restrict__ Q = reinterpret_cast<const float4*>(p.q) + (size_t)q * UP;
+    float4 qf[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) qf[j] = Q[t + j * L];
+    const float qn = (!L2K && sim == SIM_COSINE) ? p.qnorm[q] : 0.0f;
+    lk = 0ull;
+    thr = 0ull;
+    for (int i0 = wave * R; i0 < nc; i0 += NW * R) {
+        const int ci = i0 + g;
+        const bool valid = ci < nc;
+        const uint32_t vrow = s_cand[valid ? ci : 0];
+        int sg = 0;
+        for (int j = 1; j < p.n_segs; ++j)
+            if ((int64_t)vrow >= p.seg_vrow[j]) sg = j;
+        const SegDev seg = p.segs[sg];
+        const int64_t ord = (int64_t)vrow - p.seg_vrow[sg];
+        const int32_t doc = seg.ord_to_doc ? seg.ord_to_doc[ord] : (int32_t)ord;
+        const float4* xr = static_cast<const float4*>(seg.rows) + ord * p.units;
+        float ax = 0.f, ay = 0.f, az = 0.f, aw = 0.f;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const int f = t + j * L;
+            const float4 x = (valid && f < p.units) ? xr[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+            if constexpr (L2K) {
+                const float dx = x.x - qf[j].x, dy = x.y - qf[j].y, dz = x.z - qf[j].z, dw = x.w - qf[j].w;
+                ax = fmaf(dx, dx, ax); ay = fmaf(dy, dy, ay); az = fmaf(dz, dz, az); aw = fmaf(dw, dw, aw);
+            } else {
+                ax = fmaf(x.x, qf[j].x, ax); ay = fmaf(x.y, qf[j].y, ay);
+                az = fmaf(x.z, qf[j].z, az); aw = fmaf(x.w, qf[j].w, aw);
+            }
+        }
+        float sum = (ax + ay) + (az + aw);
+#pragma unroll
+        for (int m = 1; m < L; m <<= 1) sum += __shfl_xor(sum, m);
+        float sc;
+        if constexpr (L2K) sc = score_f32_l2(sum);
+        else sc = score_f32(sim, sum, qn, (sim == SIM_COSINE && valid) ? seg.xnorm_f[ord] : 0.0f);
+        const uint64_t key = valid ? make_key(sc, (uint32_t)(seg.doc_base + doc)) : 0ull;
+        wave_offer(key, t == 0, lk, thr, lane, k);
+    }
+    __syncthreads();
+    s_lists[wave * 64 + lane] = lane < k ? lk : 0ull;
+    __syncthreads();
+    if (wave == 0) {
+        for (int w = 1; w < NW; ++w) {
+            const uint64_t key = lane < k ? s_lists[w * 64 + lane] : 0ull;
+            wave_offer(key, true, lk, thr, lane, k);
+        }
+        const size_t o = (size_t)q * S + s;
+        if (lane < k) p.shard_keys[o * k + lane] = lk;
+        const int cnt = __popcll(__ballot(lane < k && lk != 0ull));
+        if (lane == 0) p.shard_counts[o] = cnt;
+    }
+}
+
+using SettleFn = void (*)(SettleParams);
+#define OSK_SETTLE_ROW(L, V) {sq8_settle<L, V, false>, sq8_settle<L, V, true>}
+static const SettleFn kSettle[9][2] = {OSK_SETTLE_ROW(4, 2),  OSK_SETTLE_ROW(8, 2),  OSK_SETTLE_ROW(8, 4),
+                                       OSK_SETTLE_ROW(16, 4), OSK_SETTLE_ROW(16, 8), OSK_SETTLE_ROW(16, 12),
+                                       OSK_SETTLE_ROW(32, 8), OSK_SETTLE_ROW(64, 8), OSK_SETTLE_ROW(64, 16)};
+
+hipError_t launch_sq8_settle(int cfg, int nq, const SettleParams& p, hipStream_t s) {
+    hipLaunchKernelGGL(kSettle[cfg][p.sim == SIM_EUCLIDEAN ? 1 : 0], dim3(p.n_shards, nq), dim3(kSettleThreads), 0, s,
+                       p);
+    return hipGetLastError();
+}
+
+}  // namespace osk

@@ -1,0 +1,110 @@
+// osk_wave.h — wavefront-level top-k helpers shared by the scan, prefilter and merge kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace osk {
+
+// ------------------------------------------------------------------------------------------------
+// wavefront helpers
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t shfl_up1_64(uint64_t v) {
+    int lo = __shfl_up((int)(uint32_t)v, 1);
+    int hi = __shfl_up((int)(uint32_t)(v >> 32), 1);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+// Insert key K (known to beat thr = lk[k-1]) into the wave's sorted-descending list held in
+// lanes 0..k-1 of lk.  Entries better than K form a prefix; K goes to lane `pos`, the tail
+// shifts down one lane and the old k-th entry falls off.
+__device__ __forceinline__ void wave_insert(uint64_t& lk, uint64_t& thr, uint64_t K, int lane,
+                                            int k) {
+    const uint64_t better = __ballot(lane < k && lk > K);
+    const int pos = __popcll(better);
+    const uint64_t up = shfl_up1_64(lk);
+    lk = lane < pos ? lk : (lane == pos ? K : up);
+    thr = readlane64(lk, k - 1);
+}
+
+// Offer each lane's key where `offer` holds; wave-uniform loop over the (few) lanes that beat thr.
+__device__ __forceinline__ void wave_offer(uint64_t key, bool offer, uint64_t& lk, uint64_t& thr,
+                                           int lane, int k) {
+    uint64_t m = __ballot(offer && key > thr);
+    while (m) {
+        const int src = __builtin_ctzll(m);
+        const uint64_t K = readlane64(key, src);
+        wave_insert(lk, thr, K, lane, k);
+        m &= ~(1ull << src);
+        m &= __ballot(offer && key > thr);
+    }
+}
+
+// wave_offer with a 32-bit payload riding along each list entry (the prefilter's lower bound).
+__device__ __forceinline__ void wave_offer2(uint64_t key, uint32_t pay, bool offer, uint64_t& lk,
+                                            uint32_t& lp, uint64_t& thr, int lane, int k) {
+    uint64_t m = __ballot(offer && key > thr);
+    while (m) {
+        const int src = __builtin_ctzll(m);
+        const uint64_t K = readlane64(key, src);
+        const uint32_t P = (uint32_t)__builtin_amdgcn_readlane((int)pay, src);
+        const uint64_t better = __ballot(lane < k && lk > K);
+        const int pos = __popcll(better);
+        const uint64_t up = shfl_up1_64(lk);
+        const uint32_t upp = (uint32_t)__shfl_up((int)lp, 1);
+        lk = lane < pos ? lk : (lane == pos ? K : up);
+        lp = lane < pos ? lp : (lane == pos ? P : upp);
+        thr = readlane64(lk, k - 1);
+        m &= ~(1ull << src);
+        m &= __ballot(offer && key > thr);
+    }
+}
+
+// Walk a wave's rows [wb, we) in groups of R (lane group g ↔ one row) and call
+// body(row, in_range, accepted_known).  Filter pushdown: with an accept bitset over a dense field
+// (doc == ord) the rows are taken 64 at a time, the accepted ones are compacted to the front of
+// the wave with one ds_permute, and only they are visited — at 1 % selectivity a wave touches ~1 %
+// of the rows instead of every row.  Otherwise every row is visited and the body checks accept.
+template <int R, class F>
+__device__ __forceinline__ void walk_rows(int64_t wb, int64_t we, const uint64_t* abits,
+                                          const int32_t* ord_to_doc, int lane, int g, F&& body) {
+    if (abits && !ord_to_doc) {
+        for (int64_t w0 = wb; w0 < we; w0 += 64) {
+            const int64_t word = w0 >> 6;
+            const int sh = (int)(w0 & 63);
+            uint64_t m = abits[word] >> sh;
+            if (sh && (word + 1) * 64 < we) m |= abits[word + 1] << (64 - sh);
+            if (we - w0 < 64) m &= (1ull << (we - w0)) - 1ull;
+            const int n = __popcll(m);
+            if (n == 0) continue;
+            // rank of each lane's bit among the set (or the unset) bits → a permutation that puts
+            // the positions of the n accepted rows into lanes 0..n-1
+            const bool bit = (m >> lane) & 1ull;
+            const int below = __popcll(m & ((1ull << lane) - 1ull));
+            const int dst = bit ? below : n + (lane - below);
+            const int pos = __builtin_amdgcn_ds_permute(dst << 2, lane);
+            for (int i0 = 0; i0 < n; i0 += R) {
+                const int idx = i0 + g;
+                const int pr = __shfl(pos, idx < 64 ? idx : 0);
+                body(w0 + pr, idx < n, true);
+            }
+        }
+    } else {
+        for (int64_t r0 = wb; r0 < we; r0 += R) body(r0 + g, r0 + g < we, false);
+    }
+}
+
+// Fold the lists of waves 1..3 (in LDS) into wave 0's list.
+__device__ __forceinline__ void block_fold(const uint64_t* lists /*[4][64]*/, uint64_t& lk,
+                                           uint64_t& thr, int lane, int k) {
+    for (int w = 1; w < 4; ++w) {
+        const uint64_t key = lane < k ? lists[w * 64 + lane] : 0ull;
+        wave_offer(key, true, lk, thr, lane, k);
+    }
+}
+
+}  // namespace osk

@@ -133,7 +133,11 @@ class LocalShards:
 
     def search(self, d_queries: int, nq: int, k: int, keys: torch.Tensor, counts: torch.Tensor,
                stream: int | None) -> None:
-        """Per-shard top-k of this rank's shards into keys [nq, s_pad, k] / counts [nq, s_pad]."""
+        """Per-shard top-k of this rank's shards into keys [nq, s_pad, k] / counts [nq, s_pad].
+        `stream` must be the handle of the torch stream the caller's tensors are used on, and not the
+        null stream (handle 0 = the library's own non-blocking stream, unordered with torch's work)."""
+        if not stream:
+            raise ValueError("pass a non-default torch stream handle (torch.cuda.Stream().cuda_stream)")
         sl = len(self.segs)
         if sl == self.s_pad:
             check(lib().osk_view_search_device(self.view, d_queries, nq, k, None, keys.data_ptr(),

@@ -350,6 +350,13 @@ class DeviceShardSet:
         check(lib().osk_view_stats(self.handle, C.byref(a), C.byref(b)))
         return a.value, b.value
 
+    def counter(self, name: str) -> int:
+        """A named counter of the view (osk_view_counter): "sq8_calls", "sq8_fallback_queries",
+        "sq8_rescored_rows", "mfma_calls", "mfma_fallback_queries"."""
+        v = C.c_int64()
+        check(lib().osk_view_counter(self.handle, name.encode(), C.byref(v)))
+        return v.value
+
     def close(self):
         if self._h.value:
             check(lib().osk_view_release(self._h))

@@ -1,0 +1,218 @@
+"""GPU parity of the certified int8 prefilter (osk_sq8.hip).
+
+The prefilter is the default path for float32 searches below the MFMA batch threshold with k ≤ 16.
+It must return exactly what the fp32 streaming scan returns — the same docs, the same score bits,
+the same tie order — which the oracle's ORDER_DEVICE restatement pins.  These tests compare the
+two paths (tune "sq8" 1 vs 0) and the oracle over similarities, ragged dims, batch sizes, k,
+filters, sparse doc maps, multi-segment multi-shard views, heavy ties and adversarial data where
+the certificate must fail and the gated exact fallback must answer instead.
+"""
+import numpy as np
+import pytest
+
+from opensearch_amd import _lib, lucene as LU
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SIMS = [LU.VectorSimilarityFunction(s) for s in range(4)]
+COS = LU.VectorSimilarityFunction.COSINE
+
+
+def corpus(n, dim, sim, seed):
+    dist = {0: 1, 1: 3, 2: 3, 3: 2}[int(sim)]
+    return O.synth(0, n, dim, seed, dist)
+
+
+def bits(a):
+    return np.asarray(a, np.float32).view(np.uint32)
+
+
+def with_tune(key, value, fn):
+    _lib.tune(key, value)
+    try:
+        return fn()
+    finally:
+        _lib.tune(key, {"sq8": 1, "sq8_force_fallback": 0}[key])
+
+
+def view_of(rows_list, sim, shard_of=None, shard_index=None):
+    """One DeviceShardSet over the given segments (segment i → shard shard_of[i])."""
+    shard_of = shard_of or [0] * len(rows_list)
+    n_shards = max(shard_of) + 1
+    shard_leaves = [[] for _ in range(n_shards)]
+    readers = []
+    bases = [0] * n_shards
+    for rows, s in zip(rows_list, shard_of):
+        r = LU.GpuFlatVectorsReader("v", rows, sim)
+        readers.append(r)
+        shard_leaves[s].append(LU.LeafReaderContext(len(shard_leaves[s]), bases[s], r))
+        bases[s] += len(rows)
+    return LU.DeviceShardSet(shard_leaves, shard_index), readers
+
+
+def close_all(ds, readers):
+    ds.close()
+    for r in readers:
+        r.close()
+
+
+def assert_same(a, b):
+    for x, y in zip(a, b):
+        x, y = np.asarray(x), np.asarray(y)
+        if x.dtype == np.float32:
+            assert np.array_equal(bits(x), bits(y)), (x, y)
+        else:
+            assert np.array_equal(x, y), (x, y)
+
+
+@pytest.mark.parametrize("dim", [1, 3, 17, 64, 96, 100, 128, 384, 768, 1000, 2048, 4096])
+@pytest.mark.parametrize("sim", SIMS, ids=lambda s: s.name)
+def test_prefilter_equals_exact_scan_and_oracle(dim, sim):
+    n = 3000 + dim % 11
+    rows = corpus(n, dim, sim, 3)
+    queries = corpus(5, dim, sim, 4)
+    r = LU.GpuFlatVectorsReader("v", rows, sim)
+    try:
+        on = r.search_batch(queries, 10)
+        off = with_tune("sq8", 0, lambda: r.search_batch(queries, 10))
+        assert_same(on, off)
+        s, d, c, v = on
+        for i in range(len(queries)):
+            os_, od, ov = O.exact_search(rows, queries[i], 10, int(sim))
+            assert np.array_equal(d[i, : c[i]], od) and np.array_equal(bits(s[i, : c[i]]), bits(os_))
+            assert v[i] == ov == n
+    finally:
+        r.close()
+
+
+@pytest.mark.parametrize("nq", [1, 2, 3, 5, 8, 9, 15])
+@pytest.mark.parametrize("k", [1, 7, 10, 16])
+def test_prefilter_batches_and_k(nq, k):
+    sim = COS
+    rows = corpus(20000, 768, sim, 5)
+    queries = corpus(nq, 768, sim, 6)
+    ds, readers = view_of([rows[:9000], rows[9000:15000], rows[15000:]], sim, [0, 1, 1])
+    try:
+        on = ds.search(queries, k, 0, k)
+        off = with_tune("sq8", 0, lambda: ds.search(queries, k, 0, k))
+        assert_same(on, off)
+        assert ds.counter("sq8_calls") >= 1
+        assert ds.counter("sq8_fallback_queries") == 0
+    finally:
+        close_all(ds, readers)
+
+
+@pytest.mark.parametrize("sim", SIMS, ids=lambda s: s.name)
+def test_prefilter_certifies_without_fallback_on_random_data(sim):
+    """On well-spread data every query is certified and only a few rows per shard are re-scored."""
+    rows = corpus(60000, 256, sim, 7)
+    queries = corpus(8, 256, sim, 8)
+    ds, readers = view_of([rows[i * 15000:(i + 1) * 15000] for i in range(4)], sim, [0, 1, 2, 3])
+    try:
+        ds.search(queries, 10, 0, 10)
+        assert ds.counter("sq8_fallback_queries") == 0
+        rescored = ds.counter("sq8_rescored_rows")
+        assert 8 * 4 * 10 <= rescored <= 8 * 4 * 2000, rescored
+    finally:
+        close_all(ds, readers)
+
+
+def test_forced_fallback_is_exact():
+    sim = LU.VectorSimilarityFunction.EUCLIDEAN
+    rows = corpus(12000, 128, sim, 9)
+    queries = corpus(11, 128, sim, 10)
+    ds, readers = view_of([rows[:5000], rows[5000:]], sim, [0, 1], [1, 0])
+    try:
+        off = with_tune("sq8", 0, lambda: ds.search(queries, 10, 0, 10))
+        forced = with_tune("sq8_force_fallback", 1, lambda: ds.search(queries, 10, 0, 10))
+        assert_same(forced, off)
+        assert ds.counter("sq8_fallback_queries") == len(queries)
+        on = ds.search(queries, 10, 0, 10)
+        assert_same(on, off)
+        assert ds.counter("sq8_fallback_queries") == len(queries)
+    finally:
+        close_all(ds, readers)
+
+
+@pytest.mark.parametrize("sim", SIMS, ids=lambda s: s.name)
+def test_prefilter_heavy_ties(sim):
+    """Every vector 3×, queries equal to rows: exact ties broken by lower doc, certified or not."""
+    base = corpus(700, 96, sim, 11)
+    rows = np.concatenate([base, base[::-1], base])
+    queries = np.concatenate([base[:3], corpus(3, 96, sim, 12)])
+    r = LU.GpuFlatVectorsReader("v", rows, sim)
+    try:
+        on = r.search_batch(queries, 16)
+        off = with_tune("sq8", 0, lambda: r.search_batch(queries, 16))
+        assert_same(on, off)
+        for i in range(len(queries)):
+            os_, od, _ = O.exact_search(rows, queries[i], 16, int(sim))
+            assert np.array_equal(on[1][i], od)
+    finally:
+        r.close()
+
+
+def test_prefilter_constant_and_zero_rows():
+    for sim in [LU.VectorSimilarityFunction.EUCLIDEAN, LU.VectorSimilarityFunction.DOT_PRODUCT,
+                LU.VectorSimilarityFunction.MAXIMUM_INNER_PRODUCT]:
+        rows = np.ones((900, 40), np.float32)
+        rows[100:200] = 0.0
+        q = np.stack([np.ones(40, np.float32), np.zeros(40, np.float32)])
+        r = LU.GpuFlatVectorsReader("v", rows, sim)
+        try:
+            assert_same(r.search_batch(q, 10), with_tune("sq8", 0, lambda: r.search_batch(q, 10)))
+        finally:
+            r.close()
+
+
+def test_prefilter_adversarial_dynamic_range():
+    """One huge component per row makes the int8 copy nearly useless: the bound is wide, many rows
+    qualify, and the result must still be exact (certified with many candidates, or the fallback)."""
+    rng = np.random.default_rng(13)
+    rows = rng.standard_normal((5000, 64)).astype(np.float32) * 1e-3
+    rows[:, 0] = 1000.0
+    queries = rng.standard_normal((4, 64)).astype(np.float32)
+    for sim in SIMS:
+        r = LU.GpuFlatVectorsReader("v", rows, sim)
+        try:
+            assert_same(r.search_batch(queries, 10), with_tune("sq8", 0, lambda: r.search_batch(queries, 10)))
+        finally:
+            r.close()
+
+
+@pytest.mark.parametrize("selectivity", [0.0, 0.002, 0.01, 0.1, 0.5, 1.0])
+def test_prefilter_with_filters_and_sparse_docs(selectivity):
+    sim = COS
+    rng = np.random.default_rng(int(selectivity * 1000) + 1)
+    n = 8000
+    rows = corpus(n, 768, sim, 14)
+    queries = corpus(3, 768, sim, 15)
+    dense = LU.GpuFlatVectorsReader("v", rows, sim)
+    docs = np.sort(rng.choice(20000, n, replace=False)).astype(np.int32)
+    sparse = LU.GpuFlatVectorsReader("v", rows, sim, ord_to_doc=docs, max_doc=20000)
+    try:
+        acc = O.bits_from_bool(rng.random(n) < selectivity)
+        on = dense.search_batch(queries, 10, acc)
+        assert_same(on, with_tune("sq8", 0, lambda: dense.search_batch(queries, 10, acc)))
+        live = O.bits_from_bool(rng.random(20000) < max(selectivity, 0.05))
+        on = sparse.search_batch(queries, 10, live)
+        assert_same(on, with_tune("sq8", 0, lambda: sparse.search_batch(queries, 10, live)))
+        for i in range(len(queries)):
+            os_, od, ov = O.exact_search(rows, queries[i], 10, int(sim), ord_to_doc=docs, accept_bits=live)
+            assert np.array_equal(on[1][i, : on[2][i]], od) and on[3][i] == ov
+    finally:
+        dense.close()
+        sparse.close()
+
+
+def test_prefilter_multi_shard_from_size():
+    sim = LU.VectorSimilarityFunction.DOT_PRODUCT
+    segs = [corpus(n, 128, sim, 20 + i) for i, n in enumerate([3000, 1, 2500, 64, 4000])]
+    ds, readers = view_of(segs, sim, [0, 0, 1, 2, 2], [2, 0, 1])
+    queries = corpus(6, 128, sim, 30)
+    try:
+        for k, f, sz in [(10, 0, 10), (10, 5, 5), (16, 3, 13), (4, 0, 4)]:
+            assert_same(ds.search(queries, k, f, sz), with_tune("sq8", 0, lambda: ds.search(queries, k, f, sz)))
+    finally:
+        close_all(ds, readers)

@@ -52,6 +52,7 @@ def run(view, queries, batch, steps, warmup, accept_ptrs=None, k=10):
     S = view.n_shards
     keys = torch.empty((batch, S, k), dtype=torch.int64, device="cuda")
     cnt = torch.empty((batch, S), dtype=torch.int32, device="cuda")
+    torch.cuda.set_stream(torch.cuda.Stream())   # non-null: 0 would mean the library's own stream
     stream = torch.cuda.current_stream().cuda_stream
     nq_pool = queries.shape[0] // batch
     acc = None if accept_ptrs is None else accept_ptrs.data_ptr()

@@ -51,6 +51,7 @@ def main():
     qs = torch.from_numpy(synth_host(0, B, dim, 43, _lib.DIST_NORMALISH_UNIT)).cuda()
     keys = torch.empty((B, nsh, 10), dtype=torch.int64, device="cuda")
     cnt = torch.empty((B, nsh), dtype=torch.int32, device="cuda")
+    torch.cuda.set_stream(torch.cuda.Stream())   # non-null: 0 would mean the library's own stream
     stream = torch.cuda.current_stream().cuda_stream
     variants = [(ab, u) for ab in [int(x) for x in a.ablate.split(",")] for u in views]
     res = {v: [] for v in variants}

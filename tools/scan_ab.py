@@ -54,6 +54,7 @@ def main():
     qs = torch.from_numpy(synth_host(0, max(batches) * 4, dim, 43, _lib.DIST_NORMALISH_UNIT)).cuda()
     keys = torch.empty((max(batches), nsh, 10), dtype=torch.int64, device="cuda")
     cnt = torch.empty((max(batches), nsh), dtype=torch.int32, device="cuda")
+    torch.cuda.set_stream(torch.cuda.Stream())   # non-null: 0 would mean the library's own stream
     stream = torch.cuda.current_stream().cuda_stream
     variants = [(nt, t, b) for nt in [int(x) for x in a.nt.split(",")] for t in views for b in batches]
     res = {v: [] for v in variants}
