@@ -887,18 +887,19 @@ int32_t ensure_sq8(osk_view* v, hipStream_t st) {
 // certificate) → exact fp32 scan of the queries whose certificate failed, gated on the device so
 // that nothing waits on the host (every fallback workgroup exits at once when no query failed).
 // ws_q / ws_qnorm hold the padded fp32 queries and |q|² (device order).
-int32_t sq8_search(osk_view* v, int nq, int k, int UP, const uint64_t* const* d_accept, uint64_t* d_shard_keys,
-                   int32_t* d_shard_counts, int64_t* d_visited, hipStream_t st) {
+int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, const uint64_t* const* d_accept,
+                   uint64_t* d_shard_keys, int32_t* d_shard_counts, int64_t* d_visited, hipStream_t st) {
     int32_t rc = ensure_sq8(v, st);
     if (rc) return rc;
     const int u8 = v->units8, S = v->n_shards;
     const int nq_pad = (nq + kMaxNQ - 1) / kMaxNQ * kMaxNQ;
-    OSK_HIP(v->ws_q8.reserve((size_t)nq_pad * u8 * 16));
-    OSK_HIP(v->ws_qc.reserve(sizeof(float4) * nq_pad));
-    OSK_HIP(launch_sq8_quantize(v->ws_q.as<float4>(), nq_pad, v->units, UP, u8, v->ws_q8.p, v->ws_qc.as<float4>(),
-                                1, st));
-    if (v->sim == SIM_COSINE)
-        OSK_HIP(launch_row_norms_f32(v->ws_q.as<float4>(), nq_pad, UP, v->cfg, v->ws_qnorm.as<float>(), st));
+    OSK_HIP(v->ws_q8.reserve((size_t)3 * nq_pad * u8 * 16));
+    OSK_HIP(v->ws_qc.reserve(sizeof(float4) * 2 * nq_pad));
+    OSK_HIP(v->ws_flags.reserve(sizeof(int) * nq));
+    // one launch: padded fp32 queries, |q|² (device order), int8 + int16 query planes, flags = 0
+    OSK_HIP(launch_sq8_prep(v->cfg, static_cast<const float*>(d_queries), v->dim, nq, nq_pad, UP, u8,
+                            v->ws_q.as<float4>(), v->ws_qnorm.as<float>(), v->ws_q8.p, v->ws_qc.as<float4>(),
+                            v->ws_flags.as<int>(), st));
     const size_t nl = (size_t)nq * v->n_tiles * kKQ;
     OSK_HIP(v->ws_sq8cand.reserve(sizeof(uint64_t) * nl));
     OSK_HIP(v->ws_sq8lb.reserve(sizeof(uint32_t) * nl));
@@ -914,6 +915,7 @@ int32_t sq8_search(osk_view* v, int nq, int k, int UP, const uint64_t* const* d_
     p.visited = reinterpret_cast<unsigned long long*>(d_visited);
     p.n_tiles = v->n_tiles;
     p.units8 = u8;
+    p.plane_stride = (int64_t)nq_pad * u8;
     p.sim = v->sim;
     p.gam = v->sq8_gam;
     p.g2 = v->sq8_g2;
@@ -922,14 +924,12 @@ int32_t sq8_search(osk_view* v, int nq, int k, int UP, const uint64_t* const* d_
         p.q0 = q0;
         p.q_count = std::min(kMaxNQ, nq - q0);
         p.q8 = v->ws_q8.as<int4>() + (size_t)q0 * u8;
-        p.qc = v->ws_qc.as<float4>() + q0;
+        p.qc = v->ws_qc.as<float4>() + 2 * q0;
         p.qn_dev = v->ws_qnorm.as<float>() + q0;
         OSK_HIP(launch_sq8_scan(p.q_count, p, st));
     }
     rc = profile_end(v, st);
     if (rc) return rc;
-    OSK_HIP(v->ws_flags.reserve(sizeof(int) * nq));
-    OSK_HIP(hipMemsetAsync(v->ws_flags.p, 0, sizeof(int) * nq, st));
     SettleParams sp{};
     sp.segs = v->d_segs.as<SegDev>();
     sp.seg_vrow = v->d_seg_vrow.as<int64_t>();
@@ -999,20 +999,21 @@ int32_t view_search_device(osk_view* v, const void* d_queries, int nq, int k,
     OSK_HIP(v->ws_cand.reserve(sizeof(uint64_t) * (size_t)nq * v->n_tiles * k));
     OSK_HIP(v->ws_q.reserve((size_t)nq_pad * UP * 16));
     OSK_HIP(v->ws_qnorm.reserve(sizeof(float) * nq_pad));
-    // queries → padded unit layout (zeros past dim and for the dummy queries of the last launch)
-    // one launch: padded queries (the scan computes |q|² itself, in its own lane layout)
-    OSK_HIP(launch_prep_queries(d_queries, (int64_t)v->dim * elem, nq, v->ws_q.p, UP, nq_pad, st));
-
-    if (d_visited) OSK_HIP(hipMemsetAsync(d_visited, 0, sizeof(int64_t) * v->segs.size(), st));
-
     const bool batched = v->enc == ENC_FLOAT32 && g_tuning.mfma_min_batch > 0 &&
                          nq >= g_tuning.mfma_min_batch && k <= kKC - 4;
     const bool prefilter = !batched && v->enc == ENC_FLOAT32 && g_tuning.sq8 && k <= kKQ;
+    // queries → padded unit layout (zeros past dim and for the dummy queries of the last launch); the
+    // prefilter path does this inside its own fused prep launch
+    if (!prefilter)
+        OSK_HIP(launch_prep_queries(d_queries, (int64_t)v->dim * elem, nq, v->ws_q.p, UP, nq_pad, st));
+
+    if (d_visited) OSK_HIP(hipMemsetAsync(d_visited, 0, sizeof(int64_t) * v->segs.size(), st));
+
     int32_t rc;
     if (prefilter && (rc = ensure_sq8(v, st)) != OSK_OK) return rc;   // one-time build, outside the timing
     if (v->profile && (rc = profile_begin(v, st)) != OSK_OK) return rc;
     if (prefilter) {
-        rc = sq8_search(v, nq, k, UP, d_accept, d_shard_keys, d_shard_counts, d_visited, st);
+        rc = sq8_search(v, d_queries, nq, k, UP, d_accept, d_shard_keys, d_shard_counts, d_visited, st);
     } else if (batched) {
         // |q|² in the device lane layout: approx transforms, the re-score (COSINE) and the bound
         OSK_HIP(launch_row_norms_f32(v->ws_q.as<float4>(), nq, UP, v->cfg, v->ws_qnorm.as<float>(), st));

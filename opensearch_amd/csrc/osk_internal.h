@@ -122,8 +122,9 @@ struct Sq8Params {
     const int4* const* rows8;        // per segment: int8 rows [n_rows][units8] 16-B units
     const float4* const* aux;        // per segment: {scale, scale·|q8|, |x − scale·q8|, |x|²} per row
     const int64_t* seg_vrow;         // view row of each segment's ord 0
-    const int4* q8;                  // this launch's int8 queries [NQ][units8]
-    const float4* qc;                // this launch's query terms {scale, |b − s·q8|, s·|q8| + |b − s·q8|, |b|²}
+    const int4* q8;                  // this launch's first query in plane 0: int8 [NQ][units8]; planes 1, 2
+                                     // (int16 query t = 256·h + l as h and l) follow at plane_stride
+    const float4* qc;                // per query [2]: int8 / int16 terms {scale, |b − s·q|, s·|q| + |b − s·q|, |b|²}
     const float* qn_dev;             // this launch's |q|² in the device lane order (COSINE)
     uint64_t* cand;                  // [nq][n_tiles][kKQ] keys (upper-bound score, view row)
     uint32_t* cand_lb;               // [nq][n_tiles][kKQ] sortable lower-bound scores
@@ -132,6 +133,7 @@ struct Sq8Params {
     int q0;
     int q_count;
     int units8;
+    int64_t plane_stride;            // int4 units between query planes
     int sim;
     float gam;                       // fp32 dot rounding: |dot_dev − x·b| ≤ gam·(|x|² + |b|²)
     float g2;                        // fp32 d² rounding:  |d²_dev − d²| ≤ g2·d²
@@ -162,6 +164,8 @@ struct SettleParams {
 hipError_t launch_sq8_quantize(const float4* x, int64_t n, int units, int pitch, int units8, void* out8,
                                float4* aux, int mode, hipStream_t s);
 hipError_t launch_sq8_scan(int nq, const Sq8Params& p, hipStream_t s);
+hipError_t launch_sq8_prep(int cfg, const float* src, int dim, int nq, int nq_pad, int UP, int units8, float4* qpad,
+                           float* qnorm, void* q8, float4* qc, int* flags, hipStream_t s);
 hipError_t launch_sq8_settle(int cfg, int nq, const SettleParams& p, hipStream_t s);
 
 int cfg_index(int units);

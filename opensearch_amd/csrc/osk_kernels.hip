@@ -560,8 +560,10 @@ hipError_t launch_merge_shards(const uint64_t* cand, int n_tiles, const int32_t*
 // hits (the shard collector's numDocs cut); hits are ranked by (score desc, shardIndex asc, doc asc)
 // and ranks [from, from+size) are emitted.  Σ shard hits → total hits; max top score → max score.
 // ------------------------------------------------------------------------------------------------
-constexpr int kCoordMax = 4096;   // shard hits considered per query
+constexpr int kCoordMax = 4096;   // shard hits considered per query (n_shards · min(k, from+size))
 
+// Slot (s, i) = hit i of shard s, a fixed position: every thread loads its slots' counts and keys at
+// once (no per-shard serialisation), then ranks each valid hit against all others.
 __global__ __launch_bounds__(kBlock) void merge_coord(const uint64_t* __restrict__ shard_keys,
                                                       const int32_t* __restrict__ shard_counts,
                                                       const int32_t* __restrict__ shard_index,
@@ -573,44 +575,50 @@ __global__ __launch_bounds__(kBlock) void merge_coord(const uint64_t* __restrict
                                                       int64_t* __restrict__ total_hits,
                                                       float* __restrict__ max_score) {
     __shared__ uint32_t s_su[kCoordMax];
-    __shared__ int32_t s_sidx[kCoordMax];
+    __shared__ int32_t s_sidx[kCoordMax];   // INT32_MIN = empty slot
     __shared__ int32_t s_doc[kCoordMax];
-    __shared__ int32_t s_n;
+    __shared__ int s_n;
     __shared__ unsigned long long s_total;
     __shared__ uint32_t s_max;
     const int b = blockIdx.x, tid = threadIdx.x;
     const int topn = min(k, from + size);
+    const int n_slots = n_shards * topn;
     if (tid == 0) { s_n = 0; s_total = 0ull; s_max = 0u; }
     __syncthreads();
+    const uint64_t* kb = shard_keys + (size_t)b * n_shards * k;
+    const int32_t* cb = shard_counts + (size_t)b * n_shards;
     for (int s = tid; s < n_shards; s += kBlock) {
-        const int c = shard_counts[(size_t)b * n_shards + s];
+        const int c = cb[s];
         atomicAdd(&s_total, (unsigned long long)c);
-        if (c > 0) atomicMax(&s_max, (uint32_t)(shard_keys[((size_t)b * n_shards + s) * k] >> 32));
+        if (c > 0) atomicMax(&s_max, (uint32_t)(kb[(size_t)s * k] >> 32));
     }
-    for (int s = 0; s < n_shards; ++s) {   // append in shard order (deterministic slots)
-        const int c = min(shard_counts[(size_t)b * n_shards + s], topn);
-        const int base = s_n;
-        for (int i = tid; i < c; i += kBlock) {
-            const int slot = base + i;
-            if (slot < kCoordMax) {
-                const uint64_t key = shard_keys[((size_t)b * n_shards + s) * k + i];
-                s_su[slot] = (uint32_t)(key >> 32);
-                s_sidx[slot] = shard_index[s];
-                s_doc[slot] = key_doc(key);
-            }
+    int mine = 0;
+    for (int slot = tid; slot < n_slots; slot += kBlock) {
+        const int s = slot / topn, i = slot - s * topn;
+        const bool valid = i < cb[s];
+        if (valid) {
+            const uint64_t key = kb[(size_t)s * k + i];
+            s_su[slot] = (uint32_t)(key >> 32);
+            s_doc[slot] = key_doc(key);
+            s_sidx[slot] = shard_index[s];
+            ++mine;
+        } else {
+            s_sidx[slot] = INT32_MIN;
         }
-        __syncthreads();
-        if (tid == 0) s_n = min(base + c, kCoordMax);
-        __syncthreads();
     }
-    const int n = s_n;
-    for (int i = tid; i < n; i += kBlock) {
+    if (mine) atomicAdd(&s_n, mine);
+    __syncthreads();
+    for (int i = tid; i < n_slots; i += kBlock) {
+        const int32_t si = s_sidx[i];
+        if (si == INT32_MIN) continue;
         const uint32_t su = s_su[i];
-        const int32_t si = s_sidx[i], d = s_doc[i];
+        const int32_t d = s_doc[i];
         int rank = 0;
-        for (int j = 0; j < n; ++j) {
-            const uint32_t sj = s_su[j];
-            rank += (sj > su) || (sj == su && (s_sidx[j] < si || (s_sidx[j] == si && s_doc[j] < d)));
+        for (int j = 0; j < n_slots; ++j) {
+            const int32_t sj = s_sidx[j];
+            if (sj == INT32_MIN) continue;
+            const uint32_t uj = s_su[j];
+            rank += (uj > su) || (uj == su && (sj < si || (sj == si && s_doc[j] < d)));
         }
         if (rank >= from && rank < from + size) {
             const size_t o = (size_t)b * size + (rank - from);
@@ -619,6 +627,7 @@ __global__ __launch_bounds__(kBlock) void merge_coord(const uint64_t* __restrict
             shard_out[o] = si;
         }
     }
+    const int n = s_n;
     const int got = max(0, min(size, n - from));
     for (int r = got + tid; r < size; r += kBlock) {
         const size_t o = (size_t)b * size + r;

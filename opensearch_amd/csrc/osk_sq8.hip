@@ -97,6 +97,112 @@ hipError_t launch_sq8_quantize(const float4* x, int64_t n, int units, int pitch,
 }
 
 // ------------------------------------------------------------------------------------------------
+// fused query preparation of the prefilter path (one wave per query, one launch):
+//   * the padded fp32 query (UP float4, zeros past dim; zero rows past nq) for the re-score and the
+//     exact fallback;
+//   * |q|² in the device lane order (identical bits to row_norms_f32 / scan_f32's in-kernel norm);
+//   * plane 0: int8 quantisation (s = max|b|/127) and its bound terms qc[2r];
+//   * planes 1, 2: an int16 quantisation t = 256·h + l (s = max|b|/32512, h ∈ [−127, 127],
+//     l ∈ [−128, 127]) and its bound terms qc[2r+1] — the query error becomes negligible, which
+//     halves the prefilter's bound for the batch-1/2 kernels;
+//   * flags[r] = 0.
+// ------------------------------------------------------------------------------------------------
+template <int L, int V>
+__global__ __launch_bounds__(kBlock) void sq8_prep(const float* __restrict__ src, int dim, int nq, int nq_pad,
+                                                   int UP, int units8, float4* __restrict__ qpad,
+                                                   float* __restrict__ qnorm, uint32_t* __restrict__ q8,
+                                                   float4* __restrict__ qc, int* __restrict__ flags) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    if (r >= nq_pad) return;
+    const bool real = r < nq;
+    const float* b = src + r * (int64_t)dim;
+    auto val = [&](int c) { return (real && c < dim) ? b[c] : 0.0f; };
+    const int dw = units8 * 4;
+    // padded fp32 copy + max|b|
+    float m = 0.0f;
+    for (int f = lane; f < UP; f += 64) {
+        const float4 v = make_float4(val(4 * f), val(4 * f + 1), val(4 * f + 2), val(4 * f + 3));
+        qpad[r * UP + f] = v;
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    // device-order |q|²: lane t of every L-lane group computes the same partial
+    {
+        const int t = lane & (L - 1);
+        float ax = 0.f, ay = 0.f, az = 0.f, aw = 0.f;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const int f = t + j * L;
+            const float x0 = val(4 * f), x1 = val(4 * f + 1), x2 = val(4 * f + 2), x3 = val(4 * f + 3);
+            ax = fmaf(x0, x0, ax); ay = fmaf(x1, x1, ay); az = fmaf(x2, x2, az); aw = fmaf(x3, x3, aw);
+        }
+        float sn = (ax + ay) + (az + aw);
+#pragma unroll
+        for (int o = 1; o < L; o <<= 1) sn += __shfl_xor(sn, o);
+        if (lane == 0) qnorm[r] = sn;
+    }
+    const float s8 = m / 127.0f, s16 = m / 32512.0f;
+    long long a8 = 0, a16 = 0;
+    double e8 = 0.0, e16 = 0.0, sx = 0.0;
+    uint32_t* p0 = q8 + r * dw;
+    uint32_t* p1 = q8 + ((int64_t)nq_pad + r) * dw;
+    uint32_t* p2 = q8 + (2 * (int64_t)nq_pad + r) * dw;
+    for (int d = lane; d < dw; d += 64) {
+        uint32_t w0 = 0u, w1 = 0u, w2 = 0u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float x = val(4 * d + e);
+            int q = 0, t = 0;
+            if (s8 > 0.0f) {
+                q = (int)fminf(fmaxf(rintf(x / s8), -127.0f), 127.0f);
+                t = (int)fminf(fmaxf(rintf(x / s16), -32512.0f), 32512.0f);
+            }
+            const int h = (t + 128) >> 8;            // floor((t + 128) / 256)
+            const int l = t - 256 * h;                // ∈ [−128, 127]
+            w0 |= ((uint32_t)q & 0xFFu) << (8 * e);
+            w1 |= ((uint32_t)h & 0xFFu) << (8 * e);
+            w2 |= ((uint32_t)l & 0xFFu) << (8 * e);
+            a8 += (long long)(q * q);
+            a16 += (long long)t * t;
+            const double r8 = (double)x - (double)s8 * (double)q;
+            const double r16 = (double)x - (double)s16 * (double)t;
+            e8 += r8 * r8;
+            e16 += r16 * r16;
+            sx += (double)x * (double)x;
+        }
+        p0[d] = w0;
+        p1[d] = w1;
+        p2[d] = w2;
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        a8 += __shfl_xor(a8, o);
+        a16 += __shfl_xor(a16, o);
+        e8 += __shfl_xor(e8, o);
+        e16 += __shfl_xor(e16, o);
+        sx += __shfl_xor(sx, o);
+    }
+    if (lane == 0) {
+        const double A8 = (double)s8 * sqrt((double)a8) * (1.0 + 1e-12), B8 = sqrt(e8) * (1.0 + 1e-12);
+        const double A16 = (double)s16 * sqrt((double)a16) * (1.0 + 1e-12), B16 = sqrt(e16) * (1.0 + 1e-12);
+        qc[2 * r] = make_float4(s8, f32_round_up(B8), f32_round_up((A8 + B8) * (1.0 + 1e-12)), (float)sx);
+        qc[2 * r + 1] = make_float4(s16, f32_round_up(B16), f32_round_up((A16 + B16) * (1.0 + 1e-12)), (float)sx);
+        if (real) flags[r] = 0;
+    }
+}
+
+using PrepFn = void (*)(const float*, int, int, int, int, int, float4*, float*, uint32_t*, float4*, int*);
+static const PrepFn kPrep[9] = {sq8_prep<4, 2>,  sq8_prep<8, 2>,  sq8_prep<8, 4>,  sq8_prep<16, 4>, sq8_prep<16, 8>,
+                                sq8_prep<16, 12>, sq8_prep<32, 8>, sq8_prep<64, 8>, sq8_prep<64, 16>};
+
+hipError_t launch_sq8_prep(int cfg, const float* src, int dim, int nq, int nq_pad, int UP, int units8, float4* qpad,
+                           float* qnorm, void* q8, float4* qc, int* flags, hipStream_t s) {
+    hipLaunchKernelGGL(kPrep[cfg], dim3((nq_pad + 3) / 4), dim3(kBlock), 0, s, src, dim, nq, nq_pad, UP, units8, qpad,
+                       qnorm, static_cast<uint32_t*>(q8), qc, flags);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
 // bounds
 // ------------------------------------------------------------------------------------------------
 // [lo, hi] ∋ the raw value the fp32 streaming scan computes for (row, query): its dot product
@@ -105,9 +211,9 @@ hipError_t launch_sq8_quantize(const float4* x, int64_t n, int units, int pitch,
 //   dot:  |dot_dev − x·b| ≤ γ_n·|x||b| ≤ gam·(|x|² + |b|²)
 //   d²:   d² = |x|² + |b|² − 2x·b,  |d²_dev − d²| ≤ g2·d²
 // Every float operation below rounds by ≤ 2^-24 relative; the 2^-20 slack covers all of them.
-__device__ __forceinline__ void sq8_bounds(int sim, int I, float4 ax, float4 qc, float gam, float g2,
+__device__ __forceinline__ void sq8_bounds(int sim, float I, float4 ax, float4 qc, float gam, float g2,
                                            float& lo, float& hi) {
-    const float approx = (float)I * (ax.x * qc.x);
+    const float approx = I * (ax.x * qc.x);
     const float eq = fmaf(ax.y, qc.y, ax.z * qc.z);
     if (sim == SIM_EUCLIDEAN) {
         const float base = ax.w + qc.w;
@@ -167,7 +273,7 @@ __device__ __forceinline__ int4 load_i4_nt(const int4* p) {
 // prefilter scan: a row is L lanes × V 16-byte int8 units; U row groups per wave-iteration are
 // loaded before any is reduced (≈ U·V·1 KiB in flight per wave).
 // ------------------------------------------------------------------------------------------------
-template <int L, int V, int NQ, int U>
+template <int L, int V, int NQ, int U, int P>
 __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
     constexpr int R = 64 / L;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -183,17 +289,27 @@ __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
     const uint32_t vbase = (uint32_t)p.seg_vrow[tile.seg];
     const int u8 = p.units8, sim = p.sim;
 
-    int4 qf[NQ][V];
+    // P = 1: the int8 query (plane 0); P = 2: the int16 query as planes h (1) and l (2), t = 256h + l
+    int4 qf[NQ][V], ql[P == 2 ? NQ : 1][P == 2 ? V : 1];
     float4 qc[NQ];
     float qnd[NQ], sqn[NQ];
 #pragma unroll
     for (int b = 0; b < NQ; ++b) {
 #pragma unroll
         for (int j = 0; j < V; ++j) {
+            // clamped index + mask (a select between the global pointer and a zero local would live
+            // in scratch)
             const int f = t + j * L;
-            qf[b][j] = f < u8 ? p.q8[b * u8 + f] : make_int4(0, 0, 0, 0);
+            const int fc = f < u8 ? f : 0;
+            const int msk = f < u8 ? -1 : 0;
+            int4 v = p.q8[(P == 1 ? 0 : p.plane_stride) + b * u8 + fc];
+            qf[b][j] = make_int4(v.x & msk, v.y & msk, v.z & msk, v.w & msk);
+            if constexpr (P == 2) {
+                v = p.q8[2 * p.plane_stride + b * u8 + fc];
+                ql[b][j] = make_int4(v.x & msk, v.y & msk, v.z & msk, v.w & msk);
+            }
         }
-        qc[b] = p.qc[b];
+        qc[b] = p.qc[2 * b + (P - 1)];
         qnd[b] = sim == SIM_COSINE ? p.qn_dev[b] : 0.0f;
         sqn[b] = sqrtf(qnd[b]);
     }
@@ -216,7 +332,23 @@ __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
     }
     uint32_t nvis = 0;
 
-    auto process = [&](const int64_t (&row)[U], bool (&valid)[U], bool known) {
+    // filt = false: rows base + u·R + g (< we); filt = true: the compacted accepted rows of the
+    // 64-row window at base (lanes' positions in `pos`), entries i0 + u·R + g of n
+    auto process = [&](int64_t base, bool filt, int i0, int n, int pos) {
+        int64_t row[U];
+        bool valid[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (filt) {
+                const int idx = i0 + u * R + g;
+                row[u] = base + __shfl(pos, idx < 64 ? idx : 0);
+                valid[u] = idx < n;
+            } else {
+                row[u] = base + u * R + g;
+                valid[u] = row[u] < we;
+            }
+        }
+        const bool known = filt;
         int4 xv[U][V];
         float4 ax[U];
 #pragma unroll
@@ -239,18 +371,29 @@ __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
             const float sx = sim == SIM_COSINE ? sqrtf(ax[u].w) : 0.0f;
 #pragma unroll
             for (int b = 0; b < NQ; ++b) {
-                int acc = 0;
+                int acc = 0, acc2 = 0;
 #pragma unroll
                 for (int j = 0; j < V; ++j) {
                     acc = __builtin_amdgcn_sdot4(xv[u][j].x, qf[b][j].x, acc, false);
                     acc = __builtin_amdgcn_sdot4(xv[u][j].y, qf[b][j].y, acc, false);
                     acc = __builtin_amdgcn_sdot4(xv[u][j].z, qf[b][j].z, acc, false);
                     acc = __builtin_amdgcn_sdot4(xv[u][j].w, qf[b][j].w, acc, false);
+                    if constexpr (P == 2) {
+                        acc2 = __builtin_amdgcn_sdot4(xv[u][j].x, ql[b][j].x, acc2, false);
+                        acc2 = __builtin_amdgcn_sdot4(xv[u][j].y, ql[b][j].y, acc2, false);
+                        acc2 = __builtin_amdgcn_sdot4(xv[u][j].z, ql[b][j].z, acc2, false);
+                        acc2 = __builtin_amdgcn_sdot4(xv[u][j].w, ql[b][j].w, acc2, false);
+                    }
                 }
 #pragma unroll
-                for (int m = 1; m < L; m <<= 1) acc += __shfl_xor(acc, m);
+                for (int m = 1; m < L; m <<= 1) {
+                    acc += __shfl_xor(acc, m);
+                    if constexpr (P == 2) acc2 += __shfl_xor(acc2, m);
+                }
+                // Σ q_x·t = 256·Σ q_x·h + Σ q_x·l (exact ints; one fma rounding, inside the slack)
+                const float I = P == 2 ? fmaf((float)acc, 256.0f, (float)acc2) : (float)acc;
                 float lo, hi;
-                sq8_bounds(sim, acc, ax[u], qc[b], p.gam, p.g2, lo, hi);
+                sq8_bounds(sim, I, ax[u], qc[b], p.gam, p.g2, lo, hi);
                 const bool pass = valid[u] && sq8_pass(sim, lo, hi, tq[b], sx);
                 if (__ballot(pass && t == 0)) {   // wave-uniform: rare once the list has filled
                     float xnd = 0.0f;
@@ -279,30 +422,10 @@ __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
             const int below = __popcll(m & ((1ull << lane) - 1ull));
             const int dst = bit ? below : n + (lane - below);
             const int pos = __builtin_amdgcn_ds_permute(dst << 2, lane);
-            for (int i0 = 0; i0 < n; i0 += R * U) {
-                int64_t rr[U];
-                bool vv[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int idx = i0 + u * R + g;
-                    const int pr = __shfl(pos, idx < 64 ? idx : 0);
-                    rr[u] = w0 + pr;
-                    vv[u] = idx < n;
-                }
-                process(rr, vv, true);
-            }
+            for (int i0 = 0; i0 < n; i0 += R * U) process(w0, true, i0, n, pos);
         }
     } else {
-        for (int64_t r0 = wb; r0 < we; r0 += R * U) {
-            int64_t rr[U];
-            bool vv[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                rr[u] = r0 + u * R + g;
-                vv[u] = rr[u] < we;
-            }
-            process(rr, vv, false);
-        }
+        for (int64_t r0 = wb; r0 < we; r0 += R * U) process(r0, false, 0, 0, 0);
     }
 
     if (p.visited && p.q0 == 0 && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
@@ -334,7 +457,7 @@ static int sq8_cfg(int u8) {
     return u8 <= 4 ? 0 : u8 <= 8 ? 1 : u8 <= 16 ? 2 : u8 <= 32 ? 3 : u8 <= 48 ? 4 : u8 <= 64 ? 5 : u8 <= 128 ? 6 : 7;
 }
 using Sq8Fn = void (*)(Sq8Params);
-#define OSK_SQ8_ROW(L, V) {sq8_scan<L, V, 1, 4>, sq8_scan<L, V, 2, 4>, sq8_scan<L, V, 4, 2>, sq8_scan<L, V, 8, 1>}
+#define OSK_SQ8_ROW(L, V) {sq8_scan<L, V, 1, 4, 2>, sq8_scan<L, V, 2, 4, 2>, sq8_scan<L, V, 4, 2, 1>, sq8_scan<L, V, 8, 1, 1>}
 static const Sq8Fn kSq8[8][4] = {OSK_SQ8_ROW(4, 1),  OSK_SQ8_ROW(8, 1),  OSK_SQ8_ROW(16, 1), OSK_SQ8_ROW(16, 2),
                                  OSK_SQ8_ROW(16, 3), OSK_SQ8_ROW(16, 4), OSK_SQ8_ROW(32, 4), OSK_SQ8_ROW(64, 4)};
 
@@ -349,7 +472,7 @@ hipError_t launch_sq8_scan(int nq, const Sq8Params& p, hipStream_t s) {
 // ------------------------------------------------------------------------------------------------
 // settle: one 512-thread workgroup per (shard, query)
 // ------------------------------------------------------------------------------------------------
-constexpr int kSettleThreads = 512;
+constexpr int kSettleThreads = 1024;
 
 template <int L, int V, bool L2K>
 __global__ __launch_bounds__(kSettleThreads) void sq8_settle(SettleParams p) {
@@ -428,11 +551,18 @@ __global__ __launch_bounds__(kSettleThreads) void sq8_settle(SettleParams p) {
         const int64_t ord = (int64_t)vrow - p.seg_vrow[sg];
         const int32_t doc = seg.ord_to_doc ? seg.ord_to_doc[ord] : (int32_t)ord;
         const float4* xr = static_cast<const float4*>(seg.rows) + ord * p.units;
-        float ax = 0.f, ay = 0.f, az = 0.f, aw = 0.f;
+        // the row norm is loaded with the row (not after the reduction: one memory round trip)
+        const float xn = (!L2K && sim == SIM_COSINE && valid) ? seg.xnorm_f[ord] : 0.0f;
+        float4 xv[V];
 #pragma unroll
         for (int j = 0; j < V; ++j) {
             const int f = t + j * L;
-            const float4 x = (valid && f < p.units) ? xr[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+            xv[j] = (valid && f < p.units) ? xr[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        float ax = 0.f, ay = 0.f, az = 0.f, aw = 0.f;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const float4 x = xv[j];
             if constexpr (L2K) {
                 const float dx = x.x - qf[j].x, dy = x.y - qf[j].y, dz = x.z - qf[j].z, dw = x.w - qf[j].w;
                 ax = fmaf(dx, dx, ax); ay = fmaf(dy, dy, ay); az = fmaf(dz, dz, az); aw = fmaf(dw, dw, aw);
@@ -446,7 +576,7 @@ __global__ __launch_bounds__(kSettleThreads) void sq8_settle(SettleParams p) {
         for (int m = 1; m < L; m <<= 1) sum += __shfl_xor(sum, m);
         float sc;
         if constexpr (L2K) sc = score_f32_l2(sum);
-        else sc = score_f32(sim, sum, qn, (sim == SIM_COSINE && valid) ? seg.xnorm_f[ord] : 0.0f);
+        else sc = score_f32(sim, sum, qn, xn);
         const uint64_t key = valid ? make_key(sc, (uint32_t)(seg.doc_base + doc)) : 0ull;
         wave_offer(key, t == 0, lk, thr, lane, k);
     }

@@ -40,15 +40,13 @@ def gather_shard_topk(keys: torch.Tensor, counts: torch.Tensor, world: int, grou
     """keys [nq, S_l, k] int64 (uint64 bit pattern), counts [nq, S_l] int32 on every rank (S_l padded
     to the same value everywhere) → gathered keys [nq, world·S_l, k], counts [nq, world·S_l]."""
     nq, sl, k = keys.shape
+    if world == 1:   # nothing to exchange
+        return keys, counts
     # concatenated along dim 0 (the layout both RCCL and gloo accept), viewed as [world, nq, …]
     gk = torch.empty((world * nq, sl, k), dtype=keys.dtype, device=keys.device)
     gc = torch.empty((world * nq, sl), dtype=counts.dtype, device=counts.device)
-    if world == 1:
-        gk.copy_(keys)
-        gc.copy_(counts)
-    else:
-        dist.all_gather_into_tensor(gk, keys.contiguous(), group=group)
-        dist.all_gather_into_tensor(gc, counts.contiguous(), group=group)
+    dist.all_gather_into_tensor(gk, keys.contiguous(), group=group)
+    dist.all_gather_into_tensor(gc, counts.contiguous(), group=group)
     gk = gk.view(world, nq, sl, k)
     gc = gc.view(world, nq, sl)
     return (gk.permute(1, 0, 2, 3).reshape(nq, world * sl, k).contiguous(),
