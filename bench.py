@@ -100,6 +100,7 @@ def main():
     ap.add_argument("--rows-per-shard", type=int, default=ROWS_PER_SHARD)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sq8", action="store_true", help="measure the fp32 streaming scan as the main path")
+    ap.add_argument("--tiles", type=int, default=0, help="A/B: workgroup tiles per view (osk_tune tiles_target)")
     # ≈10 s of CPU work on 16 host threads (≈1e8 row·queries/s measured): a bounded sample of C3
     ap.add_argument("--cpu-sample-rows", type=int, default=524_288)
     ap.add_argument("--cpu-queries", type=int, default=2048)
@@ -114,6 +115,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
+    if a.tiles:
+        _lib.tune("tiles_target", a.tiles)
     t0 = time.perf_counter()
     shards = D.LocalShards(rank, world, N_SHARDS, a.rows_per_shard, DIM, _lib.COSINE, _lib.FLOAT32, 42,
                            _lib.DIST_NORMALISH_UNIT, local_rank)
@@ -126,7 +129,7 @@ def main():
     B = a.batch
     keys = torch.empty((B, shards.s_pad, K), dtype=torch.int64, device="cuda")
     counts = torch.empty((B, shards.s_pad), dtype=torch.int32, device="cuda")
-    gsi = shards.global_shard_index.cuda()
+    xchg = D.ShardExchange(world, shards.s_pad, B, K, FROM, SIZE, shards.global_shard_index, device=local_rank)
     # One explicit stream for the library calls and torch's own ops (gather copy, events): the null
     # stream's handle is 0, which the C-ABI reads as "the library's own (non-blocking) stream".
     torch.cuda.set_stream(torch.cuda.Stream())
@@ -135,8 +138,7 @@ def main():
     def step(i):
         q = qpool[(i % n_pool) * B:(i % n_pool + 1) * B]
         shards.search(q.data_ptr(), B, K, keys, counts, stream)
-        gk, gc = D.gather_shard_topk(keys, counts, world)
-        return D.merge_gathered(gk, gc, gsi, K, FROM, SIZE, local_rank, stream)
+        return xchg(keys, stream)   # one all-gather of the per-shard top-k + device TopDocs.merge
 
     def timed(steps, warmup, offset=0):
         """W untimed steps, then K steps between barrier + synchronize; returns the max-over-ranks wall
@@ -177,7 +179,7 @@ def main():
         _lib.check(_lib.lib().osk_view_counter(shards.view, name.encode(), C.byref(v)))
         return v.value
 
-    prefilter = B < 16 and K <= 16 and not a.no_sq8
+    prefilter = B < 16 and K <= 12 and not a.no_sq8
     batched = B >= 16 and K <= 12           # the library's batched MFMA path (osk_tune "mfma_min_batch")
     _lib.tune("sq8", 0 if a.no_sq8 else 1)
     fb0, rs0, calls0 = counter("sq8_fallback_queries"), counter("sq8_rescored_rows"), counter("sq8_calls")
@@ -217,7 +219,7 @@ def main():
         s_el, s_scan, _, _ = timed(min(a.steps, 50), 2)
         mism = 0
         for i in range(min(8, n_pool)):
-            ref = step(i)
+            ref = [t.clone() for t in step(i)]
             _lib.tune("sq8", 1)
             got = step(i)
             _lib.tune("sq8", 0)

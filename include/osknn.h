@@ -159,6 +159,17 @@ int32_t osk_merge_device(int32_t device, const uint64_t* d_shard_keys,
                          int32_t* d_count, int64_t* d_total_hits, float* d_max_score,
                          void* stream);
 
+/* The same reduce straight over an all-gather's output (no counts, no re-layout): per-rank lists
+ * [n_queries][shards_per_rank][k] concatenated rank after rank, i.e. shard s = r·shards_per_rank + j
+ * of query q at ((r·n_queries + q)·shards_per_rank + j)·k.  A list's hits are its non-zero keys
+ * (best first, zero-padded, as osk_view_search_device writes them).  d_shard_index has
+ * n_ranks·shards_per_rank entries. */
+int32_t osk_merge_device_ranked(int32_t device, const uint64_t* d_keys, int32_t n_ranks,
+                                int32_t shards_per_rank, const int32_t* d_shard_index, int32_t n_queries,
+                                int32_t k, int32_t from, int32_t size, float* d_scores, int32_t* d_docs,
+                                int32_t* d_shard_out, int32_t* d_count, int64_t* d_total_hits,
+                                float* d_max_score, void* stream);
+
 /* Scan-kernel timing (benchmarks): enable/disable and reset; then read the summed duration of the
  * scan launches of every osk_view_search_device call since enabling (HIP events on the call's
  * stream) and the number of calls.  Enabling adds one event wait per call; keep it off in
@@ -169,20 +180,22 @@ int32_t osk_view_scan_time(osk_view* view, double* total_ms, int64_t* calls);
 /* Process-wide tuning knobs for benchmarks / A-B runs:
  *   "scan_nt"         0|1 non-temporal corpus loads in the streaming scan (default 1)
  *   "tiles_target"    workgroup tiles per view for the streaming scan (default 4096; at view create)
+ *   "tile_min_rows"   ...with at least this many rows per tile (default 1024; at view create)
  *   "mfma_min_batch"  batches of at least this many float32 queries (and k ≤ 12) take the batched
  *                     MFMA path (default 16; 0 = never)
  *   "mfma_units"      workgroup units of the MFMA candidate pass per view (default 512)
  *   "sq8"             0|1 certified int8 prefilter for float32 searches below mfma_min_batch with
- *                     k ≤ 16 (default 1; results are bit-identical either way)
- *   "sq8_force_fallback"  tests: every prefiltered query takes the exact fallback scan */
+ *                     k ≤ 12 (default 1; results are bit-identical either way)
+ *   "sq8_force_fallback"  tests: every tile of a prefiltered search is re-scanned exactly */
 int32_t osk_tune_set(const char* key, int64_t value);
 
 /* Batched-path counters of a view: searches that took the MFMA path, and queries among them whose
  * certificate failed and were recomputed by the exact streaming scan. */
 int32_t osk_view_stats(osk_view* view, int64_t* batched_calls, int64_t* fallback_queries);
 /* Named counters of a view: "mfma_calls", "mfma_fallback_queries" (as osk_view_stats),
- * "sq8_calls" (prefiltered searches), "sq8_fallback_queries" (queries whose certificate failed and
- * were answered by the exact scan), "sq8_rescored_rows" (rows re-scored exactly, all calls). */
+ * "sq8_calls" (prefiltered searches), "sq8_fallback_queries" (queries where some tile's candidate
+ * list overflowed past the certificate and the tile was re-scanned exactly), "sq8_exact_tiles"
+ * (such tiles), "sq8_rescored_rows" (rows re-scored exactly, all calls). */
 int32_t osk_view_counter(osk_view* view, const char* name, int64_t* value);
 /* Tests / debugging only: copy `bytes` of an internal buffer of the view's last search
  * ("akeys", "cand_a", "flags", "qsplit", "qnorm", "sq8cand",
@@ -210,6 +223,25 @@ int32_t osk_topdocs_merge(int32_t n_shards, const int32_t* shard_counts, const f
 
 /* Decode hit keys (host). */
 int32_t osk_decode_keys(const uint64_t* keys, int64_t n, float* scores, int32_t* docs);
+
+/* Shard-result wire format (host, no device): S/common/lucene/Lucene.java:407-447 writeTopDocs for a
+ * plain TopDocs (type byte 0 — what the shard collector of a k-NN DocAndScoreQuery returns):
+ *   byte 0 | vLong total_hits | vInt relation | int32 BE floatToIntBits(max_score) | vInt n |
+ *   n × (vInt doc, int32 BE floatToIntBits(score))
+ * with StreamOutput's encodings (libs/core/.../io/stream/StreamOutput.java:247-337,480-482).
+ *   relation  [L] TotalHits.Relation ordinal: 0 = EQUAL_TO, 1 = GREATER_THAN_OR_EQUAL_TO
+ *   out       NULL (cap 0) = size query only; *out_len = the encoded size either way
+ * total_hits < 0 fails like StreamOutput.writeVLong ("Negative longs unsupported, …"). */
+int32_t osk_topdocs_write(int64_t total_hits, int32_t relation, float max_score, int32_t n,
+                          const int32_t* docs, const float* scores, uint8_t* out, int64_t cap,
+                          int64_t* out_len);
+/* Lucene.readTopDocs (:314-357) for type 0; types 1/2 (field-sorted / collapsed docs, never a k-NN
+ * shard result) → OSK_ERR_UNSUPPORTED; malformed input (unknown type, invalid vInt/vLong, bad
+ * relation ordinal, negative count, truncation) → OSK_ERR_INVALID with StreamInput's message.
+ * *consumed (optional) = bytes read. */
+int32_t osk_topdocs_read(const uint8_t* buf, int64_t len, int64_t* total_hits, int32_t* relation,
+                         float* max_score, int32_t cap_hits, int32_t* n, int32_t* docs, float* scores,
+                         int64_t* consumed);
 
 #ifdef __cplusplus
 }

@@ -59,9 +59,12 @@ SIGNATURES = {
     "osk_view_release": (_I32, [_P]),
     "osk_view_search_device": (_I32, [_P, _P, _I32, _I32, _P, _P, _P, _P, _P]),
     "osk_merge_device": (_I32, [_I32, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
+    "osk_merge_device_ranked": (_I32, [_I32, _P, _I32, _I32, _P, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
     "osk_view_search": (_I32, [_P, _P, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]),
     "osk_topdocs_merge": (_I32, [_I32, _P, _P, _P, _I32, _P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     "osk_decode_keys": (_I32, [_P, _I64, _P, _P]),
+    "osk_topdocs_write": (_I32, [_I64, _I32, C.c_float, _I32, _P, _P, _P, _I64, _PI64]),
+    "osk_topdocs_read": (_I32, [_P, _I64, _PI64, _PI32, _PF, _I32, _PI32, _P, _P, _PI64]),
     "osk_view_profile": (_I32, [_P, _I32]),
     "osk_tune_set": (_I32, [C.c_char_p, _I64]),
     "osk_view_stats": (_I32, [_P, _PI64, _PI64]),

@@ -224,8 +224,12 @@ struct osk_view {
     bool sq8_ready = false;
     int units8 = 0;
     float sq8_gam = 0.f, sq8_g2 = 0.f, sq8_cos_slack = 0.f;
-    DevBuf d_sq8_rows, d_sq8_aux, d_counters;   // counters: [0] fallback queries, [1] rows re-scored
-    DevBuf ws_q8, ws_qc, ws_sq8cand, ws_sq8lb;
+    DevBuf d_sq8_rows, d_sq8_aux, d_counters;   // counters: SettleParams::counters
+    DevBuf ws_q8, ws_qc, ws_sq8cand, ws_sq8lb, ws_lbmax, ws_trace;
+    // settle slices: kSliceLists wave lists each, never spanning shards (an empty shard gets one
+    // empty slice so that its result is still written)
+    int n_slices = 0;
+    DevBuf d_slices, d_shard_slice_begin, ws_part;
     int64_t sq8_calls = 0;
     std::mutex mu;
     // scan-kernel timing (osk_view_profile): events bracket the scan launches on the search stream
@@ -351,9 +355,14 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         g_tuning.sq8 = value != 0;
     } else if (k == "sq8_force_fallback") {
         g_tuning.sq8_force_fallback = value != 0;
+    } else if (k == "settle_trace") {
+        g_tuning.settle_trace = value != 0;
     } else if (k == "tiles_target") {
         OSK_REQUIRE(value >= 1 && value <= (1 << 22), "tiles_target out of range");
         g_tuning.tiles_target = (int)value;
+    } else if (k == "tile_min_rows") {
+        OSK_REQUIRE(value >= 1 && value <= (1 << 24), "tile_min_rows out of range");
+        g_tuning.tile_min_rows = (int)value;
     } else {
         set_error("unknown tuning key: " + k);
         return OSK_ERR_INVALID;
@@ -504,7 +513,7 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
     const int R = 64 / kL[v->cfg];
     int64_t total = 0;
     for (int i = 0; i < n_segs; ++i) total += segs[i]->n_rows;
-    const int64_t min_rows = 4LL * R * 8;
+    const int64_t min_rows = std::max<int64_t>(4LL * R * 8, g_tuning.tile_min_rows);
     const int64_t target = std::max(1, g_tuning.tiles_target);
     const int64_t rows_per_tile = std::max<int64_t>(min_rows, (total + target - 1) / target);
     std::vector<TileDev> tiles;
@@ -868,6 +877,26 @@ int32_t ensure_sq8(osk_view* v, hipStream_t st) {
         aux[i] = v->segs[i]->d_q8aux;
     }
     v->units8 = (v->dim + 15) / 16;
+    {
+        std::vector<int4> sl;
+        std::vector<int32_t> ssb(v->n_shards + 1, 0);
+        for (int sh = 0; sh < v->n_shards; ++sh) {
+            ssb[sh] = (int32_t)sl.size();
+            const int l0 = 4 * v->shard_tile_begin[sh], l1 = 4 * v->shard_tile_begin[sh + 1];
+            if (l0 == l1) sl.push_back(make_int4(l0, l0, l0, l0));
+            for (int l = l0; l < l1; l += kSliceLists) {   // L groups: aligned chunks of kLGroupLists lists
+                const int ga = l0 + (l - l0) / kLGroupLists * kLGroupLists;
+                sl.push_back(make_int4(l, std::min(l + kSliceLists, l1), ga, std::min(ga + kLGroupLists, l1)));
+            }
+        }
+        ssb[v->n_shards] = (int32_t)sl.size();
+        v->n_slices = (int)sl.size();
+        OSK_HIP(v->d_slices.reserve(sizeof(int4) * sl.size()));
+        OSK_HIP(v->d_shard_slice_begin.reserve(sizeof(int32_t) * ssb.size()));
+        OSK_HIP(hipMemcpyAsync(v->d_slices.p, sl.data(), sizeof(int4) * sl.size(), hipMemcpyHostToDevice, st));
+        OSK_HIP(hipMemcpyAsync(v->d_shard_slice_begin.p, ssb.data(), sizeof(int32_t) * ssb.size(),
+                               hipMemcpyHostToDevice, st));
+    }
     // rounding bounds of the fp32 device order over n = 4·units products: γ_n ≤ n·2^-24
     // (any summation tree); gam = γ_n/2 with a 2× margin, g2 ≥ γ_{n+2} with margin.
     const double n = 4.0 * v->units;
@@ -883,9 +912,9 @@ int32_t ensure_sq8(osk_view* v, hipStream_t st) {
     return OSK_OK;
 }
 
-// Certified int8 prefilter search (float32, k ≤ kKQ): int8 scan → settle (exact re-score +
-// certificate) → exact fp32 scan of the queries whose certificate failed, gated on the device so
-// that nothing waits on the host (every fallback workgroup exits at once when no query failed).
+// Certified int8 prefilter search (float32, k ≤ kKQ): int8 scan → settle per slice of tiles (exact
+// re-score of the rows the certificate cannot exclude; a tile whose list overflowed is re-scanned
+// exactly inside the settle) → per-shard merge.  Nothing waits on the host.
 // ws_q / ws_qnorm hold the padded fp32 queries and |q|² (device order).
 int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, const uint64_t* const* d_accept,
                    uint64_t* d_shard_keys, int32_t* d_shard_counts, int64_t* d_visited, hipStream_t st) {
@@ -893,16 +922,17 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     if (rc) return rc;
     const int u8 = v->units8, S = v->n_shards;
     const int nq_pad = (nq + kMaxNQ - 1) / kMaxNQ * kMaxNQ;
-    OSK_HIP(v->ws_q8.reserve((size_t)3 * nq_pad * u8 * 16));
-    OSK_HIP(v->ws_qc.reserve(sizeof(float4) * 2 * nq_pad));
+    OSK_HIP(v->ws_q8.reserve((size_t)nq_pad * u8 * 16));
+    OSK_HIP(v->ws_qc.reserve(sizeof(float4) * nq_pad));
     OSK_HIP(v->ws_flags.reserve(sizeof(int) * nq));
-    // one launch: padded fp32 queries, |q|² (device order), int8 + int16 query planes, flags = 0
+    // one launch: padded fp32 queries, |q|² (device order), int8 queries + bound terms, flags = 0
     OSK_HIP(launch_sq8_prep(v->cfg, static_cast<const float*>(d_queries), v->dim, nq, nq_pad, UP, u8,
                             v->ws_q.as<float4>(), v->ws_qnorm.as<float>(), v->ws_q8.p, v->ws_qc.as<float4>(),
                             v->ws_flags.as<int>(), st));
-    const size_t nl = (size_t)nq * v->n_tiles * kKQ;
+    const size_t nl = (size_t)nq * 4 * v->n_tiles * kKQ;
     OSK_HIP(v->ws_sq8cand.reserve(sizeof(uint64_t) * nl));
     OSK_HIP(v->ws_sq8lb.reserve(sizeof(uint32_t) * nl));
+    OSK_HIP(v->ws_lbmax.reserve(sizeof(uint32_t) * (size_t)nq * 4 * v->n_tiles));
     Sq8Params p{};
     p.segs = v->d_segs.as<SegDev>();
     p.tiles = v->d_tiles.as<TileDev>();
@@ -912,10 +942,11 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     p.seg_vrow = v->d_seg_vrow.as<int64_t>();
     p.cand = v->ws_sq8cand.as<uint64_t>();
     p.cand_lb = v->ws_sq8lb.as<uint32_t>();
+    p.list_lbmax = v->ws_lbmax.as<uint32_t>();
     p.visited = reinterpret_cast<unsigned long long*>(d_visited);
     p.n_tiles = v->n_tiles;
+    p.n_lists = 4 * v->n_tiles;
     p.units8 = u8;
-    p.plane_stride = (int64_t)nq_pad * u8;
     p.sim = v->sim;
     p.gam = v->sq8_gam;
     p.g2 = v->sq8_g2;
@@ -924,56 +955,45 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
         p.q0 = q0;
         p.q_count = std::min(kMaxNQ, nq - q0);
         p.q8 = v->ws_q8.as<int4>() + (size_t)q0 * u8;
-        p.qc = v->ws_qc.as<float4>() + 2 * q0;
+        p.qc = v->ws_qc.as<float4>() + q0;
         p.qn_dev = v->ws_qnorm.as<float>() + q0;
         OSK_HIP(launch_sq8_scan(p.q_count, p, st));
     }
     rc = profile_end(v, st);
     if (rc) return rc;
+    OSK_HIP(v->ws_part.reserve(sizeof(uint64_t) * (size_t)nq * v->n_slices * k));
     SettleParams sp{};
+    sp.slices = v->d_slices.as<int4>();
+    sp.shard_slice_begin = v->d_shard_slice_begin.as<int32_t>();
+    sp.tiles = v->d_tiles.as<TileDev>();
+    sp.accept = d_accept;
+    sp.part = v->ws_part.as<uint64_t>();
+    sp.n_slices = v->n_slices;
     sp.segs = v->d_segs.as<SegDev>();
     sp.seg_vrow = v->d_seg_vrow.as<int64_t>();
-    sp.shard_tile_begin = v->d_shard_tile_begin.as<int32_t>();
     sp.cand = p.cand;
     sp.cand_lb = p.cand_lb;
+    sp.list_lbmax = p.list_lbmax;
     sp.q = v->ws_q.p;
     sp.qnorm = v->ws_qnorm.as<float>();
     sp.shard_keys = d_shard_keys;
     sp.shard_counts = d_shard_counts;
     sp.flags = v->ws_flags.as<int>();
     sp.counters = v->d_counters.as<unsigned long long>();
-    sp.n_tiles = v->n_tiles;
+    sp.n_lists = 4 * v->n_tiles;
+    sp.scan_R = 64 / sq8_lanes(u8);
     sp.n_shards = S;
     sp.n_segs = (int)v->segs.size();
     sp.units = v->units;
     sp.k = k;
     sp.sim = v->sim;
     sp.force_fail = g_tuning.sq8_force_fallback;
+    if (g_tuning.settle_trace) {
+        OSK_HIP(v->ws_trace.reserve(sizeof(unsigned long long) * 8 * (size_t)nq * v->n_slices));
+        sp.trace = v->ws_trace.as<unsigned long long>();
+    }
     OSK_HIP(launch_sq8_settle(v->cfg, nq, sp, st));
     v->sq8_calls += 1;
-    // exact fallback, gated per query on the device
-    OSK_HIP(v->ws_cand.reserve(sizeof(uint64_t) * (size_t)nq * v->n_tiles * k));
-    ScanParams fp{};
-    fp.segs = v->d_segs.as<SegDev>();
-    fp.tiles = v->d_tiles.as<TileDev>();
-    fp.accept = d_accept;
-    fp.cand = v->ws_cand.as<uint64_t>();
-    fp.visited = nullptr;
-    fp.n_tiles = v->n_tiles;
-    fp.units = v->units;
-    fp.k = k;
-    fp.sim = v->sim;
-    fp.dim = v->dim;
-    fp.gate = v->ws_flags.as<int>();
-    for (int q0 = 0; q0 < nq; q0 += kMaxNQ) {
-        fp.q0 = q0;
-        fp.q_count = std::min(kMaxNQ, nq - q0);
-        fp.q = v->ws_q.as<char>() + (size_t)q0 * UP * 16;
-        fp.qnorm_f = v->ws_qnorm.as<float>() + q0;
-        OSK_HIP(launch_scan(ENC_FLOAT32, v->cfg, fp.q_count, fp, st));
-    }
-    OSK_HIP(launch_merge_shards(v->ws_cand.as<uint64_t>(), v->n_tiles, v->d_shard_tile_begin.as<int32_t>(), S, nq,
-                                k, d_shard_keys, d_shard_counts, st, v->ws_flags.as<int>()));
     return OSK_OK;
 }
 
@@ -1001,7 +1021,8 @@ int32_t view_search_device(osk_view* v, const void* d_queries, int nq, int k,
     OSK_HIP(v->ws_qnorm.reserve(sizeof(float) * nq_pad));
     const bool batched = v->enc == ENC_FLOAT32 && g_tuning.mfma_min_batch > 0 &&
                          nq >= g_tuning.mfma_min_batch && k <= kKC - 4;
-    const bool prefilter = !batched && v->enc == ENC_FLOAT32 && g_tuning.sq8 && k <= kKQ;
+    // k ≤ kKQ − 4: a tile list holds 4 more rows than k, so it rarely overflows past the certificate
+    const bool prefilter = !batched && v->enc == ENC_FLOAT32 && g_tuning.sq8 && k <= kKQ - 4;
     // queries → padded unit layout (zeros past dim and for the dummy queries of the last launch); the
     // prefilter path does this inside its own fused prep launch
     if (!prefilter)
@@ -1063,9 +1084,34 @@ int32_t osk_merge_device(int32_t device, const uint64_t* d_shard_keys, const int
     int32_t rc = check_device(device);
     if (rc) return rc;
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : device_stream(device);
-    OSK_HIP(launch_merge_coord(d_shard_keys, d_shard_counts, d_shard_index, n_queries, n_shards, k,
+    OSK_HIP(launch_merge_coord(d_shard_keys, d_shard_counts, d_shard_index, n_queries, 1, n_shards, k,
                                from, size, d_scores, d_docs, d_shard_out, d_count, d_total_hits,
                                d_max_score, st));
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_merge_device_ranked(int32_t device, const uint64_t* d_keys, int32_t n_ranks,
+                                int32_t shards_per_rank, const int32_t* d_shard_index, int32_t n_queries,
+                                int32_t k, int32_t from, int32_t size, float* d_scores, int32_t* d_docs,
+                                int32_t* d_shard_out, int32_t* d_count, int64_t* d_total_hits,
+                                float* d_max_score, void* stream) {
+    OSK_GUARD_BEGIN
+    clear_error();
+    OSK_REQUIRE(n_queries >= 1 && n_ranks >= 1 && shards_per_rank >= 1,
+                "n_queries, n_ranks and shards_per_rank must be >= 1");
+    OSK_REQUIRE(k >= 1 && k <= OSK_MAX_K, "k must be in [1, OSK_MAX_K]");
+    OSK_REQUIRE(from >= 0 && size >= 1 && (int64_t)from + size <= 100000, "bad from/size");
+    OSK_REQUIRE((int64_t)n_ranks * shards_per_rank * std::min(k, from + size) <= 4096,
+                "n_shards * min(k, from+size) exceeds 4096 hits per query");
+    OSK_REQUIRE(d_keys && d_shard_index && d_scores && d_docs && d_shard_out && d_count && d_total_hits &&
+                    d_max_score,
+                "null device buffer");
+    int32_t rc = check_device(device);
+    if (rc) return rc;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : device_stream(device);
+    OSK_HIP(launch_merge_coord(d_keys, nullptr, d_shard_index, n_queries, n_ranks, shards_per_rank, k, from,
+                               size, d_scores, d_docs, d_shard_out, d_count, d_total_hits, d_max_score, st));
     return OSK_OK;
     OSK_GUARD_END
 }
@@ -1101,6 +1147,7 @@ int32_t osk_view_debug_copy(osk_view* v, const char* name, void* host, int64_t b
     const DevBuf* b = n == "akeys" ? &v->ws_akeys : n == "cand_a" ? &v->ws_cand_a : n == "flags" ? &v->ws_flags
                     : n == "qsplit" ? &v->ws_qsplit : n == "qnorm" ? &v->ws_qnorm
                     : n == "sq8cand" ? &v->ws_sq8cand : n == "sq8lb" ? &v->ws_sq8lb : n == "qc" ? &v->ws_qc
+                    : n == "settle_trace" ? &v->ws_trace
                     : nullptr;
     OSK_REQUIRE(b != nullptr, "unknown buffer");
     OSK_REQUIRE((size_t)bytes <= b->cap, "bytes exceed the buffer");
@@ -1129,10 +1176,12 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
     if (n == "mfma_calls") *value = v->mfma_calls;
     else if (n == "mfma_fallback_queries") *value = v->mfma_fallback_queries;
     else if (n == "sq8_calls") *value = v->sq8_calls;
-    else if (n == "sq8_fallback_queries" || n == "sq8_rescored_rows") {
+    else if (n == "sq8_slices")
+        *value = v->n_slices;
+    else if (n == "sq8_fallback_queries" || n == "sq8_rescored_rows" || n == "sq8_exact_tiles") {
         unsigned long long c[4];
         OSK_HIP(hipMemcpy(c, v->d_counters.p, sizeof(c), hipMemcpyDeviceToHost));
-        *value = (int64_t)(n == "sq8_fallback_queries" ? c[0] : c[1]);
+        *value = (int64_t)(n == "sq8_fallback_queries" ? c[0] : n == "sq8_rescored_rows" ? c[1] : c[2]);
     } else {
         set_error("unknown counter: " + n);
         return OSK_ERR_INVALID;
@@ -1222,7 +1271,7 @@ int32_t osk_view_search(osk_view* v, const void* queries, int32_t n_queries, int
     OSK_HIP(v->ws_out.reserve(total_b));
     char* ob = v->ws_out.as<char>();
     OSK_HIP(launch_merge_coord(v->ws_keys.as<uint64_t>(), v->ws_counts.as<int32_t>(),
-                               v->d_shard_index.as<int32_t>(), nq, S, k, from, size,
+                               v->d_shard_index.as<int32_t>(), nq, 1, S, k, from, size,
                                reinterpret_cast<float*>(ob + o_sc), reinterpret_cast<int32_t*>(ob + o_doc),
                                reinterpret_cast<int32_t*>(ob + o_sh), reinterpret_cast<int32_t*>(ob + o_cnt),
                                reinterpret_cast<int64_t*>(ob + o_tot), reinterpret_cast<float*>(ob + o_max),

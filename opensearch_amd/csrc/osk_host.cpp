@@ -147,4 +147,205 @@ int32_t osk_topdocs_merge(int32_t n_shards, const int32_t* shard_counts, const f
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Shard-result wire format: S/common/lucene/Lucene.java:407-447 (writeTopDocs, type 0 = plain
+// TopDocs, what a k-NN DocAndScoreQuery's TopScoreDocCollector yields) and :314-357 (readTopDocs),
+// with the StreamOutput / StreamInput encodings of libs/core/.../io/stream/StreamOutput.java
+// (writeInt :247-254 big-endian, writeVInt :262-285, writeVLong :308-337, writeFloat :480-482 =
+// writeInt(Float.floatToIntBits)) and StreamInput.java (readVInt :218-244, readVLong :267-319,
+// readEnum :1280-1290).
+// ------------------------------------------------------------------------------------------------
+}  // extern "C"
+
+namespace {
+
+struct WireOut {
+    uint8_t* p;
+    int64_t cap, n = 0;
+    void byte(uint8_t b) {
+        if (p && n < cap) p[n] = b;
+        ++n;
+    }
+    void i32(uint32_t v) {   // writeInt: big-endian
+        byte((uint8_t)(v >> 24)); byte((uint8_t)(v >> 16)); byte((uint8_t)(v >> 8)); byte((uint8_t)v);
+    }
+    void vint(int32_t i) {   // writeVInt: 7-bit groups, low first; negatives take 5 bytes
+        uint32_t u = (uint32_t)i;
+        while (u & ~0x7Fu) { byte((uint8_t)((u & 0x7F) | 0x80)); u >>= 7; }
+        byte((uint8_t)u);
+    }
+    void vlong(int64_t i) {
+        uint64_t u = (uint64_t)i;
+        while (u & ~0x7Full) { byte((uint8_t)((u & 0x7F) | 0x80)); u >>= 7; }
+        byte((uint8_t)u);
+    }
+    void f32(float f) {      // Float.floatToIntBits: every NaN → 0x7fc00000
+        uint32_t u;
+        std::memcpy(&u, &f, 4);
+        if (std::isnan(f)) u = 0x7fc00000u;
+        i32(u);
+    }
+};
+
+std::string hex32(uint32_t v) {   // Integer.toHexString
+    char b[16];
+    std::snprintf(b, sizeof b, "%x", v);
+    return b;
+}
+
+struct WireIn {
+    const uint8_t* p;
+    int64_t len, pos = 0;
+    std::string err;
+    bool byte(int8_t& b) {
+        if (pos >= len) { err = "EOF: tried to read past the end of the stream"; return false; }
+        b = (int8_t)p[pos++];
+        return true;
+    }
+    bool i32(uint32_t& v) {
+        v = 0;
+        for (int i = 0; i < 4; ++i) {
+            int8_t b;
+            if (!byte(b)) return false;
+            v = (v << 8) | (uint8_t)b;
+        }
+        return true;
+    }
+    bool vint(int32_t& out) {   // StreamInput.readVInt: at most 5 bytes, the 5th without a continuation bit
+        uint32_t i = 0;
+        for (int sh = 0; sh < 28; sh += 7) {
+            int8_t b;
+            if (!byte(b)) return false;
+            i |= (uint32_t)(b & 0x7F) << sh;
+            if ((b & 0x80) == 0) { out = (int32_t)i; return true; }
+        }
+        int8_t b;
+        if (!byte(b)) return false;
+        if (b & 0x80) {
+            err = "Invalid vInt ((" + hex32((uint32_t)(int32_t)b) + " & 0x7f) << 28) | " + hex32(i);
+            return false;
+        }
+        out = (int32_t)(i | ((uint32_t)(b & 0x7F) << 28));
+        return true;
+    }
+    bool vlong(int64_t& out) {  // StreamInput.readVLong: 9 groups of 7 bits, then a 0/1 sign byte
+        uint64_t i = 0;
+        for (int sh = 0; sh < 63; sh += 7) {
+            int8_t b;
+            if (!byte(b)) return false;
+            i |= (uint64_t)(b & 0x7F) << sh;
+            if ((b & 0x80) == 0) { out = (int64_t)i; return true; }
+        }
+        int8_t b;
+        if (!byte(b)) return false;
+        if (b != 0 && b != 1) {
+            char h[32];
+            std::snprintf(h, sizeof h, "%llx", (unsigned long long)i);
+            err = "Invalid vlong (" + hex32((uint32_t)(int32_t)b) + " << 63) | " + h;
+            return false;
+        }
+        out = (int64_t)(i | ((uint64_t)b << 63));
+        return true;
+    }
+    bool f32(float& f) {
+        uint32_t u;
+        if (!i32(u)) return false;
+        std::memcpy(&f, &u, 4);
+        return true;
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int32_t osk_topdocs_write(int64_t total_hits, int32_t relation, float max_score, int32_t n,
+                          const int32_t* docs, const float* scores, uint8_t* out, int64_t cap,
+                          int64_t* out_len) {
+    clear_error();
+    if (!out_len || n < 0 || (n > 0 && (!docs || !scores)) || cap < 0 || (cap > 0 && !out)) {
+        set_error("osk_topdocs_write: bad argument");
+        return OSK_ERR_INVALID;
+    }
+    if (total_hits < 0) {   // StreamOutput.writeVLong :308-313
+        set_error("Negative longs unsupported, use writeLong or writeZLong for negative numbers [" +
+                  std::to_string(total_hits) + "]");
+        return OSK_ERR_INVALID;
+    }
+    if (relation != 0 && relation != 1) {   // TotalHits.Relation {EQUAL_TO, GREATER_THAN_OR_EQUAL_TO}
+        set_error("osk_topdocs_write: relation must be 0 (EQUAL_TO) or 1 (GREATER_THAN_OR_EQUAL_TO)");
+        return OSK_ERR_INVALID;
+    }
+    WireOut w{out, cap};
+    w.byte(0);                 // plain TopDocs
+    w.vlong(total_hits);       // writeTotalHits (:402-405)
+    w.vint(relation);          // writeEnum = writeVInt(ordinal)
+    w.f32(max_score);
+    w.vint(n);
+    for (int32_t i = 0; i < n; ++i) {   // writeScoreDoc (:525-531)
+        w.vint(docs[i]);
+        w.f32(scores[i]);
+    }
+    *out_len = w.n;
+    if (out && w.n > cap) {
+        set_error("osk_topdocs_write: output buffer too small (need " + std::to_string(w.n) + " bytes)");
+        return OSK_ERR_INVALID;
+    }
+    return OSK_OK;
+}
+
+int32_t osk_topdocs_read(const uint8_t* buf, int64_t len, int64_t* total_hits, int32_t* relation,
+                         float* max_score, int32_t cap_hits, int32_t* n, int32_t* docs, float* scores,
+                         int64_t* consumed) {
+    clear_error();
+    if ((!buf && len > 0) || len < 0 || !total_hits || !relation || !max_score || !n || cap_hits < 0 ||
+        (cap_hits > 0 && (!docs || !scores))) {
+        set_error("osk_topdocs_read: bad argument");
+        return OSK_ERR_INVALID;
+    }
+    WireIn r{buf, len};
+    int8_t type;
+    int32_t rel, cnt;
+    int64_t total;
+    float mx;
+    if (!r.byte(type)) { set_error(r.err); return OSK_ERR_INVALID; }
+    if (type == 1 || type == 2) {   // TopFieldDocs / CollapseTopFieldDocs: never a k-NN shard result
+        set_error("osk_topdocs_read: TopDocs type " + std::to_string(type) + " (field docs) is not produced by the k-NN path");
+        return OSK_ERR_UNSUPPORTED;
+    }
+    if (type != 0) {
+        set_error("Unknown type " + std::to_string(type));
+        return OSK_ERR_INVALID;
+    }
+    if (!r.vlong(total) || !r.vint(rel) || (rel >= 0 && rel <= 1 && (!r.f32(mx) || !r.vint(cnt)))) {
+        set_error(r.err);
+        return OSK_ERR_INVALID;
+    }
+    if (rel < 0 || rel > 1) {
+        set_error("Unknown Relation ordinal [" + std::to_string(rel) + "]");
+        return OSK_ERR_INVALID;
+    }
+    if (cnt < 0) {
+        set_error("Negative array size: " + std::to_string(cnt));
+        return OSK_ERR_INVALID;
+    }
+    if (cnt > cap_hits) {
+        set_error("osk_topdocs_read: " + std::to_string(cnt) + " hits exceed the output capacity " +
+                  std::to_string(cap_hits));
+        return OSK_ERR_INVALID;
+    }
+    for (int32_t i = 0; i < cnt; ++i) {
+        if (!r.vint(docs[i]) || !r.f32(scores[i])) {
+            set_error(r.err);
+            return OSK_ERR_INVALID;
+        }
+    }
+    *total_hits = total;
+    *relation = rel;
+    *max_score = mx;
+    *n = cnt;
+    if (consumed) *consumed = r.pos;
+    return OSK_OK;
+}
+
 }  // extern "C"

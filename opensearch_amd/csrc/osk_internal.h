@@ -42,7 +42,6 @@ struct ScanParams {
     int k;
     int sim;
     int dim;
-    const int* gate;                 // fallback re-scan: skip the launch unless some query's flag is set
 };
 
 constexpr int kBlock = 256;          // 4 wavefronts per workgroup
@@ -113,7 +112,8 @@ hipError_t launch_rescore(int cfg, int nq, const RescoreParams& p, hipStream_t s
 // kernel re-scores exactly the rows that can still reach the shard's top k and proves the rest
 // cannot.  Results are bit-identical to the fp32 streaming scan.
 constexpr int kKQ = 16;              // per-tile candidate list of the prefilter (k ≤ kKQ)
-constexpr int kSettleCap = 4096;     // candidates re-scored per (query, shard) before the fallback
+constexpr int kSliceLists = 32;      // wave lists per settle workgroup (32 × kKQ = 512 entries)
+constexpr int kLGroupLists = 4096;   // lists whose best lower bounds define one settle threshold
 
 struct Sq8Params {
     const SegDev* segs;
@@ -122,18 +122,18 @@ struct Sq8Params {
     const int4* const* rows8;        // per segment: int8 rows [n_rows][units8] 16-B units
     const float4* const* aux;        // per segment: {scale, scale·|q8|, |x − scale·q8|, |x|²} per row
     const int64_t* seg_vrow;         // view row of each segment's ord 0
-    const int4* q8;                  // this launch's first query in plane 0: int8 [NQ][units8]; planes 1, 2
-                                     // (int16 query t = 256·h + l as h and l) follow at plane_stride
-    const float4* qc;                // per query [2]: int8 / int16 terms {scale, |b − s·q|, s·|q| + |b − s·q|, |b|²}
+    const int4* q8;                  // this launch's int8 queries [NQ][units8]
+    const float4* qc;                // per query {scale, |b − s·q8|, s·|q8| + |b − s·q8|, |b|²}
     const float* qn_dev;             // this launch's |q|² in the device lane order (COSINE)
-    uint64_t* cand;                  // [nq][n_tiles][kKQ] keys (upper-bound score, view row)
-    uint32_t* cand_lb;               // [nq][n_tiles][kKQ] sortable lower-bound scores
+    uint64_t* cand;                  // [nq][n_lists][kKQ] keys (upper-bound score, view row); list = tile·4 + wave
+    uint32_t* cand_lb;               // [nq][n_lists][kKQ] sortable lower-bound scores
+    uint32_t* list_lbmax;            // [nq][n_lists] best lower bound of each list (0 = empty)
     unsigned long long* visited;
     int n_tiles;
+    int n_lists;                     // 4 · n_tiles
     int q0;
     int q_count;
     int units8;
-    int64_t plane_stride;            // int4 units between query planes
     int sim;
     float gam;                       // fp32 dot rounding: |dot_dev − x·b| ≤ gam·(|x|² + |b|²)
     float g2;                        // fp32 d² rounding:  |d²_dev − d²| ≤ g2·d²
@@ -143,27 +143,37 @@ struct Sq8Params {
 struct SettleParams {
     const SegDev* segs;
     const int64_t* seg_vrow;
-    const int32_t* shard_tile_begin;
-    const uint64_t* cand;
+    const uint64_t* cand;            // the scan's wave lists [nq][n_lists][kKQ]
     const uint32_t* cand_lb;
+    const uint32_t* list_lbmax;      // [nq][n_lists]
     const void* q;                   // padded fp32 queries [nq][UP] float4
     const float* qnorm;              // |q|² device order (COSINE)
     uint64_t* shard_keys;            // [nq][n_shards][k]
     int32_t* shard_counts;
-    int* flags;                      // [nq] set when the query needs the exact fallback
-    unsigned long long* counters;    // [0] fallback queries, [1] rows re-scored
-    int n_tiles;
+    int* flags;                      // [nq] set when some list of the query was re-scanned exactly
+    unsigned long long* counters;    // [0] queries with an exactly re-scanned list, [1] rows re-scored,
+                                     // [2] lists re-scanned exactly
+    const int4* slices;              // [n_slices] {list_begin, list_end, L-group begin, L-group end}
+    const int32_t* shard_slice_begin;// [n_shards + 1]
+    const TileDev* tiles;            // the view's tiles (exact re-scan of an overflowed list)
+    const uint64_t* const* accept;   // per-segment accept bitsets (or null)
+    uint64_t* part;                  // [nq][n_slices][k] per-slice exact top k
+    int n_slices;
+    int n_lists;                     // 4 · n_tiles (list = tile·4 + scan wave)
+    int scan_R;                      // rows per wave-iteration of the int8 scan (its per-wave row split)
     int n_shards;
     int n_segs;
     int units;
     int k;
     int sim;
-    int force_fail;                  // tests: send every query to the fallback
+    int force_fail;                  // tests: re-scan every list exactly
+    unsigned long long* trace;       // A/B only: per (query, slice) 8 slots of phase timestamps, or null
 };
 
 hipError_t launch_sq8_quantize(const float4* x, int64_t n, int units, int pitch, int units8, void* out8,
                                float4* aux, int mode, hipStream_t s);
 hipError_t launch_sq8_scan(int nq, const Sq8Params& p, hipStream_t s);
+int sq8_lanes(int units8);         // lanes per row of the int8 scan
 hipError_t launch_sq8_prep(int cfg, const float* src, int dim, int nq, int nq_pad, int UP, int units8, float4* qpad,
                            float* qnorm, void* q8, float4* qc, int* flags, hipStream_t s);
 hipError_t launch_sq8_settle(int cfg, int nq, const SettleParams& p, hipStream_t s);
@@ -174,10 +184,13 @@ int cfg_index(int units);
 struct Tuning {
     int scan_nt = 1;          // non-temporal corpus loads in scan_f32 (+4% HBM rate, profiles/r01_scan_ab.txt)
     int tiles_target = 4096;  // workgroup tiles per view (scan grid size)
+    int tile_min_rows = 1024; // ...but at least this many rows per tile (1.25M rows: 1221 tiles, +10% QPS
+                              // over 4096 tiles of 305 rows — profiles/r01e/tiles_ab.txt)
     int mfma_min_batch = 16;  // batches ≥ this use the MFMA candidate path (0 = never)
     int mfma_units = 512;     // workgroup units of the MFMA candidate pass per view
     int sq8 = 1;              // certified int8 prefilter for float32 batches below mfma_min_batch
-    int sq8_force_fallback = 0;   // tests: every prefiltered query takes the exact fallback
+    int sq8_force_fallback = 0;   // tests: every list of a prefiltered search is re-scanned exactly
+    int settle_trace = 0;     // A/B only: record settle phase timestamps (debug copy "settle_trace")
     int mfma_ablate = 0;      // A/B only: 1 skip the epilogue, 2 skip query staging, 4 skip corpus staging,
                               // 8 force the full staging epilogue, 16 skip the pilot pass
                               // (results are wrong and the exact fallback is skipped)
@@ -197,9 +210,9 @@ hipError_t launch_pad_rows(const void* src, int64_t src_pitch, void* dst, int64_
                            int64_t n_rows, int64_t row_bytes, hipStream_t s);
 hipError_t launch_merge_shards(const uint64_t* cand, int n_tiles, const int32_t* shard_tile_begin,
                                int n_shards, int nq, int k, uint64_t* shard_keys,
-                               int32_t* shard_counts, hipStream_t s, const int* gate = nullptr);
+                               int32_t* shard_counts, hipStream_t s);
 hipError_t launch_merge_coord(const uint64_t* shard_keys, const int32_t* shard_counts,
-                              const int32_t* shard_index, int nq, int n_shards, int k, int from,
+                              const int32_t* shard_index, int nq, int n_ranks, int sl, int k, int from,
                               int size, float* scores, int32_t* docs, int32_t* shard_out,
                               int32_t* count, int64_t* total_hits, float* max_score,
                               hipStream_t s);

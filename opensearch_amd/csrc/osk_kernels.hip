@@ -43,11 +43,6 @@ __global__ __launch_bounds__(kBlock) void scan_f32(ScanParams p) {
     constexpr int R = 64 / L;                 // rows per wave-iteration
     constexpr int UP = L * V;                 // padded float4s per query
     constexpr bool QREG = NQ * V * 4 <= 64;   // query fragments in VGPRs, else read from LDS
-    if (p.gate) {   // exact fallback of the prefilter: run only if one of this launch's queries failed
-        bool any = false;
-        for (int b = 0; b < p.q_count; ++b) any |= p.gate[p.q0 + b] != 0;
-        if (!any) return;
-    }
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float4* sq = reinterpret_cast<float4*>(smem);
     uint64_t* slist = reinterpret_cast<uint64_t*>(smem + (QREG ? 0 : NQ * UP * 16));
@@ -174,11 +169,6 @@ __global__ __launch_bounds__(kBlock) void scan_i8(ScanParams p) {
     constexpr int R = 64 / L;
     constexpr int UP = L * V;
     constexpr bool QREG = NQ * V * 4 <= 64;
-    if (p.gate) {   // exact fallback of the prefilter: run only if one of this launch's queries failed
-        bool any = false;
-        for (int b = 0; b < p.q_count; ++b) any |= p.gate[p.q0 + b] != 0;
-        if (!any) return;
-    }
     extern __shared__ __attribute__((aligned(16))) char smem[];
     int4* sq = reinterpret_cast<int4*>(smem);
     uint64_t* slist = reinterpret_cast<uint64_t*>(smem + (QREG ? 0 : NQ * UP * 16));
@@ -521,11 +511,9 @@ __global__ __launch_bounds__(kBlock) void merge_shards(const uint64_t* __restric
                                                        const int32_t* __restrict__ shard_tile_begin,
                                                        int n_shards, int k,
                                                        uint64_t* __restrict__ shard_keys,
-                                                       int32_t* __restrict__ shard_counts,
-                                                       const int* __restrict__ gate) {
+                                                       int32_t* __restrict__ shard_counts) {
     __shared__ uint64_t lists[4 * 64];
     const int s = blockIdx.x, b = blockIdx.y;
-    if (gate && !gate[b]) return;   // prefilter fallback: only the queries that failed
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int t0 = shard_tile_begin[s], t1 = shard_tile_begin[s + 1];
     const uint64_t* c = cand + ((size_t)b * n_tiles + t0) * k;
@@ -549,9 +537,9 @@ __global__ __launch_bounds__(kBlock) void merge_shards(const uint64_t* __restric
 
 hipError_t launch_merge_shards(const uint64_t* cand, int n_tiles, const int32_t* shard_tile_begin,
                                int n_shards, int nq, int k, uint64_t* shard_keys,
-                               int32_t* shard_counts, hipStream_t s, const int* gate) {
+                               int32_t* shard_counts, hipStream_t s) {
     hipLaunchKernelGGL(merge_shards, dim3(n_shards, nq), dim3(kBlock), 0, s, cand, n_tiles,
-                       shard_tile_begin, n_shards, k, shard_keys, shard_counts, gate);
+                       shard_tile_begin, n_shards, k, shard_keys, shard_counts);
     return hipGetLastError();
 }
 
@@ -562,63 +550,91 @@ hipError_t launch_merge_shards(const uint64_t* cand, int n_tiles, const int32_t*
 // ------------------------------------------------------------------------------------------------
 constexpr int kCoordMax = 4096;   // shard hits considered per query (n_shards · min(k, from+size))
 
-// Slot (s, i) = hit i of shard s, a fixed position: every thread loads its slots' counts and keys at
-// once (no per-shard serialisation), then ranks each valid hit against all others.
+// Slot (s, i) = hit i of shard s, a fixed position: every thread loads its slots' keys at once (no
+// per-shard serialisation), then ranks each valid hit against all others.
+// Layout: shard s = (rank r, local shard j), s = r·sl + j, its list at ((r·nq + b)·sl + j)·k — the
+// rank-major image an all-gather of per-rank [nq][sl][k] lists produces (n_ranks = 1: [nq][S][k]).
+// shard_counts null: a list's hits are its non-zero keys (lists are best-first, zero-padded).
 __global__ __launch_bounds__(kBlock) void merge_coord(const uint64_t* __restrict__ shard_keys,
                                                       const int32_t* __restrict__ shard_counts,
                                                       const int32_t* __restrict__ shard_index,
-                                                      int n_shards, int k, int from, int size,
+                                                      int n_ranks, int sl, int k, int from, int size,
                                                       float* __restrict__ scores,
                                                       int32_t* __restrict__ docs,
                                                       int32_t* __restrict__ shard_out,
                                                       int32_t* __restrict__ count,
                                                       int64_t* __restrict__ total_hits,
                                                       float* __restrict__ max_score) {
-    __shared__ uint32_t s_su[kCoordMax];
-    __shared__ int32_t s_sidx[kCoordMax];   // INT32_MIN = empty slot
-    __shared__ int32_t s_doc[kCoordMax];
+    // empty slot = (su 0, shardIndex INT32_MAX, doc INT32_MAX): it never ranks above a hit
+    __shared__ __attribute__((aligned(16))) uint32_t s_su[kCoordMax];
+    __shared__ __attribute__((aligned(16))) int32_t s_sidx[kCoordMax];
+    __shared__ __attribute__((aligned(16))) int32_t s_doc[kCoordMax];
     __shared__ int s_n;
     __shared__ unsigned long long s_total;
     __shared__ uint32_t s_max;
-    const int b = blockIdx.x, tid = threadIdx.x;
+    const int b = blockIdx.x, tid = threadIdx.x, nq = gridDim.x;
+    const int n_shards = n_ranks * sl;
     const int topn = min(k, from + size);
     const int n_slots = n_shards * topn;
+    const int n4 = (n_slots + 3) & ~3;   // ≤ kCoordMax (the host checks n_slots ≤ 4096)
     if (tid == 0) { s_n = 0; s_total = 0ull; s_max = 0u; }
     __syncthreads();
-    const uint64_t* kb = shard_keys + (size_t)b * n_shards * k;
-    const int32_t* cb = shard_counts + (size_t)b * n_shards;
-    for (int s = tid; s < n_shards; s += kBlock) {
-        const int c = cb[s];
-        atomicAdd(&s_total, (unsigned long long)c);
-        if (c > 0) atomicMax(&s_max, (uint32_t)(kb[(size_t)s * k] >> 32));
-    }
-    int mine = 0;
-    for (int slot = tid; slot < n_slots; slot += kBlock) {
-        const int s = slot / topn, i = slot - s * topn;
-        const bool valid = i < cb[s];
-        if (valid) {
-            const uint64_t key = kb[(size_t)s * k + i];
-            s_su[slot] = (uint32_t)(key >> 32);
-            s_doc[slot] = key_doc(key);
-            s_sidx[slot] = shard_index[s];
-            ++mine;
-        } else {
-            s_sidx[slot] = INT32_MIN;
+    auto list = [&](int s) -> size_t {
+        const int r = s / sl, j = s - r * sl;
+        return ((size_t)(r * nq + b) * sl + j);
+    };
+    // stats (TopDocsStats): Σ hits over the shards, max of their top scores
+    if (shard_counts) {
+        for (int s = tid; s < n_shards; s += kBlock) {
+            const size_t o = list(s);
+            const int c = shard_counts[o];
+            const uint64_t top = shard_keys[o * k];
+            atomicAdd(&s_total, (unsigned long long)c);
+            if (c > 0) atomicMax(&s_max, (uint32_t)(top >> 32));
         }
+    } else {
+        int hits = 0;
+        for (int e = tid; e < n_shards * k; e += kBlock) {
+            const int s = e / k, i = e - s * k;
+            const uint64_t key = shard_keys[list(s) * k + i];
+            hits += key != 0ull;
+            if (i == 0 && key) atomicMax(&s_max, (uint32_t)(key >> 32));
+        }
+        if (hits) atomicAdd(&s_total, (unsigned long long)hits);
+    }
+    // one round of independent loads per slot (i < topn ≤ k keeps the key load in bounds)
+    int mine = 0;
+    for (int slot = tid; slot < n4; slot += kBlock) {
+        const int s = slot / topn, i = slot - s * topn;
+        const bool real = slot < n_slots;
+        const size_t o = real ? list(s) : 0;
+        const uint64_t key = real ? shard_keys[o * k + i] : 0ull;
+        const int c = real && shard_counts ? shard_counts[o] : 0;
+        const int32_t si = real ? shard_index[s] : 0;
+        const bool hit = real && (shard_counts ? i < c : key != 0ull);
+        s_su[slot] = hit ? (uint32_t)(key >> 32) : 0u;
+        s_doc[slot] = hit ? key_doc(key) : INT32_MAX;
+        s_sidx[slot] = hit ? si : INT32_MAX;
+        mine += hit;
     }
     if (mine) atomicAdd(&s_n, mine);
     __syncthreads();
+    // rank of each hit = number of hits ordered before it; the slots are read 4 at a time with
+    // independent 16-byte LDS loads (a scalar loop with a branch per slot is latency-bound)
     for (int i = tid; i < n_slots; i += kBlock) {
-        const int32_t si = s_sidx[i];
-        if (si == INT32_MIN) continue;
         const uint32_t su = s_su[i];
-        const int32_t d = s_doc[i];
+        if (su == 0u && s_sidx[i] == INT32_MAX) continue;   // empty
+        const int32_t si = s_sidx[i], d = s_doc[i];
         int rank = 0;
-        for (int j = 0; j < n_slots; ++j) {
-            const int32_t sj = s_sidx[j];
-            if (sj == INT32_MIN) continue;
-            const uint32_t uj = s_su[j];
-            rank += (uj > su) || (uj == su && (sj < si || (sj == si && s_doc[j] < d)));
+#pragma unroll 4
+        for (int j = 0; j < n4; j += 4) {
+            const uint4 u4 = *reinterpret_cast<const uint4*>(s_su + j);
+            const int4 s4 = *reinterpret_cast<const int4*>(s_sidx + j);
+            const int4 d4 = *reinterpret_cast<const int4*>(s_doc + j);
+            rank += (u4.x > su) || (u4.x == su && (s4.x < si || (s4.x == si && d4.x < d)));
+            rank += (u4.y > su) || (u4.y == su && (s4.y < si || (s4.y == si && d4.y < d)));
+            rank += (u4.z > su) || (u4.z == su && (s4.z < si || (s4.z == si && d4.z < d)));
+            rank += (u4.w > su) || (u4.w == su && (s4.w < si || (s4.w == si && d4.w < d)));
         }
         if (rank >= from && rank < from + size) {
             const size_t o = (size_t)b * size + (rank - from);
@@ -643,12 +659,12 @@ __global__ __launch_bounds__(kBlock) void merge_coord(const uint64_t* __restrict
 }
 
 hipError_t launch_merge_coord(const uint64_t* shard_keys, const int32_t* shard_counts,
-                              const int32_t* shard_index, int nq, int n_shards, int k, int from,
+                              const int32_t* shard_index, int nq, int n_ranks, int sl, int k, int from,
                               int size, float* scores, int32_t* docs, int32_t* shard_out,
                               int32_t* count, int64_t* total_hits, float* max_score,
                               hipStream_t s) {
     hipLaunchKernelGGL(merge_coord, dim3(nq), dim3(kBlock), 0, s, shard_keys, shard_counts,
-                       shard_index, n_shards, k, from, size, scores, docs, shard_out, count,
+                       shard_index, n_ranks, sl, k, from, size, scores, docs, shard_out, count,
                        total_hits, max_score);
     return hipGetLastError();
 }

@@ -12,14 +12,16 @@
 //                 score the fp32 streaming scan computes for that row (quantisation error bound +
 //                 the fp32 rounding bound of the device summation order).  Per tile it keeps the
 //                 kKQ rows with the highest upper bound (keys) and their lower bounds.
-//   sq8_settle    per (query, shard): L = k-th best lower bound; every listed row whose upper bound
-//                 reaches L is re-scored with the streaming scan's exact arithmetic; a tile whose
-//                 list is full and whose last upper bound reaches L (a dropped row might qualify), or
-//                 more than kSettleCap candidates, sends the query to the exact fallback scan.
+//   sq8_settle    per (query, slice of 16 tiles): L = k-th best lower bound of the listed rows of
+//                 its group of slices; every listed row whose upper bound reaches L is re-scored with the streaming
+//                 scan's exact arithmetic; a tile whose list is full and whose last upper bound
+//                 reaches L (a dropped row might qualify) is re-scanned exactly, every row.
 //
-// Soundness: every non-re-scored row r has score(r) ≤ ub(r) < L ≤ T, where T is the
-// k-th exact score among the re-scored rows (the k rows that define L are all re-scored, and each
-// scores ≥ its lower bound ≥ L).  Strictness (ub < L) makes doc-order ties irrelevant.
+// Soundness: L is the k-th best lower bound among listed rows of a group of slices
+// of one shard.  Those k rows have ub ≥ lb ≥ L, so each is re-scored (or lies in an exactly
+// re-scanned tile) and scores ≥ L: the shard's k-th exact score T ≥ L.  A row that is neither
+// re-scored nor in an exact tile has score ≤ ub < L ≤ T, so it cannot enter the top k; strictness
+// (ub < L) makes doc-order ties irrelevant.
 #include "osk_internal.h"
 #include "osk_wave.h"
 
@@ -101,10 +103,9 @@ hipError_t launch_sq8_quantize(const float4* x, int64_t n, int units, int pitch,
 //   * the padded fp32 query (UP float4, zeros past dim; zero rows past nq) for the re-score and the
 //     exact fallback;
 //   * |q|² in the device lane order (identical bits to row_norms_f32 / scan_f32's in-kernel norm);
-//   * plane 0: int8 quantisation (s = max|b|/127) and its bound terms qc[2r];
-//   * planes 1, 2: an int16 quantisation t = 256·h + l (s = max|b|/32512, h ∈ [−127, 127],
-//     l ∈ [−128, 127]) and its bound terms qc[2r+1] — the query error becomes negligible, which
-//     halves the prefilter's bound for the batch-1/2 kernels;
+//   * the int8 quantisation (s = max|b|/127) and its bound terms qc[r];
+//     (an int16 query — 256× smaller query error — was measured: 4.4× fewer re-scored rows but a
+//     slower scan, its extra sdot4 work is not free at the HBM ceiling; so int8 it is)
 //   * flags[r] = 0.
 // ------------------------------------------------------------------------------------------------
 template <int L, int V>
@@ -142,51 +143,32 @@ __global__ __launch_bounds__(kBlock) void sq8_prep(const float* __restrict__ src
         for (int o = 1; o < L; o <<= 1) sn += __shfl_xor(sn, o);
         if (lane == 0) qnorm[r] = sn;
     }
-    const float s8 = m / 127.0f, s16 = m / 32512.0f;
-    long long a8 = 0, a16 = 0;
-    double e8 = 0.0, e16 = 0.0, sx = 0.0;
+    const float s8 = m / 127.0f;
+    long long a8 = 0;
+    double e8 = 0.0, sx = 0.0;
     uint32_t* p0 = q8 + r * dw;
-    uint32_t* p1 = q8 + ((int64_t)nq_pad + r) * dw;
-    uint32_t* p2 = q8 + (2 * (int64_t)nq_pad + r) * dw;
     for (int d = lane; d < dw; d += 64) {
-        uint32_t w0 = 0u, w1 = 0u, w2 = 0u;
+        uint32_t w0 = 0u;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const float x = val(4 * d + e);
-            int q = 0, t = 0;
-            if (s8 > 0.0f) {
-                q = (int)fminf(fmaxf(rintf(x / s8), -127.0f), 127.0f);
-                t = (int)fminf(fmaxf(rintf(x / s16), -32512.0f), 32512.0f);
-            }
-            const int h = (t + 128) >> 8;            // floor((t + 128) / 256)
-            const int l = t - 256 * h;                // ∈ [−128, 127]
+            const int q = s8 > 0.0f ? (int)fminf(fmaxf(rintf(x / s8), -127.0f), 127.0f) : 0;
             w0 |= ((uint32_t)q & 0xFFu) << (8 * e);
-            w1 |= ((uint32_t)h & 0xFFu) << (8 * e);
-            w2 |= ((uint32_t)l & 0xFFu) << (8 * e);
             a8 += (long long)(q * q);
-            a16 += (long long)t * t;
-            const double r8 = (double)x - (double)s8 * (double)q;
-            const double r16 = (double)x - (double)s16 * (double)t;
+            const double r8 = (double)x - (double)s8 * (double)q;   // exact in double
             e8 += r8 * r8;
-            e16 += r16 * r16;
             sx += (double)x * (double)x;
         }
         p0[d] = w0;
-        p1[d] = w1;
-        p2[d] = w2;
     }
     for (int o = 32; o >= 1; o >>= 1) {
         a8 += __shfl_xor(a8, o);
-        a16 += __shfl_xor(a16, o);
         e8 += __shfl_xor(e8, o);
-        e16 += __shfl_xor(e16, o);
         sx += __shfl_xor(sx, o);
     }
     if (lane == 0) {
         const double A8 = (double)s8 * sqrt((double)a8) * (1.0 + 1e-12), B8 = sqrt(e8) * (1.0 + 1e-12);
-        const double A16 = (double)s16 * sqrt((double)a16) * (1.0 + 1e-12), B16 = sqrt(e16) * (1.0 + 1e-12);
-        qc[2 * r] = make_float4(s8, f32_round_up(B8), f32_round_up((A8 + B8) * (1.0 + 1e-12)), (float)sx);
-        qc[2 * r + 1] = make_float4(s16, f32_round_up(B16), f32_round_up((A16 + B16) * (1.0 + 1e-12)), (float)sx);
+        qc[r] = make_float4(s8, f32_round_up(B8), f32_round_up((A8 + B8) * (1.0 + 1e-12)), (float)sx);
         if (real) flags[r] = 0;
     }
 }
@@ -273,13 +255,9 @@ __device__ __forceinline__ int4 load_i4_nt(const int4* p) {
 // prefilter scan: a row is L lanes × V 16-byte int8 units; U row groups per wave-iteration are
 // loaded before any is reduced (≈ U·V·1 KiB in flight per wave).
 // ------------------------------------------------------------------------------------------------
-template <int L, int V, int NQ, int U, int P>
+template <int L, int V, int NQ, int U>
 __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
     constexpr int R = 64 / L;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    uint64_t* slist = reinterpret_cast<uint64_t*>(smem);                      // [NQ][4][64]
-    uint32_t* splb = reinterpret_cast<uint32_t*>(smem + NQ * 4 * 64 * 8);    // [NQ][4][64]
-
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int t = lane & (L - 1), g = lane / L;
     const TileDev tile = p.tiles[blockIdx.x];
@@ -289,8 +267,7 @@ __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
     const uint32_t vbase = (uint32_t)p.seg_vrow[tile.seg];
     const int u8 = p.units8, sim = p.sim;
 
-    // P = 1: the int8 query (plane 0); P = 2: the int16 query as planes h (1) and l (2), t = 256h + l
-    int4 qf[NQ][V], ql[P == 2 ? NQ : 1][P == 2 ? V : 1];
+    int4 qf[NQ][V];
     float4 qc[NQ];
     float qnd[NQ], sqn[NQ];
 #pragma unroll
@@ -302,14 +279,10 @@ __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
             const int f = t + j * L;
             const int fc = f < u8 ? f : 0;
             const int msk = f < u8 ? -1 : 0;
-            int4 v = p.q8[(P == 1 ? 0 : p.plane_stride) + b * u8 + fc];
+            const int4 v = p.q8[b * u8 + fc];
             qf[b][j] = make_int4(v.x & msk, v.y & msk, v.z & msk, v.w & msk);
-            if constexpr (P == 2) {
-                v = p.q8[2 * p.plane_stride + b * u8 + fc];
-                ql[b][j] = make_int4(v.x & msk, v.y & msk, v.z & msk, v.w & msk);
-            }
         }
-        qc[b] = p.qc[2 * b + (P - 1)];
+        qc[b] = p.qc[b];
         qnd[b] = sim == SIM_COSINE ? p.qn_dev[b] : 0.0f;
         sqn[b] = sqrtf(qnd[b]);
     }
@@ -371,29 +344,18 @@ __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
             const float sx = sim == SIM_COSINE ? sqrtf(ax[u].w) : 0.0f;
 #pragma unroll
             for (int b = 0; b < NQ; ++b) {
-                int acc = 0, acc2 = 0;
+                int acc = 0;
 #pragma unroll
                 for (int j = 0; j < V; ++j) {
                     acc = __builtin_amdgcn_sdot4(xv[u][j].x, qf[b][j].x, acc, false);
                     acc = __builtin_amdgcn_sdot4(xv[u][j].y, qf[b][j].y, acc, false);
                     acc = __builtin_amdgcn_sdot4(xv[u][j].z, qf[b][j].z, acc, false);
                     acc = __builtin_amdgcn_sdot4(xv[u][j].w, qf[b][j].w, acc, false);
-                    if constexpr (P == 2) {
-                        acc2 = __builtin_amdgcn_sdot4(xv[u][j].x, ql[b][j].x, acc2, false);
-                        acc2 = __builtin_amdgcn_sdot4(xv[u][j].y, ql[b][j].y, acc2, false);
-                        acc2 = __builtin_amdgcn_sdot4(xv[u][j].z, ql[b][j].z, acc2, false);
-                        acc2 = __builtin_amdgcn_sdot4(xv[u][j].w, ql[b][j].w, acc2, false);
-                    }
                 }
 #pragma unroll
-                for (int m = 1; m < L; m <<= 1) {
-                    acc += __shfl_xor(acc, m);
-                    if constexpr (P == 2) acc2 += __shfl_xor(acc2, m);
-                }
-                // Σ q_x·t = 256·Σ q_x·h + Σ q_x·l (exact ints; one fma rounding, inside the slack)
-                const float I = P == 2 ? fmaf((float)acc, 256.0f, (float)acc2) : (float)acc;
+                for (int m = 1; m < L; m <<= 1) acc += __shfl_xor(acc, m);
                 float lo, hi;
-                sq8_bounds(sim, I, ax[u], qc[b], p.gam, p.g2, lo, hi);
+                sq8_bounds(sim, (float)acc, ax[u], qc[b], p.gam, p.g2, lo, hi);
                 const bool pass = valid[u] && sq8_pass(sim, lo, hi, tq[b], sx);
                 if (__ballot(pass && t == 0)) {   // wave-uniform: rare once the list has filled
                     float xnd = 0.0f;
@@ -430,24 +392,21 @@ __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
 
     if (p.visited && p.q0 == 0 && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
 
+    // one list per wave (its own row range of the tile): finer lists overflow the certificate less
+    // often than one folded list per tile, and need no LDS fold.  With it, the list's best lower
+    // bound (the settle's threshold is selected among these, one distinct row per list).
 #pragma unroll
     for (int b = 0; b < NQ; ++b) {
-        slist[(b * 4 + wave) * 64 + lane] = lane < kKQ ? lk[b] : 0ull;
-        splb[(b * 4 + wave) * 64 + lane] = lp[b];
-    }
-    __syncthreads();
-    if (wave == 0) {
+        uint32_t m = (lane < kKQ && lk[b]) ? lp[b] : 0u;
 #pragma unroll
-        for (int b = 0; b < NQ; ++b) {
-            for (int w = 1; w < 4; ++w) {
-                const uint64_t key = lane < kKQ ? slist[(b * 4 + w) * 64 + lane] : 0ull;
-                wave_offer2(key, splb[(b * 4 + w) * 64 + lane], true, lk[b], lp[b], thr[b], lane, kKQ);
+        for (int o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+        if (b < p.q_count) {
+            const size_t l = (size_t)(p.q0 + b) * p.n_lists + blockIdx.x * 4 + wave;
+            if (lane < kKQ) {
+                p.cand[l * kKQ + lane] = lk[b];
+                p.cand_lb[l * kKQ + lane] = lp[b];
             }
-            if (b < p.q_count && lane < kKQ) {
-                const size_t o = ((size_t)(p.q0 + b) * p.n_tiles + blockIdx.x) * kKQ + lane;
-                p.cand[o] = lk[b];
-                p.cand_lb[o] = lp[b];
-            }
+            if (lane == 0) p.list_lbmax[l] = m;
         }
     }
 }
@@ -456,141 +415,252 @@ __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
 static int sq8_cfg(int u8) {
     return u8 <= 4 ? 0 : u8 <= 8 ? 1 : u8 <= 16 ? 2 : u8 <= 32 ? 3 : u8 <= 48 ? 4 : u8 <= 64 ? 5 : u8 <= 128 ? 6 : 7;
 }
+int sq8_lanes(int u8) {   // L of the scan's config (its rows per wave-iteration are 64 / L)
+    static const int kL[8] = {4, 8, 16, 16, 16, 16, 32, 64};
+    return kL[sq8_cfg(u8)];
+}
 using Sq8Fn = void (*)(Sq8Params);
-#define OSK_SQ8_ROW(L, V) {sq8_scan<L, V, 1, 4, 2>, sq8_scan<L, V, 2, 4, 2>, sq8_scan<L, V, 4, 2, 1>, sq8_scan<L, V, 8, 1, 1>}
+#define OSK_SQ8_ROW(L, V) {sq8_scan<L, V, 1, 4>, sq8_scan<L, V, 2, 4>, sq8_scan<L, V, 4, 2>, sq8_scan<L, V, 8, 1>}
 static const Sq8Fn kSq8[8][4] = {OSK_SQ8_ROW(4, 1),  OSK_SQ8_ROW(8, 1),  OSK_SQ8_ROW(16, 1), OSK_SQ8_ROW(16, 2),
                                  OSK_SQ8_ROW(16, 3), OSK_SQ8_ROW(16, 4), OSK_SQ8_ROW(32, 4), OSK_SQ8_ROW(64, 4)};
 
 hipError_t launch_sq8_scan(int nq, const Sq8Params& p, hipStream_t s) {
     const int slot = nq <= 1 ? 0 : nq <= 2 ? 1 : nq <= 4 ? 2 : 3;
-    const int NQ = 1 << slot;
-    const size_t lds = (size_t)NQ * 4 * 64 * 12;
-    hipLaunchKernelGGL(kSq8[sq8_cfg(p.units8)][slot], dim3(p.n_tiles), dim3(kBlock), lds, s, p);
+    hipLaunchKernelGGL(kSq8[sq8_cfg(p.units8)][slot], dim3(p.n_tiles), dim3(kBlock), 0, s, p);
     return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------------
-// settle: one 512-thread workgroup per (shard, query)
+// settle, in slices of kSliceLists wave lists (≤ 512 entries), one workgroup per (slice, query), so
+// every (query, shard) spreads over many workgroups (one workgroup per (query, shard) is
+// latency-bound: ~50 µs):
+//   sq8_settle        L_g = the k-th best of the lists' best lower bounds over a group of up to
+//                     kLGroupLists lists of the shard (k distinct rows) — at most the shard's k-th
+//                     best lower bound, so excluding a row with ub < L_g is sound; the slice's rows
+//                     with ub ≥ L_g are re-scored exactly; a
+//                     wave list that is full and whose last ub reaches L_g (it may have dropped a
+//                     qualifying row) has its row range re-scanned exactly inside the same
+//                     workgroup (rare; no fallback launch).
+//                     The slice's top k → part.
+//   sq8_settle_merge  per (query, shard): the top k of its slices' lists → shard keys / counts.
 // ------------------------------------------------------------------------------------------------
-constexpr int kSettleThreads = 1024;
+constexpr int kSettleThreads = 256;
+constexpr int kSettleWaves = kSettleThreads / 64;
+
+// exact score of one row (the streaming scan's arithmetic: same lane layout and fma order)
+template <int L, int V, bool L2K>
+__device__ __forceinline__ float settle_exact(const float4* xr, bool valid, int units, int t,
+                                              const float4 (&qf)[V], int sim, float qn, float xn) {
+    float4 xv[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+        const int f = t + j * L;
+        xv[j] = (valid && f < units) ? xr[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float ax = 0.f, ay = 0.f, az = 0.f, aw = 0.f;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+        const float4 x = xv[j];
+        if constexpr (L2K) {
+            const float dx = x.x - qf[j].x, dy = x.y - qf[j].y, dz = x.z - qf[j].z, dw = x.w - qf[j].w;
+            ax = fmaf(dx, dx, ax); ay = fmaf(dy, dy, ay); az = fmaf(dz, dz, az); aw = fmaf(dw, dw, aw);
+        } else {
+            ax = fmaf(x.x, qf[j].x, ax); ay = fmaf(x.y, qf[j].y, ay);
+            az = fmaf(x.z, qf[j].z, az); aw = fmaf(x.w, qf[j].w, aw);
+        }
+    }
+    float sum = (ax + ay) + (az + aw);
+#pragma unroll
+    for (int m = 1; m < L; m <<= 1) sum += __shfl_xor(sum, m);
+    if constexpr (L2K) return score_f32_l2(sum);
+    else return score_f32(sim, sum, qn, xn);
+}
 
 template <int L, int V, bool L2K>
 __global__ __launch_bounds__(kSettleThreads) void sq8_settle(SettleParams p) {
-    constexpr int NW = kSettleThreads / 64, R = 64 / L, UP = L * V;
-    __shared__ uint64_t s_lists[NW * 64];
-    __shared__ uint32_t s_cand[kSettleCap];
-    __shared__ int s_nc, s_fail;
+    constexpr int R = 64 / L, UP = L * V;
+    __shared__ uint64_t s_lists[kSettleWaves * 64];
+    __shared__ uint64_t s_top[64];
+    __shared__ uint32_t s_cand[kSliceLists * kKQ];
+    __shared__ __attribute__((aligned(16))) uint64_t s_keys[64];
+    __shared__ int s_nc;
     __shared__ uint32_t s_L;
-    const int s = blockIdx.x, q = blockIdx.y, S = p.n_shards;
+    __shared__ uint32_t s_exact;   // bit i: list l0 + i of the slice is re-scanned exactly
+    const int g = blockIdx.x, q = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int t = lane & (L - 1), g = lane / L;
+    const int t = lane & (L - 1), gr = lane / L;
     const int k = p.k, sim = p.sim;
-    const int t0 = p.shard_tile_begin[s], t1 = p.shard_tile_begin[s + 1];
-    const size_t base = ((size_t)q * p.n_tiles + t0) * kKQ;
-    const uint64_t* __restrict__ E = p.cand + base;
-    const uint32_t* __restrict__ LB = p.cand_lb + base;
-    const int n = (t1 - t0) * kKQ;
-    if (tid == 0) {
-        s_nc = 0;
-        s_fail = p.force_fail;
+    if (p.trace && tid == 0) p.trace[((size_t)q * p.n_slices + g) * 8 + 0] = wall_clock64();
+    const int4 sl = p.slices[g];   // {first list, end list, first list of the L group, its end}
+    const int nt = sl.y - sl.x, n = nt * kKQ;
+    const size_t base = ((size_t)q * p.n_lists + sl.x) * kKQ;
+    constexpr int kEnt = kSliceLists * kKQ / kSettleThreads;   // entries per thread
+    uint64_t key[kEnt];
+#pragma unroll
+    for (int u = 0; u < kEnt; ++u) {
+        const int e = u * kSettleThreads + tid;
+        key[u] = e < n ? p.cand[base + e] : 0ull;
     }
-
-    // (a) L = the k-th best lower bound among the listed rows (0 when fewer than k are listed)
-    uint64_t lk = 0ull, thr = 0ull;
-    for (int b0 = wave * 64; b0 < n; b0 += kSettleThreads) {
-        const int i = b0 + lane;
-        const uint64_t key = i < n ? E[i] : 0ull;
-        const uint64_t lkey = key ? (((uint64_t)LB[i] << 32) | (uint32_t)i) : 0ull;
-        wave_offer(lkey, true, lk, thr, lane, k);
-    }
-    s_lists[wave * 64 + lane] = lane < k ? lk : 0ull;
-    __syncthreads();
-    if (wave == 0) {
-        for (int w = 1; w < NW; ++w) {
-            const uint64_t key = lane < k ? s_lists[w * 64 + lane] : 0ull;
-            wave_offer(key, true, lk, thr, lane, k);
-        }
-        if (lane == 0) s_L = (uint32_t)(thr >> 32);
-    }
-    __syncthreads();
-    const uint32_t Lb = s_L;
-
-    // (b) candidates: listed rows whose upper bound reaches L.  A full tile list whose last entry
-    // reaches L may have dropped a qualifying row → no certificate.
-    for (int i = tid; i < n; i += kSettleThreads) {
-        const uint64_t key = E[i];
-        if (!key || (uint32_t)(key >> 32) < Lb) continue;
-        if ((i % kKQ) == kKQ - 1) s_fail = 1;
-        const int slot = atomicAdd(&s_nc, 1);
-        if (slot < kSettleCap) s_cand[slot] = 0xFFFFFFFFu - (uint32_t)key;
-    }
-    __syncthreads();
-    const int nc = s_nc;
-    if (s_fail || nc > kSettleCap) {
-        if (tid == 0 && atomicOr(&p.flags[q], 1) == 0) atomicAdd(&p.counters[0], 1ull);
-        return;
-    }
-    if (tid == 0 && nc) atomicAdd(&p.counters[1], (unsigned long long)nc);
-
-    // (c) exact re-score with the streaming scan's arithmetic (same lane layout and fma order)
+    // query fragments and norm: independent of everything below, issued first
     const float4* __restrict__ Q = reinterpret_cast<const float4*>(p.q) + (size_t)q * UP;
     float4 qf[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) qf[j] = Q[t + j * L];
     const float qn = (!L2K && sim == SIM_COSINE) ? p.qnorm[q] : 0.0f;
-    lk = 0ull;
-    thr = 0ull;
-    for (int i0 = wave * R; i0 < nc; i0 += NW * R) {
-        const int ci = i0 + g;
+    const SegDev seg0 = p.segs[0];   // the common case (one segment per view) needs no lookup below
+    if (tid == 0) {
+        s_nc = 0;
+        s_exact = p.force_fail ? (nt >= 32 ? 0xFFFFFFFFu : (1u << nt) - 1u) : 0u;
+    }
+    if (tid < 64) s_top[tid] = 0ull;
+
+    // (a) L_g: the k-th best of 64 maxima of the best lower bounds of the group's lists (each over
+    // 64 lists).  Each maximum belongs to a distinct row, so L_g ≤ the shard's k-th best lower
+    // bound; every block of the group computes the same L_g.  Selection by rank (no serial
+    // insertion chain).
+    uint32_t mx = 0u;
+    {
+        constexpr int kPer = kLGroupLists / kSettleThreads;
+        const uint32_t* __restrict__ lm = p.list_lbmax + (size_t)q * p.n_lists;
+        const int ne = sl.w - sl.z;
+        uint32_t m[kPer];
+        // thread t holds lists (t & 3)·64 + (t >> 2) + 256·u: the 4 threads of a bucket t >> 2 hold
+        // lists ≡ bucket (mod 64), so a group of ≤ 64 lists keeps one list per bucket (exact k-th)
+        const int i0 = (tid & 3) * 64 + (tid >> 2);
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int i = u * kSettleThreads + i0;
+            m[u] = i < ne ? lm[sl.z + i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) mx = max(mx, m[u]);
+    }
+    if (p.trace && tid == 0) p.trace[((size_t)q * p.n_slices + g) * 8 + 1] = wall_clock64();
+    // 4 adjacent threads' maxima → 64 values (one per 64 lists), ranked by 64 threads
+#pragma unroll
+    for (int o = 1; o <= 2; o <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    if ((tid & 3) == 0) s_keys[tid >> 2] = ((uint64_t)mx << 32) | (uint32_t)(tid >> 2);   // distinct
+    __syncthreads();
+    if (tid < 64) {
+        const uint64_t mkey = s_keys[tid];
+        int rank = 0;
+#pragma unroll
+        for (int j = 0; j < 64; j += 2) {
+            const ulonglong2 v2 = *reinterpret_cast<const ulonglong2*>(s_keys + j);
+            rank += (v2.x > mkey) + (v2.y > mkey);
+        }
+        if (rank == k - 1) s_L = (uint32_t)(mkey >> 32);   // 0 when fewer than k lists hold rows
+    }
+    __syncthreads();
+    const uint32_t Lb = s_L;
+    // (b) overflowed lists → exact row ranges; the other lists' rows with ub ≥ L_g → candidates
+    bool reach[kEnt];
+#pragma unroll
+    for (int u = 0; u < kEnt; ++u) {
+        const int e = u * kSettleThreads + tid;
+        reach[u] = key[u] && (uint32_t)(key[u] >> 32) >= Lb;
+        if (reach[u] && (e % kKQ) == kKQ - 1) atomicOr(&s_exact, 1u << (e / kKQ));
+    }
+    __syncthreads();
+    const uint32_t exact = s_exact;
+#pragma unroll
+    for (int u = 0; u < kEnt; ++u) {
+        const int e = u * kSettleThreads + tid;
+        if (reach[u] && !((exact >> (e / kKQ)) & 1u)) s_cand[atomicAdd(&s_nc, 1)] = 0xFFFFFFFFu - (uint32_t)key[u];
+    }
+    if (tid < 64) s_top[tid] = 0ull;   // every thread has read L_g (barrier above)
+    __syncthreads();
+    const int nc = s_nc;
+    if (p.trace && tid == 0) p.trace[((size_t)q * p.n_slices + g) * 8 + 2] = wall_clock64();
+    if (tid == 0) {
+        if (exact) {
+            if (atomicOr(&p.flags[q], 1) == 0) atomicAdd(&p.counters[0], 1ull);
+            atomicAdd(&p.counters[2], (unsigned long long)__popc(exact));
+        }
+        if (nc) atomicAdd(&p.counters[1], (unsigned long long)nc);
+    }
+
+    // (c) exact re-score of the candidates
+    uint64_t lk = 0ull, thr = 0ull;
+    for (int i0 = wave * R; i0 < nc; i0 += kSettleWaves * R) {
+        const int ci = i0 + gr;
         const bool valid = ci < nc;
         const uint32_t vrow = s_cand[valid ? ci : 0];
         int sg = 0;
         for (int j = 1; j < p.n_segs; ++j)
             if ((int64_t)vrow >= p.seg_vrow[j]) sg = j;
-        const SegDev seg = p.segs[sg];
-        const int64_t ord = (int64_t)vrow - p.seg_vrow[sg];
+        const SegDev seg = sg == 0 ? seg0 : p.segs[sg];
+        const int64_t ord = (int64_t)vrow - (sg == 0 ? 0 : p.seg_vrow[sg]);
         const int32_t doc = seg.ord_to_doc ? seg.ord_to_doc[ord] : (int32_t)ord;
-        const float4* xr = static_cast<const float4*>(seg.rows) + ord * p.units;
-        // the row norm is loaded with the row (not after the reduction: one memory round trip)
         const float xn = (!L2K && sim == SIM_COSINE && valid) ? seg.xnorm_f[ord] : 0.0f;
-        float4 xv[V];
-#pragma unroll
-        for (int j = 0; j < V; ++j) {
-            const int f = t + j * L;
-            xv[j] = (valid && f < p.units) ? xr[f] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        float ax = 0.f, ay = 0.f, az = 0.f, aw = 0.f;
-#pragma unroll
-        for (int j = 0; j < V; ++j) {
-            const float4 x = xv[j];
-            if constexpr (L2K) {
-                const float dx = x.x - qf[j].x, dy = x.y - qf[j].y, dz = x.z - qf[j].z, dw = x.w - qf[j].w;
-                ax = fmaf(dx, dx, ax); ay = fmaf(dy, dy, ay); az = fmaf(dz, dz, az); aw = fmaf(dw, dw, aw);
-            } else {
-                ax = fmaf(x.x, qf[j].x, ax); ay = fmaf(x.y, qf[j].y, ay);
-                az = fmaf(x.z, qf[j].z, az); aw = fmaf(x.w, qf[j].w, aw);
-            }
-        }
-        float sum = (ax + ay) + (az + aw);
-#pragma unroll
-        for (int m = 1; m < L; m <<= 1) sum += __shfl_xor(sum, m);
-        float sc;
-        if constexpr (L2K) sc = score_f32_l2(sum);
-        else sc = score_f32(sim, sum, qn, xn);
-        const uint64_t key = valid ? make_key(sc, (uint32_t)(seg.doc_base + doc)) : 0ull;
-        wave_offer(key, t == 0, lk, thr, lane, k);
+        const float sc = settle_exact<L, V, L2K>(static_cast<const float4*>(seg.rows) + ord * p.units, valid,
+                                                 p.units, t, qf, sim, qn, xn);
+        wave_offer(valid ? make_key(sc, (uint32_t)(seg.doc_base + doc)) : 0ull, t == 0, lk, thr, lane, k);
     }
-    __syncthreads();
+    if (p.trace && tid == 0) p.trace[((size_t)q * p.n_slices + g) * 8 + 3] = wall_clock64();
+    // (c') overflowed lists: every accepted row of the scan wave's range (the scan's split of its
+    // tile: per_wave = ⌈rows / 4R_s⌉·R_s), walked by this block's 4 waves (filter pushdown included)
+    for (uint32_t bits = exact; bits; bits &= bits - 1u) {
+        const int list = sl.x + __builtin_ctz(bits);
+        const TileDev td = p.tiles[list >> 2];
+        const SegDev seg = p.segs[td.seg];
+        const uint64_t* abits = p.accept ? p.accept[td.seg] : nullptr;
+        const int64_t trows = td.row_end - td.row_begin;
+        const int64_t spw = ((trows + 4 * p.scan_R - 1) / (4 * p.scan_R)) * p.scan_R;
+        const int64_t lb0 = min(td.row_begin + (list & 3) * spw, td.row_end);
+        const int64_t lb1 = min(lb0 + spw, td.row_end);
+        const int64_t rows = lb1 - lb0;
+        const int64_t per_wave = ((rows + kSettleWaves * R - 1) / (kSettleWaves * R)) * R;
+        const int64_t wb = lb0 + wave * per_wave;
+        const int64_t we = min(wb + per_wave, lb1);
+        const float4* X = static_cast<const float4*>(seg.rows);
+        walk_rows<R>(wb, we, abits, seg.ord_to_doc, lane, gr, [&](const int64_t row, bool valid, bool known) {
+            int32_t doc = 0;
+            if (valid) {
+                doc = seg.ord_to_doc ? seg.ord_to_doc[row] : (int32_t)row;
+                if (abits && !known) valid = (abits[doc >> 6] >> (doc & 63)) & 1ull;
+            }
+            const float xn = (!L2K && sim == SIM_COSINE && valid) ? seg.xnorm_f[row] : 0.0f;
+            const float sc = settle_exact<L, V, L2K>(X + row * p.units, valid, p.units, t, qf, sim, qn, xn);
+            wave_offer(valid ? make_key(sc, (uint32_t)(seg.doc_base + doc)) : 0ull, t == 0, lk, thr, lane, k);
+        });
+    }
+    // (d) the slice's top k → part
     s_lists[wave * 64 + lane] = lane < k ? lk : 0ull;
     __syncthreads();
+    block_rank_topk<kSettleWaves>(s_lists, k, tid, s_top);
+    __syncthreads();
+    if (tid < k) p.part[((size_t)q * p.n_slices + g) * k + tid] = s_top[tid];
+    if (p.trace && tid == 0) {
+        p.trace[((size_t)q * p.n_slices + g) * 8 + 4] = wall_clock64();
+        p.trace[((size_t)q * p.n_slices + g) * 8 + 5] = (unsigned long long)nc;
+    }
+}
+
+// per (shard, query): the top k of the shard's slice lists → shard keys and counts
+__global__ __launch_bounds__(kSettleThreads) void sq8_settle_merge(SettleParams p) {
+    __shared__ uint64_t s_lists[kSettleWaves * 64];
+    __shared__ uint64_t s_top[64];
+    const int sh = blockIdx.x, q = blockIdx.y, S = p.n_shards, k = p.k;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g0 = p.shard_slice_begin[sh], g1 = p.shard_slice_begin[sh + 1];
+    const uint64_t* __restrict__ src = p.part + ((size_t)q * p.n_slices + g0) * k;
+    const int n = (g1 - g0) * k;
+    uint64_t lk = 0ull, thr = 0ull;
+    for (int i0 = wave * 64; i0 < n; i0 += kSettleThreads) {
+        const int i = i0 + lane;
+        wave_offer(i < n ? src[i] : 0ull, true, lk, thr, lane, k);
+    }
+    if (tid < 64) s_top[tid] = 0ull;
+    s_lists[wave * 64 + lane] = lane < k ? lk : 0ull;
+    __syncthreads();
+    block_rank_topk<kSettleWaves>(s_lists, k, tid, s_top);
+    __syncthreads();
     if (wave == 0) {
-        for (int w = 1; w < NW; ++w) {
-            const uint64_t key = lane < k ? s_lists[w * 64 + lane] : 0ull;
-            wave_offer(key, true, lk, thr, lane, k);
-        }
-        const size_t o = (size_t)q * S + s;
-        if (lane < k) p.shard_keys[o * k + lane] = lk;
-        const int cnt = __popcll(__ballot(lane < k && lk != 0ull));
+        const uint64_t key = lane < k ? s_top[lane] : 0ull;
+        const size_t o = (size_t)q * S + sh;
+        if (lane < k) p.shard_keys[o * k + lane] = key;
+        const int cnt = __popcll(__ballot(key != 0ull));
         if (lane == 0) p.shard_counts[o] = cnt;
     }
 }
@@ -602,8 +672,9 @@ static const SettleFn kSettle[9][2] = {OSK_SETTLE_ROW(4, 2),  OSK_SETTLE_ROW(8, 
                                        OSK_SETTLE_ROW(32, 8), OSK_SETTLE_ROW(64, 8), OSK_SETTLE_ROW(64, 16)};
 
 hipError_t launch_sq8_settle(int cfg, int nq, const SettleParams& p, hipStream_t s) {
-    hipLaunchKernelGGL(kSettle[cfg][p.sim == SIM_EUCLIDEAN ? 1 : 0], dim3(p.n_shards, nq), dim3(kSettleThreads), 0, s,
+    hipLaunchKernelGGL(kSettle[cfg][p.sim == SIM_EUCLIDEAN ? 1 : 0], dim3(p.n_slices, nq), dim3(kSettleThreads), 0, s,
                        p);
+    hipLaunchKernelGGL(sq8_settle_merge, dim3(p.n_shards, nq), dim3(kSettleThreads), 0, s, p);
     return hipGetLastError();
 }
 

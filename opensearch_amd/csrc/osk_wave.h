@@ -98,6 +98,26 @@ __device__ __forceinline__ void walk_rows(int64_t wb, int64_t we, const uint64_t
     }
 }
 
+// Top-k of NW wave lists in LDS (lists[w·64 + i], i < k, best first, 0 = empty; non-zero keys are
+// distinct): thread t < NW·k ranks its key against all NW·k keys and writes it to out[rank] when
+// rank < k.  Every thread works at once (a serial fold of NW lists by one wave costs ~NW·k insertion
+// rounds); out[] slots past the number of keys keep what the caller put there (zeros).
+template <int NW>
+__device__ __forceinline__ void block_rank_topk(const uint64_t* lists, int k, int tid, uint64_t* out) {
+    if (tid < NW * k) {
+        const int w = tid / k, i = tid - w * k;
+        const uint64_t key = lists[w * 64 + i];
+        if (key) {
+            int rank = 0;
+            for (int w2 = 0; w2 < NW; ++w2) {
+                const uint64_t* l2 = lists + w2 * 64;
+                for (int i2 = 0; i2 < k; ++i2) rank += l2[i2] > key;
+            }
+            if (rank < k) out[rank] = key;
+        }
+    }
+}
+
 // Fold the lists of waves 1..3 (in LDS) into wave 0's list.
 __device__ __forceinline__ void block_fold(const uint64_t* lists /*[4][64]*/, uint64_t& lk,
                                            uint64_t& thr, int lane, int k) {

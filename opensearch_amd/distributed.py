@@ -6,9 +6,10 @@ Mapping onto the reference:
     the shard results by score (SearchPhaseController.java:224-246).
   * Here shard s lives on rank `shard_owner(s)` (contiguous blocks, so a GPU owns 8/G shards of an
     8-shard index).  Each rank scans its shards in one launch and produces per-shard top-k lists of
-    8-byte hit keys; `torch.distributed.all_gather_into_tensor` (backend "nccl" = RCCL over xGMI on
-    the MI355X node, "gloo" in CPU tests) exchanges them; the coordinator reduce then runs on the
-    device (`osk_merge_device`) or, for host tensors, in the library's host reduce.
+    8-byte hit keys; one `torch.distributed.all_gather_into_tensor` (backend "nccl" = RCCL over xGMI
+    on the MI355X node, "gloo" in CPU tests) exchanges them; the coordinator reduce then runs on the
+    device straight over the gathered image (`osk_merge_device_ranked`) or, for host tensors, in the
+    library's host reduce.
 The exchange is k·B·8 bytes per shard — latency-bound, microseconds next to a millisecond scan.
 """
 from __future__ import annotations
@@ -36,67 +37,69 @@ def max_shards_per_rank(n_shards: int, world: int) -> int:
     return max(len(owned_shards(r, n_shards, world)) for r in range(world))
 
 
-def gather_shard_topk(keys: torch.Tensor, counts: torch.Tensor, world: int, group=None):
-    """keys [nq, S_l, k] int64 (uint64 bit pattern), counts [nq, S_l] int32 on every rank (S_l padded
-    to the same value everywhere) → gathered keys [nq, world·S_l, k], counts [nq, world·S_l]."""
-    nq, sl, k = keys.shape
-    if world == 1:   # nothing to exchange
-        return keys, counts
-    # concatenated along dim 0 (the layout both RCCL and gloo accept), viewed as [world, nq, …]
-    gk = torch.empty((world * nq, sl, k), dtype=keys.dtype, device=keys.device)
-    gc = torch.empty((world * nq, sl), dtype=counts.dtype, device=counts.device)
-    dist.all_gather_into_tensor(gk, keys.contiguous(), group=group)
-    dist.all_gather_into_tensor(gc, counts.contiguous(), group=group)
-    gk = gk.view(world, nq, sl, k)
-    gc = gc.view(world, nq, sl)
-    return (gk.permute(1, 0, 2, 3).reshape(nq, world * sl, k).contiguous(),
-            gc.permute(1, 0, 2).reshape(nq, world * sl).contiguous())
+class ShardExchange:
+    """The exchange step and the coordinator reduce of one rank, for a fixed (batch, k, from, size).
 
+    keys [nq, s_pad, k] int64 (uint64 hit-key bit patterns, best first, zero-padded) of this rank's
+    shards → ONE all-gather (RCCL over xGMI on the node, gloo in CPU tests) into a preallocated
+    rank-major buffer [world·nq, s_pad, k] → the coordinator reduce straight over that image
+    (device: osk_merge_device_ranked; host tensors: libosknn's host reduce).  A list's hit count is
+    its number of non-zero keys, so counts are not exchanged.  The outputs (scores, docs, shard
+    index, count, total hits, max score) are preallocated and overwritten by the next call."""
 
-def merge_gathered(keys: torch.Tensor, counts: torch.Tensor, shard_index: torch.Tensor, k: int,
-                   from_: int, size: int, device: int = 0, stream: int | None = None):
-    """Coordinator reduce over gathered per-shard lists → (scores, docs, shard_index, count,
-    total_hits, max_score) tensors.  Device tensors: osk_merge_device on the GPU.  Host tensors:
-    the library's host reduce (osk_topdocs_merge) per query."""
-    nq, S, _ = keys.shape
-    if keys.is_cuda:
-        dev = keys.device
-        scores = torch.empty((nq, size), dtype=torch.float32, device=dev)
-        docs = torch.empty((nq, size), dtype=torch.int32, device=dev)
-        shard = torch.empty((nq, size), dtype=torch.int32, device=dev)
-        count = torch.empty(nq, dtype=torch.int32, device=dev)
-        total = torch.empty(nq, dtype=torch.int64, device=dev)
-        mx = torch.empty(nq, dtype=torch.float32, device=dev)
-        si = shard_index.to(device=dev, dtype=torch.int32).contiguous()
-        check(lib().osk_merge_device(device, keys.data_ptr(), counts.data_ptr(), si.data_ptr(), nq, S, k,
-                                     from_, size, scores.data_ptr(), docs.data_ptr(), shard.data_ptr(),
-                                     count.data_ptr(), total.data_ptr(), mx.data_ptr(), stream))
-        return scores, docs, shard, count, total, mx
-    kk = keys.numpy().view(np.uint64)
-    cc = counts.numpy().astype(np.int32)
-    si = shard_index.numpy().astype(np.int32)
-    scores = np.empty((nq, size), np.float32)
-    docs = np.empty((nq, size), np.int32)
-    shard = np.empty((nq, size), np.int32)
-    count = np.empty(nq, np.int32)
-    total = np.empty(nq, np.int64)
-    mx = np.empty(nq, np.float32)
-    for q in range(nq):
-        sc = np.empty((S, k), np.float32)
-        dc = np.empty((S, k), np.int32)
-        kq = np.ascontiguousarray(kk[q])
-        check(lib().osk_decode_keys(ptr(kq), kq.size, ptr(sc), ptr(dc)))
-        cq = np.ascontiguousarray(cc[q])
-        c32, t64, m32 = C.c_int32(), C.c_int64(), C.c_float()
-        os_ = np.empty(size, np.float32)
-        od = np.empty(size, np.int32)
-        osh = np.empty(size, np.int32)
-        check(lib().osk_topdocs_merge(S, ptr(cq), ptr(sc), ptr(dc), k, ptr(si), None, from_, size, ptr(os_),
-                                      ptr(od), ptr(osh), C.byref(c32), C.byref(t64), C.byref(m32)))
-        scores[q], docs[q], shard[q] = os_, od, osh
-        count[q], total[q], mx[q] = c32.value, t64.value, m32.value
-    t = torch.from_numpy
-    return t(scores), t(docs), t(shard), t(count), t(total), t(mx)
+    def __init__(self, world: int, s_pad: int, nq: int, k: int, from_: int, size: int,
+                 global_shard_index: torch.Tensor, device: int | None = None, group=None):
+        self.world, self.s_pad, self.nq, self.k = world, s_pad, nq, k
+        self.from_, self.size, self.group = from_, size, group
+        self.device = device
+        dev = torch.device("cuda", device) if device is not None else torch.device("cpu")
+        self.gathered = torch.empty((world * nq, s_pad, k), dtype=torch.int64, device=dev)
+        self.si = global_shard_index.to(device=dev, dtype=torch.int32).contiguous()
+        self.out = (torch.empty((nq, size), dtype=torch.float32, device=dev),
+                    torch.empty((nq, size), dtype=torch.int32, device=dev),
+                    torch.empty((nq, size), dtype=torch.int32, device=dev),
+                    torch.empty(nq, dtype=torch.int32, device=dev),
+                    torch.empty(nq, dtype=torch.int64, device=dev),
+                    torch.empty(nq, dtype=torch.float32, device=dev))
+
+    def gather(self, keys: torch.Tensor) -> torch.Tensor:
+        if self.world == 1:   # nothing to exchange
+            return keys
+        dist.all_gather_into_tensor(self.gathered, keys, group=self.group)
+        return self.gathered
+
+    def reduce(self, gathered: torch.Tensor, stream: int | None = None):
+        nq, sl, k = self.nq, self.s_pad, self.k
+        if gathered.is_cuda:
+            sc, dc, sh, cnt, tot, mx = self.out
+            check(lib().osk_merge_device_ranked(self.device, gathered.data_ptr(), self.world, sl,
+                                                self.si.data_ptr(), nq, k, self.from_, self.size, sc.data_ptr(),
+                                                dc.data_ptr(), sh.data_ptr(), cnt.data_ptr(), tot.data_ptr(),
+                                                mx.data_ptr(), stream))
+            return self.out
+        kk = gathered.numpy().view(np.uint64).reshape(self.world, nq, sl, k)
+        si = self.si.numpy()
+        S = self.world * sl
+        for q in range(nq):
+            lists = np.ascontiguousarray(kk[:, q].reshape(S, k))
+            counts = np.count_nonzero(lists, axis=1).astype(np.int32)
+            sc = np.empty((S, k), np.float32)
+            dc = np.empty((S, k), np.int32)
+            check(lib().osk_decode_keys(ptr(lists), lists.size, ptr(sc), ptr(dc)))
+            c32, t64, m32 = C.c_int32(), C.c_int64(), C.c_float()
+            os_ = np.empty(self.size, np.float32)
+            od = np.empty(self.size, np.int32)
+            osh = np.empty(self.size, np.int32)
+            check(lib().osk_topdocs_merge(S, ptr(counts), ptr(sc), ptr(dc), k, ptr(si), None, self.from_, self.size,
+                                          ptr(os_), ptr(od), ptr(osh), C.byref(c32), C.byref(t64), C.byref(m32)))
+            self.out[0][q] = torch.from_numpy(os_)
+            self.out[1][q] = torch.from_numpy(od)
+            self.out[2][q] = torch.from_numpy(osh)
+            self.out[3][q], self.out[4][q], self.out[5][q] = c32.value, t64.value, m32.value
+        return self.out
+
+    def __call__(self, keys: torch.Tensor, stream: int | None = None):
+        return self.reduce(self.gather(keys), stream)
 
 
 class LocalShards:

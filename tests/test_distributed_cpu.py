@@ -2,8 +2,8 @@
 
 Each rank computes its shards' per-shard top-k (here with the oracle, since there is no GPU — the
 device path is covered by the -m gpu tests), encodes them as libosknn hit keys, and runs the same
-gather + coordinator-reduce code bench.py runs on the MI355X node (distributed.gather_shard_topk +
-merge_gathered, host reduce for host tensors).  Every rank must end with the oracle's global
+gather + coordinator-reduce code bench.py runs on the MI355X node (distributed.ShardExchange: one
+all-gather of the keys, host reduce for host tensors).  Every rank must end with the oracle's global
 TopDocs.merge(from, size) with shardIndex = global shard number."""
 import os
 import socket
@@ -57,12 +57,12 @@ def _worker(rank, world, port, from_, size, q):
                 kk = np.array([_key(a, b) for a, b in zip(sc, dc)], np.uint64)
                 keys[qi, j, : len(kk)] = torch.from_numpy(kk.view(np.int64))
                 counts[qi, j] = len(kk)
-        gk, gc = D.gather_shard_topk(keys, counts, world)
         gi = []
         for r in range(world):
             o = D.owned_shards(r, N_SHARDS, world)
             gi += o + [2**31 - 1] * (s_pad - len(o))
-        res = D.merge_gathered(gk, gc, torch.tensor(gi, dtype=torch.int32), K, from_, size)
+        xchg = D.ShardExchange(world, s_pad, NQ, K, from_, size, torch.tensor(gi, dtype=torch.int32))
+        res = xchg(keys)
         q.put((rank, [t.numpy().tolist() for t in res]))
     except Exception as e:   # surface the failure instead of letting the parent wait
         q.put((rank, repr(e)))

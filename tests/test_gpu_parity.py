@@ -298,3 +298,45 @@ def test_errors_are_codes_not_crashes():
             r.search_batch(np.ones((1, 9), np.float32), 5)
     finally:
         r.close()
+
+
+def _rand_lists(rng, world, nq, sl, k, tie_every=0):
+    """Rank-major gathered image [world·nq, sl, k] of random best-first, zero-padded key lists."""
+    keys = np.zeros((world * nq, sl, k), np.uint64)
+    for r in range(world):
+        for q in range(nq):
+            for j in range(sl):
+                c = int(rng.integers(0, k + 1))
+                sc = np.sort(rng.integers(0, 6, c) if tie_every else rng.random(c)).astype(np.float32)[::-1]
+                docs = np.sort(rng.choice(1000, c, replace=False)).astype(np.int64)
+                # same score → ascending doc inside one list (as a shard returns them)
+                order = np.lexsort((docs, -sc.astype(np.float64)))
+                sc, docs = sc[order], docs[order]
+                u = sc.view(np.uint32).astype(np.uint64)
+                sortable = np.where(u & 0x80000000, (~u) & 0xFFFFFFFF, u | 0x80000000)
+                keys[r * nq + q, j, :c] = (sortable << np.uint64(32)) | (np.uint64(0xFFFFFFFF) - docs.astype(np.uint64))
+    return keys
+
+
+@pytest.mark.parametrize("world,sl,k,from_,size,ties", [(1, 8, 10, 0, 10, 0), (2, 4, 10, 5, 8, 0), (3, 3, 16, 0, 12, 1),
+                                                         (8, 1, 10, 0, 10, 1), (4, 2, 64, 10, 30, 0)])
+def test_merge_device_ranked_matches_host_reduce(world, sl, k, from_, size, ties):
+    """osk_merge_device_ranked straight over an all-gather image == the host reduce of the same lists
+    (counts = non-zero keys; shardIndex = the owner's global shard numbers, pads INT32_MAX)."""
+    import torch
+    from opensearch_amd import distributed as D
+    rng = np.random.default_rng(world * 100 + sl)
+    nq = 5
+    keys = _rand_lists(rng, world, nq, sl, k, ties)
+    si = torch.tensor(rng.permutation(world * sl).astype(np.int32))
+    host = D.ShardExchange(world, sl, nq, k, from_, size, si)
+    want = [t.clone() for t in host.reduce(torch.from_numpy(keys.view(np.int64)))]
+    dev = D.ShardExchange(world, sl, nq, k, from_, size, si, device=0)
+    got = dev.reduce(torch.from_numpy(keys.view(np.int64)).cuda())
+    torch.cuda.synchronize()
+    for w, g in zip(want, got):
+        g = g.cpu()
+        if w.dtype == torch.float32:
+            assert torch.equal(w.view(torch.int32), g.view(torch.int32)), (w, g)
+        else:
+            assert torch.equal(w, g), (w, g)
