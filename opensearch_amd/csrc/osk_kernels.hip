@@ -592,7 +592,7 @@ __global__ __launch_bounds__(kBlock) void merge_coord(const uint64_t* __restrict
             atomicAdd(&s_total, (unsigned long long)c);
             if (c > 0) atomicMax(&s_max, (uint32_t)(top >> 32));
         }
-    } else {
+    } else if (topn < k) {   // (topn == k: the slot loop below sees every list entry)
         int hits = 0;
         for (int e = tid; e < n_shards * k; e += kBlock) {
             const int s = e / k, i = e - s * k;
@@ -616,8 +616,12 @@ __global__ __launch_bounds__(kBlock) void merge_coord(const uint64_t* __restrict
         s_doc[slot] = hit ? key_doc(key) : INT32_MAX;
         s_sidx[slot] = hit ? si : INT32_MAX;
         mine += hit;
+        if (!shard_counts && topn == k && hit && i == 0) atomicMax(&s_max, (uint32_t)(key >> 32));
     }
-    if (mine) atomicAdd(&s_n, mine);
+    if (mine) {
+        atomicAdd(&s_n, mine);
+        if (!shard_counts && topn == k) atomicAdd(&s_total, (unsigned long long)mine);
+    }
     __syncthreads();
     // rank of each hit = number of hits ordered before it; the slots are read 4 at a time with
     // independent 16-byte LDS loads (a scalar loop with a branch per slot is latency-bound)

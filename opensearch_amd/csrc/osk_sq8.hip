@@ -113,23 +113,33 @@ __global__ __launch_bounds__(kBlock) void sq8_prep(const float* __restrict__ src
                                                    int UP, int units8, float4* __restrict__ qpad,
                                                    float* __restrict__ qnorm, uint32_t* __restrict__ q8,
                                                    float4* __restrict__ qc, int* __restrict__ flags) {
-    const int lane = threadIdx.x & 63;
-    const int64_t r = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-    if (r >= nq_pad) return;
+    // one workgroup per query: every element is loaded once, by one thread, and the reductions are
+    // block-wide (a single wave per query walks 768 floats three times: ~8 µs of latency)
+    __shared__ float s_m[4];
+    __shared__ long long s_a[4];
+    __shared__ double s_e[4], s_x[4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t r = blockIdx.x;
     const bool real = r < nq;
     const float* b = src + r * (int64_t)dim;
     auto val = [&](int c) { return (real && c < dim) ? b[c] : 0.0f; };
-    const int dw = units8 * 4;
-    // padded fp32 copy + max|b|
+    const int dw = units8 * 4;   // int8 dwords (4 dims each); dw ≥ UP·… covers every real dim
+    // this thread's dwords: d = tid, tid + 256, … (4 dims each; the padded fp32 copy uses the same
+    // float4 units where d < UP)
+    constexpr int kPer = 4;      // dw ≤ 1024 (OSK_MAX_DIM 4096)
+    float4 x[kPer];
     float m = 0.0f;
-    for (int f = lane; f < UP; f += 64) {
-        const float4 v = make_float4(val(4 * f), val(4 * f + 1), val(4 * f + 2), val(4 * f + 3));
-        qpad[r * UP + f] = v;
-        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+        const int d = u * kBlock + tid;
+        x[u] = make_float4(val(4 * d), val(4 * d + 1), val(4 * d + 2), val(4 * d + 3));
+        if (d < UP) qpad[r * UP + d] = x[u];
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(x[u].x), fabsf(x[u].y)), fmaxf(fabsf(x[u].z), fabsf(x[u].w))));
     }
     for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-    // device-order |q|²: lane t of every L-lane group computes the same partial
-    {
+    if (lane == 0) s_m[wave] = m;
+    // device-order |q|² (wave 0): lane t of every L-lane group computes the same partial
+    if (wave == 0) {
         const int t = lane & (L - 1);
         float ax = 0.f, ay = 0.f, az = 0.f, aw = 0.f;
 #pragma unroll
@@ -143,21 +153,26 @@ __global__ __launch_bounds__(kBlock) void sq8_prep(const float* __restrict__ src
         for (int o = 1; o < L; o <<= 1) sn += __shfl_xor(sn, o);
         if (lane == 0) qnorm[r] = sn;
     }
+    __syncthreads();
+    m = fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]));
     const float s8 = m / 127.0f;
     long long a8 = 0;
     double e8 = 0.0, sx = 0.0;
     uint32_t* p0 = q8 + r * dw;
-    for (int d = lane; d < dw; d += 64) {
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+        const int d = u * kBlock + tid;
+        if (d >= dw) break;
+        const float xs[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
         uint32_t w0 = 0u;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const float x = val(4 * d + e);
-            const int q = s8 > 0.0f ? (int)fminf(fmaxf(rintf(x / s8), -127.0f), 127.0f) : 0;
-            w0 |= ((uint32_t)q & 0xFFu) << (8 * e);
-            a8 += (long long)(q * q);
-            const double r8 = (double)x - (double)s8 * (double)q;   // exact in double
+            const int qi = s8 > 0.0f ? (int)fminf(fmaxf(rintf(xs[e] / s8), -127.0f), 127.0f) : 0;
+            w0 |= ((uint32_t)qi & 0xFFu) << (8 * e);
+            a8 += (long long)(qi * qi);
+            const double r8 = (double)xs[e] - (double)s8 * (double)qi;   // exact in double
             e8 += r8 * r8;
-            sx += (double)x * (double)x;
+            sx += (double)xs[e] * (double)xs[e];
         }
         p0[d] = w0;
     }
@@ -167,6 +182,15 @@ __global__ __launch_bounds__(kBlock) void sq8_prep(const float* __restrict__ src
         sx += __shfl_xor(sx, o);
     }
     if (lane == 0) {
+        s_a[wave] = a8;
+        s_e[wave] = e8;
+        s_x[wave] = sx;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        a8 = s_a[0] + s_a[1] + s_a[2] + s_a[3];
+        e8 = s_e[0] + s_e[1] + s_e[2] + s_e[3];
+        sx = s_x[0] + s_x[1] + s_x[2] + s_x[3];
         const double A8 = (double)s8 * sqrt((double)a8) * (1.0 + 1e-12), B8 = sqrt(e8) * (1.0 + 1e-12);
         qc[r] = make_float4(s8, f32_round_up(B8), f32_round_up((A8 + B8) * (1.0 + 1e-12)), (float)sx);
         if (real) flags[r] = 0;
@@ -179,7 +203,7 @@ static const PrepFn kPrep[9] = {sq8_prep<4, 2>,  sq8_prep<8, 2>,  sq8_prep<8, 4>
 
 hipError_t launch_sq8_prep(int cfg, const float* src, int dim, int nq, int nq_pad, int UP, int units8, float4* qpad,
                            float* qnorm, void* q8, float4* qc, int* flags, hipStream_t s) {
-    hipLaunchKernelGGL(kPrep[cfg], dim3((nq_pad + 3) / 4), dim3(kBlock), 0, s, src, dim, nq, nq_pad, UP, units8, qpad,
+    hipLaunchKernelGGL(kPrep[cfg], dim3(nq_pad), dim3(kBlock), 0, s, src, dim, nq, nq_pad, UP, units8, qpad,
                        qnorm, static_cast<uint32_t*>(q8), qc, flags);
     return hipGetLastError();
 }
@@ -637,24 +661,68 @@ __global__ __launch_bounds__(kSettleThreads) void sq8_settle(SettleParams p) {
     }
 }
 
-// per (shard, query): the top k of the shard's slice lists → shard keys and counts
+// per (shard, query): the top k of the shard's slice lists → shard keys and counts.
+// Selection without a serial insertion chain: t = the k-th best of 64 bucket maxima of the lists'
+// first (best) keys — a lower bound of the k-th best key (distinct keys) — then only keys ≥ t
+// (≈ k … 2k of them) are ranked against each other in LDS.
+constexpr int kMergeCap = 2048;
 __global__ __launch_bounds__(kSettleThreads) void sq8_settle_merge(SettleParams p) {
-    __shared__ uint64_t s_lists[kSettleWaves * 64];
+    __shared__ __attribute__((aligned(16))) uint64_t s_b[64];
+    __shared__ __attribute__((aligned(16))) uint64_t s_surv[kMergeCap];
     __shared__ uint64_t s_top[64];
+    __shared__ int s_ns;
+    __shared__ uint64_t s_t;
     const int sh = blockIdx.x, q = blockIdx.y, S = p.n_shards, k = p.k;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g0 = p.shard_slice_begin[sh], g1 = p.shard_slice_begin[sh + 1];
     const uint64_t* __restrict__ src = p.part + ((size_t)q * p.n_slices + g0) * k;
-    const int n = (g1 - g0) * k;
-    uint64_t lk = 0ull, thr = 0ull;
-    for (int i0 = wave * 64; i0 < n; i0 += kSettleThreads) {
-        const int i = i0 + lane;
-        wave_offer(i < n ? src[i] : 0ull, true, lk, thr, lane, k);
-    }
-    if (tid < 64) s_top[tid] = 0ull;
-    s_lists[wave * 64 + lane] = lane < k ? lk : 0ull;
+    const int nl = g1 - g0, n = nl * k;
+    if (tid == 0) { s_ns = 0; s_t = 0ull; }
+    if (tid < 64) { s_top[tid] = 0ull; s_b[tid] = 0ull; }
     __syncthreads();
-    block_rank_topk<kSettleWaves>(s_lists, k, tid, s_top);
+    // bucket maxima of the lists' first keys (list l → bucket l mod 64)
+    for (int l = tid; l < nl; l += kSettleThreads) {
+        const uint64_t f = src[(size_t)l * k];
+        if (f) atomicMax(reinterpret_cast<unsigned long long*>(&s_b[l & 63]), (unsigned long long)f);
+    }
+    __syncthreads();
+    if (tid < 64) {
+        const uint64_t v = s_b[tid];
+        int rank = 0;
+#pragma unroll
+        for (int j = 0; j < 64; j += 2) {
+            const ulonglong2 v2 = *reinterpret_cast<const ulonglong2*>(s_b + j);
+            rank += (v2.x > v) + (v2.y > v);
+        }
+        // buckets are distinct keys or 0; with fewer than k non-empty buckets t stays 0
+        if (rank == k - 1 && v) s_t = v;
+    }
+    __syncthreads();
+    const uint64_t t = s_t;
+    for (int e = tid; e < n; e += kSettleThreads) {
+        const uint64_t key = src[e];
+        if (key && key >= t) {
+            const int slot = atomicAdd(&s_ns, 1);
+            if (slot < kMergeCap) s_surv[slot] = key;
+        }
+    }
+    __syncthreads();
+    const int ns = s_ns;
+    if (ns <= kMergeCap) {
+        for (int i = tid; i < ns; i += kSettleThreads) {
+            const uint64_t key = s_surv[i];
+            int rank = 0;
+            for (int j = 0; j < ns && rank < k; ++j) rank += s_surv[j] > key;
+            if (rank < k) s_top[rank] = key;
+        }
+    } else if (wave == 0) {   // degenerate (> kMergeCap keys ≥ t): one wave inserts them all
+        uint64_t lk = 0ull, thr = 0ull;
+        for (int i0 = 0; i0 < n; i0 += 64) {
+            const int i = i0 + lane;
+            wave_offer(i < n ? src[i] : 0ull, true, lk, thr, lane, k);
+        }
+        if (lane < k) s_top[lane] = lk;
+    }
     __syncthreads();
     if (wave == 0) {
         const uint64_t key = lane < k ? s_top[lane] : 0ull;

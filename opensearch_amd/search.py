@@ -7,6 +7,8 @@ for the k-NN path (server/src/main/java/org/opensearch/action/search/).
   * TopDocsStats        SearchPhaseController.java:839-901
   * QueryPhaseResultConsumer  QueryPhaseResultConsumer.java:160-277 (batched partial reduce,
                         default batched_reduce_size 512, SearchRequest.java:88)
+  * fill_doc_ids_to_load / get_hits  the fetch handoff: SearchPhaseController.java:274-284 and
+                        :340-405 as driven by FetchSearchPhase.innerRun (FetchSearchPhase.java:132-165)
 
 The merges run in libosknn's host reduce; the device reduce (`osk_merge_device`) implements the same
 ordering on the GPU after the RCCL all-gather (see distributed.py).
@@ -95,6 +97,7 @@ class ReducedQueryPhase:
     num_reduce_phases: int
     from_: int
     size: int
+    fetch_hits: int = 0      # Σ shard hit-list lengths (TopDocsStats.fetchHits, SearchPhaseController.java:874)
 
 
 class QueryPhaseResultConsumer:
@@ -146,4 +149,57 @@ class QueryPhaseResultConsumer:
             lst.append(r.top_docs)
         docs = sort_docs(False, lst, self.from_, self.size)
         return ReducedQueryPhase(self.stats.get_total_hits(), self.stats.max_score, docs,
-                                 self.num_reduce_phases + 1, self.from_, self.size)
+                                 self.num_reduce_phases + 1, self.from_, self.size, self.stats.fetch_hits)
+
+
+# ---- fetch handoff (adjacent to the hot path: maps the merged hits back to their shards) ----
+
+def fill_doc_ids_to_load(num_shards: int, shard_docs: Sequence[ScoreDoc]) -> list[list[int] | None]:
+    """SearchPhaseController.fillDocIdsToLoad (:274-284): per shard, the docs to fetch in merged
+    order (None for a shard with nothing to fetch)."""
+    out: list[list[int] | None] = [None] * num_shards
+    for sd in shard_docs:
+        if out[sd.shard_index] is None:
+            out[sd.shard_index] = []
+        out[sd.shard_index].append(sd.doc)
+    return out
+
+
+@dataclass
+class SearchHit:
+    """The slice of SearchHit the merge sets: docId, score and the shard it came from."""
+    doc_id: int
+    score: float = math.nan
+    shard: int | None = None
+
+
+@dataclass
+class SearchHits:
+    hits: list[SearchHit]
+    total_hits: TotalHits | None
+    max_score: float
+
+
+def get_hits(reduced: ReducedQueryPhase, fetch_results: dict[int, list[SearchHit]],
+             ignore_from: bool = False) -> SearchHits:
+    """SearchPhaseController.getHits (:340-405) for score-sorted (k-NN) results: walks the merged
+    ScoreDocs in order, takes the next fetched hit of each one's shard (each shard answered its
+    docIdsToLoad in that order), sets the hit's score from the ScoreDoc, and skips a hit whose shard
+    failed during fetch (absent from `fetch_results`)."""
+    counters = {s: 0 for s in fetch_results}
+    from_ = 0 if ignore_from else reduced.from_
+    n = min(reduced.fetch_hits - from_, reduced.size)
+    n = min(len(reduced.score_docs), n)
+    hits: list[SearchHit] = []
+    if fetch_results:
+        for sd in reduced.score_docs[: max(0, n)]:
+            fetched = fetch_results.get(sd.shard_index)
+            if fetched is None:   # shard failure during fetch: the hit is dropped
+                continue
+            i = counters[sd.shard_index]
+            counters[sd.shard_index] = i + 1
+            hit = fetched[i]
+            hit.shard = sd.shard_index
+            hit.score = sd.score
+            hits.append(hit)
+    return SearchHits(hits, reduced.total_hits, reduced.max_score)

@@ -124,3 +124,46 @@ def test_total_hits_tracking_threshold():
     assert th.value == 5 and th.relation == LU.Relation.GREATER_THAN_OR_EQUAL_TO
     assert st.max_score == 2.0
     assert math.isnan(SP.TopDocsStats().max_score)
+
+
+def _two_shard_fetch(fail_shard=None):
+    """FetchSearchPhaseTests.testFetchTwoDocument (:124-218) / testFailFetchOneDoc (:220-313): shard 0
+    returns (42, 1.0), shard 1 (84, 2.0), each with maxScore 2.0."""
+    c = SP.QueryPhaseResultConsumer(2)
+    for shard, doc, score in [(0, 42, 1.0), (1, 84, 2.0)]:
+        td = LU.TopDocs(LU.TotalHits(1), [LU.ScoreDoc(doc, score)])
+        c.consume_result(SP.QuerySearchResult(shard, td, 2.0))
+    r = c.reduce()
+    to_load = SP.fill_doc_ids_to_load(2, r.score_docs)
+    fetched = {s: [SP.SearchHit(d) for d in docs] for s, docs in enumerate(to_load)
+               if docs is not None and s != fail_shard}
+    return r, to_load, SP.get_hits(r, fetched)
+
+
+def test_fetch_two_document():
+    r, to_load, hits = _two_shard_fetch()
+    assert to_load == [[42], [84]]
+    assert hits.total_hits.value == 2 and hits.max_score == 2.0
+    assert [h.doc_id for h in hits.hits] == [84, 42]
+    assert [h.score for h in hits.hits] == [2.0, 1.0] and [h.shard for h in hits.hits] == [1, 0]
+
+
+def test_fail_fetch_one_doc():
+    _, _, hits = _two_shard_fetch(fail_shard=0)
+    assert hits.total_hits.value == 2
+    assert [h.doc_id for h in hits.hits] == [84]
+
+
+def test_fetch_with_from_offset():
+    """testReduceTopNWithFromOffset's shards (:1347-1392) through the fetch handoff: the 5 hits of
+    ranks 5…9, each fetched from its own shard in merged order."""
+    c = SP.QueryPhaseResultConsumer(4, from_=5, size=5)
+    score = 100
+    for i in range(4):
+        c.consume_result(_result(i, [score, score - 1, score - 2], [10 * i, 10 * i + 1, 10 * i + 2], 5, 5))
+        score -= 3
+    r = c.reduce()
+    to_load = SP.fill_doc_ids_to_load(4, r.score_docs)
+    hits = SP.get_hits(r, {s: [SP.SearchHit(d) for d in docs] for s, docs in enumerate(to_load) if docs})
+    assert [h.score for h in hits.hits] == [95.0, 94.0, 93.0, 92.0, 91.0]
+    assert [(h.shard, h.doc_id) for h in hits.hits] == [(1, 12), (2, 20), (2, 21), (2, 22), (3, 30)]

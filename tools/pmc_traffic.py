@@ -31,7 +31,8 @@ def main():
     w, _ = load(a.write)
     out = {}
     for k in f:
-        wide = "scan_" in k   # 16-B-per-lane streaming loads: apply the gfx950 ×2 FETCH correction
+        # 16-B-per-lane streaming loads: apply the gfx950 ×2 FETCH correction
+        wide = "scan_f32<" in k or "scan_i8<" in k or "sq8_scan<" in k
         rd = f[k] * 1024 * (2 if wide else 1)
         wr = w.get(k, 0.0) * 1024
         out[k] = {"dispatches": n[k], "fetch_kib_raw": f[k], "write_kib_raw": w.get(k),
