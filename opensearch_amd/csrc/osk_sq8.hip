@@ -275,9 +275,52 @@ __device__ __forceinline__ int4 load_i4_nt(const int4* p) {
     return make_int4(v.x, v.y, v.z, v.w);
 }
 
+// Reduce-scatter of NQ per-query partial dots over the L lanes of a row: H = min(log2 NQ, log2 L)
+// halving stages (lane keeps the half of its queries selected by one lane bit and adds the partner's
+// copy of them), then butterflies over the remaining lane bits.  Lane t ends with the full sums of
+// queries rs_base(t) + [0, P), P = NQ >> H, replicated over the butterfly bits.  Exact: int32 sums.
+constexpr int ilog2c(int x) { return x <= 1 ? 0 : 1 + ilog2c(x >> 1); }
+template <int L, int NQ>
+struct RsShape {
+    static constexpr int H = ilog2c(NQ) < ilog2c(L) ? ilog2c(NQ) : ilog2c(L);
+    static constexpr int P = NQ >> H;
+    static constexpr int REP = L >> H;   // lanes holding the same (row, query) sums
+};
+template <int L, int NQ>
+__device__ __forceinline__ void rs_reduce(int (&acc)[NQ], int t) {
+    constexpr int H = RsShape<L, NQ>::H, P = RsShape<L, NQ>::P;
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+        const int h = NQ >> (i + 1), msk = L >> (i + 1);
+        const bool up = (t & msk) != 0;
+#pragma unroll
+        for (int j = 0; j < h; ++j) {
+            // both values loaded first: a select between two elements' addresses would push
+            // acc[] to scratch
+            const int lo_v = acc[j], hi_v = acc[h + j];
+            const int keep = up ? hi_v : lo_v;
+            const int send = up ? lo_v : hi_v;
+            acc[j] = keep + __shfl_xor(send, msk);
+        }
+    }
+#pragma unroll
+    for (int m = L >> (H + 1); m >= 1; m >>= 1)
+#pragma unroll
+        for (int q = 0; q < P; ++q) acc[q] += __shfl_xor(acc[q], m);
+}
+template <int L, int NQ>
+__device__ __forceinline__ int rs_base(int t) {
+    int b = 0;
+#pragma unroll
+    for (int i = 0; i < RsShape<L, NQ>::H; ++i) b += (t & (L >> (i + 1))) ? (NQ >> (i + 1)) : 0;
+    return b;
+}
+
 // ------------------------------------------------------------------------------------------------
 // prefilter scan: a row is L lanes × V 16-byte int8 units; U row groups per wave-iteration are
-// loaded before any is reduced (≈ U·V·1 KiB in flight per wave).
+// loaded before any is reduced (≈ U·V·1 KiB in flight per wave).  NQ > 1: the per-query partial
+// dots are reduce-scattered (rs_reduce) so each lane finishes the bound and quick test of P
+// (row, query) pairs instead of all NQ.
 // ------------------------------------------------------------------------------------------------
 template <int L, int V, int NQ, int U>
 __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
@@ -291,11 +334,14 @@ __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
     const uint32_t vbase = (uint32_t)p.seg_vrow[tile.seg];
     const int u8 = p.units8, sim = p.sim;
 
-    int4 qf[NQ][V];
-    float4 qc[NQ];
-    float qnd[NQ], sqn[NQ];
-#pragma unroll
-    for (int b = 0; b < NQ; ++b) {
+    // NQ == 1: the query fragment and the wave's list in VGPRs.  NQ > 1: all queries in LDS
+    // ([NQ][units8] int4) and every wave's per-query lists in LDS ([4][NQ][kKQ] keys + lower bounds),
+    // so that no per-query array needs a dynamic register index.
+    extern __shared__ __attribute__((aligned(16))) int4 sq[];
+    uint64_t* s_lk = reinterpret_cast<uint64_t*>(sq + (NQ > 1 ? NQ * u8 : 0));
+    uint32_t* s_lp = reinterpret_cast<uint32_t*>(s_lk + 4 * NQ * kKQ);
+    int4 qf[1][NQ == 1 ? V : 1];
+    if constexpr (NQ == 1) {
 #pragma unroll
         for (int j = 0; j < V; ++j) {
             // clamped index + mask (a select between the global pointer and a zero local would live
@@ -303,13 +349,20 @@ __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
             const int f = t + j * L;
             const int fc = f < u8 ? f : 0;
             const int msk = f < u8 ? -1 : 0;
-            const int4 v = p.q8[b * u8 + fc];
-            qf[b][j] = make_int4(v.x & msk, v.y & msk, v.z & msk, v.w & msk);
+            const int4 v = p.q8[fc];
+            qf[0][j] = make_int4(v.x & msk, v.y & msk, v.z & msk, v.w & msk);
         }
-        qc[b] = p.qc[b];
-        qnd[b] = sim == SIM_COSINE ? p.qn_dev[b] : 0.0f;
-        sqn[b] = sqrtf(qnd[b]);
+    } else {
+        for (int i = tid; i < NQ * u8; i += kBlock) sq[i] = p.q8[i];
+        for (int i = tid; i < 4 * NQ * kKQ; i += kBlock) {
+            s_lk[i] = 0ull;
+            s_lp[i] = 0u;
+        }
+        __syncthreads();
     }
+    const float4 qc0 = p.qc[0];
+    const float qnd0 = sim == SIM_COSINE ? p.qn_dev[0] : 0.0f;
+    const float sqn0 = sqrtf(qnd0);
 
     const int64_t rows = tile.row_end - tile.row_begin;
     const int64_t per_wave = ((rows + 4 * R - 1) / (4 * R)) * R;
@@ -317,15 +370,19 @@ __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
     const int64_t we = min(wb + per_wave, tile.row_end);
     const uint64_t* abits = p.accept ? p.accept[tile.seg] : nullptr;
 
-    uint64_t lk[NQ], thr[NQ];
-    uint32_t lp[NQ];
-    float tq[NQ];
+    uint64_t lk0 = 0ull, thr0 = 0ull;   // NQ == 1: the wave's list
+    uint32_t lp0 = 0u;
+    float tq0 = sq8_quick(sim, 0ull, 0.0f, 0.0f);
+    // NQ > 1: the P queries this lane finishes after the reduce-scatter, and their thresholds
+    constexpr int P = RsShape<L, NQ>::P;
+    const int qb = rs_base<L, NQ>(t);
+    const bool rep = (t & (RsShape<L, NQ>::REP - 1)) == 0;
+    float tql[P];
+    float4 qcl[P];
 #pragma unroll
-    for (int b = 0; b < NQ; ++b) {
-        lk[b] = 0ull;
-        thr[b] = 0ull;
-        lp[b] = 0u;
-        tq[b] = sq8_quick(sim, 0ull, 0.0f, 0.0f);
+    for (int j = 0; j < P; ++j) {
+        tql[j] = sq8_quick(sim, 0ull, 0.0f, 0.0f);
+        qcl[j] = p.qc[qb + j];   // per-lane load (a select chain over qc[] becomes a scratch index)
     }
     uint32_t nvis = 0;
 
@@ -362,33 +419,107 @@ __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
             }
             ax[u] = valid[u] ? AX[row[u]] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
+        if constexpr (NQ == 1) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            nvis += __popcll(__ballot(t == 0 && valid[u]));
-            const float sx = sim == SIM_COSINE ? sqrtf(ax[u].w) : 0.0f;
-#pragma unroll
-            for (int b = 0; b < NQ; ++b) {
+            for (int u = 0; u < U; ++u) {
+                nvis += __popcll(__ballot(t == 0 && valid[u]));
+                const float sx = sim == SIM_COSINE ? sqrtf(ax[u].w) : 0.0f;
                 int acc = 0;
 #pragma unroll
                 for (int j = 0; j < V; ++j) {
-                    acc = __builtin_amdgcn_sdot4(xv[u][j].x, qf[b][j].x, acc, false);
-                    acc = __builtin_amdgcn_sdot4(xv[u][j].y, qf[b][j].y, acc, false);
-                    acc = __builtin_amdgcn_sdot4(xv[u][j].z, qf[b][j].z, acc, false);
-                    acc = __builtin_amdgcn_sdot4(xv[u][j].w, qf[b][j].w, acc, false);
+                    acc = __builtin_amdgcn_sdot4(xv[u][j].x, qf[0][j].x, acc, false);
+                    acc = __builtin_amdgcn_sdot4(xv[u][j].y, qf[0][j].y, acc, false);
+                    acc = __builtin_amdgcn_sdot4(xv[u][j].z, qf[0][j].z, acc, false);
+                    acc = __builtin_amdgcn_sdot4(xv[u][j].w, qf[0][j].w, acc, false);
                 }
 #pragma unroll
                 for (int m = 1; m < L; m <<= 1) acc += __shfl_xor(acc, m);
                 float lo, hi;
-                sq8_bounds(sim, (float)acc, ax[u], qc[b], p.gam, p.g2, lo, hi);
-                const bool pass = valid[u] && sq8_pass(sim, lo, hi, tq[b], sx);
+                sq8_bounds(sim, (float)acc, ax[u], qc0, p.gam, p.g2, lo, hi);
+                const bool pass = valid[u] && sq8_pass(sim, lo, hi, tq0, sx);
                 if (__ballot(pass && t == 0)) {   // wave-uniform: rare once the list has filled
                     float xnd = 0.0f;
                     if (sim == SIM_COSINE && pass) xnd = seg.xnorm_f[row[u]];
-                    const float ub = sim == SIM_EUCLIDEAN ? score_f32_l2(lo) : score_f32(sim, hi, qnd[b], xnd);
-                    const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qnd[b], xnd);
+                    const float ub = sim == SIM_EUCLIDEAN ? score_f32_l2(lo) : score_f32(sim, hi, qnd0, xnd);
+                    const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qnd0, xnd);
                     const uint64_t key = pass ? make_key(ub, vbase + (uint32_t)row[u]) : 0ull;
-                    wave_offer2(key, float_to_sortable(lb), pass && t == 0, lk[b], lp[b], thr[b], lane, kKQ);
-                    tq[b] = sq8_quick(sim, thr[b], sqn[b], p.cos_slack);
+                    wave_offer2(key, float_to_sortable(lb), pass && t == 0, lk0, lp0, thr0, lane, kKQ);
+                    tq0 = sq8_quick(sim, thr0, sqn0, p.cos_slack);
+                }
+            }
+        } else {
+            // every query's fragment is read from LDS once per U row groups (registers hold rows)
+            int acc[U][NQ];
+#pragma unroll
+            for (int b = 0; b < NQ; ++b) {
+                int4 qv[V];
+#pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    const int f = t + j * L;
+                    qv[j] = sq[b * u8 + (f < u8 ? f : 0)];
+                    if (f >= u8) qv[j] = make_int4(0, 0, 0, 0);
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    int a = 0;
+#pragma unroll
+                    for (int j = 0; j < V; ++j) {
+                        a = __builtin_amdgcn_sdot4(xv[u][j].x, qv[j].x, a, false);
+                        a = __builtin_amdgcn_sdot4(xv[u][j].y, qv[j].y, a, false);
+                        a = __builtin_amdgcn_sdot4(xv[u][j].z, qv[j].z, a, false);
+                        a = __builtin_amdgcn_sdot4(xv[u][j].w, qv[j].w, a, false);
+                    }
+                    acc[u][b] = a;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                nvis += __popcll(__ballot(t == 0 && valid[u]));
+                const float sx = sim == SIM_COSINE ? sqrtf(ax[u].w) : 0.0f;
+                rs_reduce<L, NQ>(acc[u], t);
+                bool pass[P];
+                float lo[P], hi[P];
+                bool anyp = false;
+#pragma unroll
+                for (int j = 0; j < P; ++j) {
+                    sq8_bounds(sim, (float)acc[u][j], ax[u], qcl[j], p.gam, p.g2, lo[j], hi[j]);
+                    pass[j] = valid[u] && rep && sq8_pass(sim, lo[j], hi[j], tql[j], sx);
+                    anyp |= pass[j];
+                }
+                if (__ballot(anyp)) {   // wave-uniform: rare once the lists have filled
+                    float xnd = 0.0f;
+                    if (sim == SIM_COSINE && anyp) xnd = seg.xnorm_f[row[u]];
+                    uint32_t qm = 0u;   // queries with a passing lane (wave-uniform)
+#pragma unroll
+                    for (int j = 0; j < P; ++j) qm |= pass[j] ? (1u << (qb + j)) : 0u;
+                    uint32_t wq = 0u;
+#pragma unroll
+                    for (int b = 0; b < NQ; ++b) wq |= __ballot((qm >> b) & 1u) ? (1u << b) : 0u;
+                    while (wq) {
+                        const int b = __builtin_ctz(wq);
+                        wq &= wq - 1u;
+                        // the wave's list of query b: LDS → lanes 0..kKQ-1, insert, back to LDS
+                        const int o0 = (wave * NQ + b) * kKQ;
+                        uint64_t lkb = lane < kKQ ? s_lk[o0 + lane] : 0ull;
+                        uint32_t lpb = lane < kKQ ? s_lp[o0 + lane] : 0u;
+                        uint64_t thrb = readlane64(lkb, kKQ - 1);
+                        const float qnb = sim == SIM_COSINE ? p.qn_dev[b] : 0.0f;
+#pragma unroll
+                        for (int j = 0; j < P; ++j) {
+                            const bool o = pass[j] && (qb + j == b);
+                            const float ub = sim == SIM_EUCLIDEAN ? score_f32_l2(lo[j]) : score_f32(sim, hi[j], qnb, xnd);
+                            const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi[j]) : score_f32(sim, lo[j], qnb, xnd);
+                            const uint64_t key = o ? make_key(ub, vbase + (uint32_t)row[u]) : 0ull;
+                            wave_offer2(key, float_to_sortable(lb), o, lkb, lpb, thrb, lane, kKQ);
+                        }
+                        if (lane < kKQ) {
+                            s_lk[o0 + lane] = lkb;
+                            s_lp[o0 + lane] = lpb;
+                        }
+                        const float nt = sq8_quick(sim, thrb, sqrtf(qnb), p.cos_slack);
+#pragma unroll
+                        for (int jj = 0; jj < P; ++jj) tql[jj] = (qb + jj == b) ? nt : tql[jj];
+                    }
                 }
             }
         }
@@ -419,16 +550,21 @@ __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
     // one list per wave (its own row range of the tile): finer lists overflow the certificate less
     // often than one folded list per tile, and need no LDS fold.  With it, the list's best lower
     // bound (the settle's threshold is selected among these, one distinct row per list).
-#pragma unroll
     for (int b = 0; b < NQ; ++b) {
-        uint32_t m = (lane < kKQ && lk[b]) ? lp[b] : 0u;
+        uint64_t lkb = lk0;
+        uint32_t lpb = lp0;
+        if constexpr (NQ > 1) {
+            lkb = lane < kKQ ? s_lk[(wave * NQ + b) * kKQ + lane] : 0ull;
+            lpb = lane < kKQ ? s_lp[(wave * NQ + b) * kKQ + lane] : 0u;
+        }
+        uint32_t m = (lane < kKQ && lkb) ? lpb : 0u;
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
         if (b < p.q_count) {
             const size_t l = (size_t)(p.q0 + b) * p.n_lists + blockIdx.x * 4 + wave;
             if (lane < kKQ) {
-                p.cand[l * kKQ + lane] = lk[b];
-                p.cand_lb[l * kKQ + lane] = lp[b];
+                p.cand[l * kKQ + lane] = lkb;
+                p.cand_lb[l * kKQ + lane] = lpb;
             }
             if (lane == 0) p.list_lbmax[l] = m;
         }
@@ -444,13 +580,15 @@ int sq8_lanes(int u8) {   // L of the scan's config (its rows per wave-iteration
     return kL[sq8_cfg(u8)];
 }
 using Sq8Fn = void (*)(Sq8Params);
-#define OSK_SQ8_ROW(L, V) {sq8_scan<L, V, 1, 4>, sq8_scan<L, V, 2, 4>, sq8_scan<L, V, 4, 2>, sq8_scan<L, V, 8, 1>}
+#define OSK_SQ8_ROW(L, V) {sq8_scan<L, V, 1, 4>, sq8_scan<L, V, 2, 4>, sq8_scan<L, V, 4, 4>, sq8_scan<L, V, 8, 2>}
 static const Sq8Fn kSq8[8][4] = {OSK_SQ8_ROW(4, 1),  OSK_SQ8_ROW(8, 1),  OSK_SQ8_ROW(16, 1), OSK_SQ8_ROW(16, 2),
                                  OSK_SQ8_ROW(16, 3), OSK_SQ8_ROW(16, 4), OSK_SQ8_ROW(32, 4), OSK_SQ8_ROW(64, 4)};
 
 hipError_t launch_sq8_scan(int nq, const Sq8Params& p, hipStream_t s) {
     const int slot = nq <= 1 ? 0 : nq <= 2 ? 1 : nq <= 4 ? 2 : 3;
-    hipLaunchKernelGGL(kSq8[sq8_cfg(p.units8)][slot], dim3(p.n_tiles), dim3(kBlock), 0, s, p);
+    // NQ > 1: the queries and the 4 waves' per-query lists in LDS
+    const size_t lds = slot == 0 ? 0 : (size_t)(1 << slot) * (p.units8 * 16 + 4 * kKQ * 12);
+    hipLaunchKernelGGL(kSq8[sq8_cfg(p.units8)][slot], dim3(p.n_tiles), dim3(kBlock), lds, s, p);
     return hipGetLastError();
 }
 
