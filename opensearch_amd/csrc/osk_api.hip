@@ -232,15 +232,22 @@ struct osk_view {
     DevBuf d_slices, d_shard_slice_begin, ws_part;
     int64_t sq8_calls = 0;
     std::mutex mu;
-    // scan-kernel timing (osk_view_profile): events bracket the scan launches on the search stream
+    // scan-kernel timing (osk_view_profile): a ring of (start, stop) event pairs, one per search call,
+    // folded into scan_ms when a slot is reused (kEvRing calls later: long complete, no host wait) or
+    // when the total is read — timing never blocks the host inside the timed loop
+    static constexpr int kEvRing = 64;
     bool profile = false;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev_start[kEvRing] = {}, ev_stop[kEvRing] = {};
+    bool ev_pending[kEvRing] = {};
+    int64_t ev_next = 0;                  // calls started since enabling
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;   // the current call's pair
     double scan_ms = 0.0;
     int64_t scan_calls = 0;
-    bool pending = false;
     ~osk_view() {
-        if (ev0) (void)hipEventDestroy(ev0);
-        if (ev1) (void)hipEventDestroy(ev1);
+        for (int i = 0; i < kEvRing; ++i) {
+            if (ev_start[i]) (void)hipEventDestroy(ev_start[i]);
+            if (ev_stop[i]) (void)hipEventDestroy(ev_stop[i]);
+        }
     }
 };
 
@@ -358,8 +365,14 @@ int32_t osk_tune_set(const char* key, int64_t value) {
     } else if (k == "settle_trace") {
         g_tuning.settle_trace = value != 0;
     } else if (k == "tiles_target") {
-        OSK_REQUIRE(value >= 1 && value <= (1 << 22), "tiles_target out of range");
+        OSK_REQUIRE(value >= 0 && value <= (1 << 22), "tiles_target out of range");
         g_tuning.tiles_target = (int)value;
+    } else if (k == "tile_slots_per_cu") {
+        OSK_REQUIRE(value >= 1 && value <= 64, "tile_slots_per_cu out of range");
+        g_tuning.tile_slots_per_cu = (int)value;
+    } else if (k == "tile_max_rounds") {
+        OSK_REQUIRE(value >= 1 && value <= 1024, "tile_max_rounds out of range");
+        g_tuning.tile_max_rounds = (int)value;
     } else if (k == "tile_min_rows") {
         OSK_REQUIRE(value >= 1 && value <= (1 << 24), "tile_min_rows out of range");
         g_tuning.tile_min_rows = (int)value;
@@ -508,14 +521,48 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
     v->shard_index.resize(n_shards);
     for (int s = 0; s < n_shards; ++s) v->shard_index[s] = shard_index ? shard_index[s] : s;
 
-    // tiles: ~2048 per view (8 per CU), never smaller than 8 row-groups per wave
+    // tiles: a whole number of "rounds" of the chip's resident workgroup slots (CUs × tile_slots_per_cu;
+    // the scan kernels run 4 waves/SIMD = 4 workgroups of 256 threads per CU), so every round is full
+    // and no tail round runs with most slots idle (profiles/r01e/tiles_ab.txt: 1.25M rows, 1024 tiles
+    // 0.190 ms vs 1221 tiles 0.219 ms).  Rounds grow with the view up to tile_max_rounds; a tile never
+    // drops below 8 row-groups per wave nor tile_min_rows rows.
     static const int kL[9] = {4, 8, 8, 16, 16, 16, 32, 64, 64};
     const int R = 64 / kL[v->cfg];
     int64_t total = 0;
     for (int i = 0; i < n_segs; ++i) total += segs[i]->n_rows;
     const int64_t min_rows = std::max<int64_t>(4LL * R * 8, g_tuning.tile_min_rows);
-    const int64_t target = std::max(1, g_tuning.tiles_target);
-    const int64_t rows_per_tile = std::max<int64_t>(min_rows, (total + target - 1) / target);
+    int64_t target = g_tuning.tiles_target;
+    if (target <= 0) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s0->device) != hipSuccess || cus <= 0)
+            cus = 256;
+        const int64_t slots = (int64_t)cus * std::max(1, g_tuning.tile_slots_per_cu);
+        const int64_t rounds = std::min<int64_t>(std::max(1, g_tuning.tile_max_rounds),
+                                                 std::max<int64_t>(1, total / (slots * min_rows)));
+        target = rounds * slots;
+    }
+    // split the target over segments in proportion to their rows (largest remainder), each segment's
+    // share capped so its tiles keep ≥ min_rows rows
+    std::vector<int64_t> seg_tiles(n_segs, 0);
+    {
+        int64_t given = 0;
+        std::vector<std::pair<double, int>> rem;
+        for (int i = 0; i < n_segs; ++i) {
+            const int64_t n = segs[i]->n_rows;
+            if (n == 0) continue;
+            const double share = total > 0 ? (double)n * (double)target / (double)total : 1.0;
+            const int64_t cap = std::max<int64_t>(1, (n + min_rows - 1) / min_rows);
+            seg_tiles[i] = std::min<int64_t>(cap, std::max<int64_t>(1, (int64_t)share));
+            given += seg_tiles[i];
+            rem.push_back({share - (double)(int64_t)share, i});
+        }
+        std::sort(rem.begin(), rem.end(), [](auto& a, auto& b) { return a.first > b.first || (a.first == b.first && a.second < b.second); });
+        for (size_t j = 0; j < rem.size() && given < target; ++j) {
+            const int i = rem[j].second;
+            const int64_t cap = std::max<int64_t>(1, (segs[i]->n_rows + min_rows - 1) / min_rows);
+            if (seg_tiles[i] < cap) { ++seg_tiles[i]; ++given; }
+        }
+    }
     std::vector<TileDev> tiles;
     v->shard_tile_begin.assign(n_shards + 1, 0);
     for (int sh = 0; sh < n_shards; ++sh) {
@@ -524,10 +571,9 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
             if ((seg_shard ? seg_shard[i] : 0) != sh) continue;
             const int64_t n = segs[i]->n_rows;
             if (n == 0) continue;
-            const int64_t nt = (n + rows_per_tile - 1) / rows_per_tile;
-            const int64_t per = (n + nt - 1) / nt;
-            for (int64_t b = 0; b < n; b += per)
-                tiles.push_back(TileDev{i, sh, b, std::min(n, b + per)});
+            const int64_t nt = seg_tiles[i];
+            for (int64_t t = 0; t < nt; ++t)   // balanced split: tile t = rows [n·t/nt, n·(t+1)/nt)
+                tiles.push_back(TileDev{i, sh, n * t / nt, n * (t + 1) / nt});
         }
     }
     v->shard_tile_begin[n_shards] = (int32_t)tiles.size();
@@ -580,24 +626,42 @@ int32_t osk_view_release(osk_view* view) {
 
 namespace {
 
-int32_t profile_begin(osk_view* v, hipStream_t st) {
-    if (v->pending) {   // fold the previous call's interval (already complete or we wait)
-        float ms = 0.f;
-        OSK_HIP(hipEventSynchronize(v->ev1));
-        OSK_HIP(hipEventElapsedTime(&ms, v->ev0, v->ev1));
-        v->scan_ms += ms;
-        v->scan_calls += 1;
-        v->pending = false;
-    }
-    OSK_HIP(hipEventRecord(v->ev0, st));
+// Scan-kernel timing (osk_view_profile).  The streaming and prefilter scans stamp v->ev0 / v->ev1
+// from their own dispatch packets (first and last launch of the call: launch_ev); the MFMA path,
+// several launches, brackets them with event records (record = true).
+int32_t profile_fold(osk_view* v, int slot) {
+    if (!v->ev_pending[slot]) return OSK_OK;
+    float ms = 0.f;
+    OSK_HIP(hipEventSynchronize(v->ev_stop[slot]));
+    OSK_HIP(hipEventElapsedTime(&ms, v->ev_start[slot], v->ev_stop[slot]));
+    v->scan_ms += ms;
+    v->scan_calls += 1;
+    v->ev_pending[slot] = false;
     return OSK_OK;
 }
 
-int32_t profile_end(osk_view* v, hipStream_t st) {
-    if (!v->profile) return OSK_OK;
-    OSK_HIP(hipEventRecord(v->ev1, st));
-    v->pending = true;
+int32_t profile_begin(osk_view* v, hipStream_t st, bool record) {
+    const int slot = (int)(v->ev_next++ % osk_view::kEvRing);
+    int32_t rc = profile_fold(v, slot);   // the call kEvRing calls ago
+    if (rc) return rc;
+    v->ev0 = v->ev_start[slot];
+    v->ev1 = v->ev_stop[slot];
+    v->ev_pending[slot] = false;
+    if (record) OSK_HIP(hipEventRecord(v->ev0, st));
     return OSK_OK;
+}
+
+int32_t profile_end(osk_view* v, hipStream_t st, bool record) {
+    if (!v->profile) return OSK_OK;
+    if (record) OSK_HIP(hipEventRecord(v->ev1, st));
+    v->ev_pending[(v->ev_next - 1) % osk_view::kEvRing] = true;
+    return OSK_OK;
+}
+
+// (start, stop) events for launch q0 of a call that launches [0, nq) in chunks of kMaxNQ
+inline hipEvent_t launch_ev_start(const osk_view* v, int q0) { return v->profile && q0 == 0 ? v->ev0 : nullptr; }
+inline hipEvent_t launch_ev_stop(const osk_view* v, int q0, int nq) {
+    return v->profile && q0 + kMaxNQ >= nq ? v->ev1 : nullptr;
 }
 
 // Streaming exact scan of queries already in the padded unit layout (≤ 8 per launch) + per-shard merge.
@@ -623,9 +687,9 @@ int32_t stream_search(osk_view* v, const void* qpad, const void* qnorm, int nq, 
         p.q = static_cast<const char*>(qpad) + (size_t)q0 * UP * 16;
         p.qnorm_f = static_cast<const float*>(qnorm) + q0;
         p.qnorm_i = static_cast<const int32_t*>(qnorm) + q0;
-        OSK_HIP(launch_scan(v->enc, v->cfg, qc, p, st));
+        OSK_HIP(launch_scan(v->enc, v->cfg, qc, p, st, launch_ev_start(v, q0), launch_ev_stop(v, q0, nq)));
     }
-    int32_t rc = profile_end(v, st);
+    int32_t rc = profile_end(v, st, false);
     if (rc) return rc;
     OSK_HIP(launch_merge_shards(v->ws_cand.as<uint64_t>(), v->n_tiles,
                                 v->d_shard_tile_begin.as<int32_t>(), v->n_shards, nq, k,
@@ -775,7 +839,7 @@ int32_t batched_search(osk_view* v, int nq, int k, int UP, const uint64_t* const
         mp.thr_counts = v->ws_pcounts.as<int32_t>();
     }
     OSK_HIP(launch_mfma_cand(mp, n_qb, false, st));
-    rc = profile_end(v, st);
+    rc = profile_end(v, st, true);
     if (rc) return rc;
     OSK_HIP(launch_merge_shards(v->ws_cand_a.as<uint64_t>(), v->n_munits * 2, v->d_shard_unit_begin.as<int32_t>(),
                                 S, nq, kKC, v->ws_akeys.as<uint64_t>(), v->ws_acounts.as<int32_t>(), st));
@@ -957,9 +1021,9 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
         p.q8 = v->ws_q8.as<int4>() + (size_t)q0 * u8;
         p.qc = v->ws_qc.as<float4>() + q0;
         p.qn_dev = v->ws_qnorm.as<float>() + q0;
-        OSK_HIP(launch_sq8_scan(p.q_count, p, st));
+        OSK_HIP(launch_sq8_scan(p.q_count, p, st, launch_ev_start(v, q0), launch_ev_stop(v, q0, nq)));
     }
-    rc = profile_end(v, st);
+    rc = profile_end(v, st, false);
     if (rc) return rc;
     OSK_HIP(v->ws_part.reserve(sizeof(uint64_t) * (size_t)nq * v->n_slices * k));
     SettleParams sp{};
@@ -1032,7 +1096,7 @@ int32_t view_search_device(osk_view* v, const void* d_queries, int nq, int k,
 
     int32_t rc;
     if (prefilter && (rc = ensure_sq8(v, st)) != OSK_OK) return rc;   // one-time build, outside the timing
-    if (v->profile && (rc = profile_begin(v, st)) != OSK_OK) return rc;
+    if (v->profile && (rc = profile_begin(v, st, batched)) != OSK_OK) return rc;
     if (prefilter) {
         rc = sq8_search(v, d_queries, nq, k, UP, d_accept, d_shard_keys, d_shard_counts, d_visited, st);
     } else if (batched) {
@@ -1124,14 +1188,17 @@ int32_t osk_view_profile(osk_view* v, int32_t enable) {
     int32_t rc = check_device(v->device);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(v->mu);
-    if (enable && !v->ev0) {
-        OSK_HIP(hipEventCreate(&v->ev0));
-        OSK_HIP(hipEventCreate(&v->ev1));
+    if (enable && !v->ev_start[0]) {
+        for (int i = 0; i < osk_view::kEvRing; ++i) {
+            OSK_HIP(hipEventCreate(&v->ev_start[i]));
+            OSK_HIP(hipEventCreate(&v->ev_stop[i]));
+        }
     }
+    for (int i = 0; i < osk_view::kEvRing; ++i) v->ev_pending[i] = false;
     v->profile = enable != 0;
     v->scan_ms = 0.0;
     v->scan_calls = 0;
-    v->pending = false;
+    v->ev_next = 0;
     return OSK_OK;
     OSK_GUARD_END
 }
@@ -1196,13 +1263,9 @@ int32_t osk_view_scan_time(osk_view* v, double* total_ms, int64_t* calls) {
     int32_t rc = check_device(v->device);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(v->mu);
-    if (v->pending) {
-        float ms = 0.f;
-        OSK_HIP(hipEventSynchronize(v->ev1));
-        OSK_HIP(hipEventElapsedTime(&ms, v->ev0, v->ev1));
-        v->scan_ms += ms;
-        v->scan_calls += 1;
-        v->pending = false;
+    for (int i = 0; i < osk_view::kEvRing; ++i) {
+        rc = profile_fold(v, i);
+        if (rc) return rc;
     }
     *total_ms = v->scan_ms;
     *calls = v->scan_calls;

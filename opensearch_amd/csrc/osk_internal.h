@@ -172,7 +172,10 @@ struct SettleParams {
 
 hipError_t launch_sq8_quantize(const float4* x, int64_t n, int units, int pitch, int units8, void* out8,
                                float4* aux, int mode, hipStream_t s);
-hipError_t launch_sq8_scan(int nq, const Sq8Params& p, hipStream_t s);
+// ev_start / ev_stop (optional): stamped by the kernel's own dispatch packet (hipExtLaunchKernelGGL),
+// so timing a launch adds no marker packets (and no gaps) to the stream
+hipError_t launch_sq8_scan(int nq, const Sq8Params& p, hipStream_t s, hipEvent_t ev_start = nullptr,
+                           hipEvent_t ev_stop = nullptr);
 int sq8_lanes(int units8);         // lanes per row of the int8 scan
 hipError_t launch_sq8_prep(int cfg, const float* src, int dim, int nq, int nq_pad, int UP, int units8, float4* qpad,
                            float* qnorm, void* q8, float4* qc, int* flags, hipStream_t s);
@@ -183,9 +186,12 @@ int cfg_index(int units);
 // Process-wide tuning knobs (osk_tune_set; benchmarks and A/B runs only).
 struct Tuning {
     int scan_nt = 1;          // non-temporal corpus loads in scan_f32 (+4% HBM rate, profiles/r01_scan_ab.txt)
-    int tiles_target = 4096;  // workgroup tiles per view (scan grid size)
-    int tile_min_rows = 1024; // ...but at least this many rows per tile (1.25M rows: 1221 tiles, +10% QPS
-                              // over 4096 tiles of 305 rows — profiles/r01e/tiles_ab.txt)
+    int tiles_target = 0;     // workgroup tiles per view (scan grid size); 0 = whole rounds of the chip's
+                              // resident slots (osk_view_create)
+    int tile_slots_per_cu = 4;    // resident scan workgroups per CU (4 waves/SIMD, 256-thread groups)
+    int tile_max_rounds = 4;      // at most this many rounds (10M rows: 4096 tiles, profiles/r01e)
+    int tile_min_rows = 1024; // ...and at least this many rows per tile (1.25M rows: 1024 tiles of 1221
+                              // rows, 4360 QPS vs 3968 for 4096 tiles of 305 rows — profiles/r01e/tiles_ab.txt)
     int mfma_min_batch = 16;  // batches ≥ this use the MFMA candidate path (0 = never)
     int mfma_units = 512;     // workgroup units of the MFMA candidate pass per view
     int sq8 = 1;              // certified int8 prefilter for float32 batches below mfma_min_batch
@@ -197,7 +203,8 @@ struct Tuning {
 };
 extern Tuning g_tuning;
 
-hipError_t launch_scan(int enc, int cfg, int nq, const ScanParams& p, hipStream_t s);
+hipError_t launch_scan(int enc, int cfg, int nq, const ScanParams& p, hipStream_t s, hipEvent_t ev_start = nullptr,
+                       hipEvent_t ev_stop = nullptr);
 hipError_t launch_row_norms_f32(const float4* rows, int64_t n_rows, int units, int cfg,
                                 float* out, hipStream_t s);
 hipError_t launch_row_norms_i8(const int4* rows, int64_t n_rows, int units, int32_t* out,

@@ -17,6 +17,8 @@
 //   * Scores never round-trip through HBM: every wavefront keeps a sorted top-k list in lanes
 //     0..k-1 of a register and a wave-uniform threshold; a row-group only costs a ballot unless a
 //     score beats the threshold (rare after the first few hundred rows).
+#include <hip/hip_ext.h>
+
 #include "osk_internal.h"
 #include "osk_wave.h"
 
@@ -309,7 +311,8 @@ static int nq_of_slot(int s) { return 1 << s; }
 
 Tuning g_tuning;
 
-hipError_t launch_scan(int enc, int cfg, int nq, const ScanParams& p, hipStream_t s) {
+hipError_t launch_scan(int enc, int cfg, int nq, const ScanParams& p, hipStream_t s, hipEvent_t ev_start,
+                       hipEvent_t ev_stop) {
     const int slot = nq_slot(nq);
     const int NQ = nq_of_slot(slot);
     const int V = kCfgLV[cfg][1], L = kCfgLV[cfg][0];
@@ -322,7 +325,10 @@ hipError_t launch_scan(int enc, int cfg, int nq, const ScanParams& p, hipStream_
     } else {
         fn = kScanI8[cfg][slot];
     }
-    hipLaunchKernelGGL(fn, dim3(p.n_tiles), dim3(kBlock), lds, s, p);
+    if (ev_start || ev_stop)
+        hipExtLaunchKernelGGL(fn, dim3(p.n_tiles), dim3(kBlock), lds, s, ev_start, ev_stop, 0, p);
+    else
+        hipLaunchKernelGGL(fn, dim3(p.n_tiles), dim3(kBlock), lds, s, p);
     return hipGetLastError();
 }
 
@@ -569,38 +575,37 @@ __global__ __launch_bounds__(kBlock) void merge_coord(const uint64_t* __restrict
     __shared__ __attribute__((aligned(16))) uint32_t s_su[kCoordMax];
     __shared__ __attribute__((aligned(16))) int32_t s_sidx[kCoordMax];
     __shared__ __attribute__((aligned(16))) int32_t s_doc[kCoordMax];
-    __shared__ int s_n;
-    __shared__ unsigned long long s_total;
-    __shared__ uint32_t s_max;
+    // per-wave partial sums / maxima (no LDS atomics: a 64-bit LDS atomic add made this one-query
+    // kernel 10 µs instead of 3.7 µs — tools/mc_micro.hip)
+    __shared__ int s_red_n[kBlock / 64], s_red_total[kBlock / 64];
+    __shared__ uint32_t s_red_max[kBlock / 64];
     const int b = blockIdx.x, tid = threadIdx.x, nq = gridDim.x;
     const int n_shards = n_ranks * sl;
     const int topn = min(k, from + size);
     const int n_slots = n_shards * topn;
     const int n4 = (n_slots + 3) & ~3;   // ≤ kCoordMax (the host checks n_slots ≤ 4096)
-    if (tid == 0) { s_n = 0; s_total = 0ull; s_max = 0u; }
-    __syncthreads();
     auto list = [&](int s) -> size_t {
         const int r = s / sl, j = s - r * sl;
         return ((size_t)(r * nq + b) * sl + j);
     };
     // stats (TopDocsStats): Σ hits over the shards, max of their top scores
+    int part_total = 0;
+    uint32_t part_max = 0u;
     if (shard_counts) {
         for (int s = tid; s < n_shards; s += kBlock) {
             const size_t o = list(s);
             const int c = shard_counts[o];
             const uint64_t top = shard_keys[o * k];
-            atomicAdd(&s_total, (unsigned long long)c);
-            if (c > 0) atomicMax(&s_max, (uint32_t)(top >> 32));
+            part_total += c;
+            if (c > 0) part_max = max(part_max, (uint32_t)(top >> 32));
         }
     } else if (topn < k) {   // (topn == k: the slot loop below sees every list entry)
-        int hits = 0;
         for (int e = tid; e < n_shards * k; e += kBlock) {
             const int s = e / k, i = e - s * k;
             const uint64_t key = shard_keys[list(s) * k + i];
-            hits += key != 0ull;
-            if (i == 0 && key) atomicMax(&s_max, (uint32_t)(key >> 32));
+            part_total += key != 0ull;
+            if (i == 0 && key) part_max = max(part_max, (uint32_t)(key >> 32));
         }
-        if (hits) atomicAdd(&s_total, (unsigned long long)hits);
     }
     // one round of independent loads per slot (i < topn ≤ k keeps the key load in bounds)
     int mine = 0;
@@ -616,29 +621,38 @@ __global__ __launch_bounds__(kBlock) void merge_coord(const uint64_t* __restrict
         s_doc[slot] = hit ? key_doc(key) : INT32_MAX;
         s_sidx[slot] = hit ? si : INT32_MAX;
         mine += hit;
-        if (!shard_counts && topn == k && hit && i == 0) atomicMax(&s_max, (uint32_t)(key >> 32));
+        if (!shard_counts && topn == k && hit && i == 0) part_max = max(part_max, (uint32_t)(key >> 32));
     }
-    if (mine) {
-        atomicAdd(&s_n, mine);
-        if (!shard_counts && topn == k) atomicAdd(&s_total, (unsigned long long)mine);
+    if (!shard_counts && topn == k) part_total = mine;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mine += __shfl_xor(mine, o);
+        part_total += __shfl_xor(part_total, o);
+        part_max = max(part_max, (uint32_t)__shfl_xor((int)part_max, o));
+    }
+    if ((tid & 63) == 0) {
+        s_red_n[tid >> 6] = mine;
+        s_red_total[tid >> 6] = part_total;
+        s_red_max[tid >> 6] = part_max;
     }
     __syncthreads();
-    // rank of each hit = number of hits ordered before it; the slots are read 4 at a time with
-    // independent 16-byte LDS loads (a scalar loop with a branch per slot is latency-bound)
+    // rank of each hit = number of hits ordered before it.  The slots' 32-bit score keys are read 4
+    // at a time (16-byte LDS loads); only a score that occurs more than once (a tie) takes the
+    // (shardIndex asc, doc asc) pass.
     for (int i = tid; i < n_slots; i += kBlock) {
         const uint32_t su = s_su[i];
         if (su == 0u && s_sidx[i] == INT32_MAX) continue;   // empty
         const int32_t si = s_sidx[i], d = s_doc[i];
-        int rank = 0;
+        int rank = 0, eq = 0;
 #pragma unroll 4
         for (int j = 0; j < n4; j += 4) {
             const uint4 u4 = *reinterpret_cast<const uint4*>(s_su + j);
-            const int4 s4 = *reinterpret_cast<const int4*>(s_sidx + j);
-            const int4 d4 = *reinterpret_cast<const int4*>(s_doc + j);
-            rank += (u4.x > su) || (u4.x == su && (s4.x < si || (s4.x == si && d4.x < d)));
-            rank += (u4.y > su) || (u4.y == su && (s4.y < si || (s4.y == si && d4.y < d)));
-            rank += (u4.z > su) || (u4.z == su && (s4.z < si || (s4.z == si && d4.z < d)));
-            rank += (u4.w > su) || (u4.w == su && (s4.w < si || (s4.w == si && d4.w < d)));
+            rank += (u4.x > su) + (u4.y > su) + (u4.z > su) + (u4.w > su);
+            eq += (u4.x == su) + (u4.y == su) + (u4.z == su) + (u4.w == su);
+        }
+        if (eq > 1) {
+            for (int j = 0; j < n_slots; ++j)
+                rank += s_su[j] == su && (s_sidx[j] < si || (s_sidx[j] == si && s_doc[j] < d));
         }
         if (rank >= from && rank < from + size) {
             const size_t o = (size_t)b * size + (rank - from);
@@ -647,7 +661,14 @@ __global__ __launch_bounds__(kBlock) void merge_coord(const uint64_t* __restrict
             shard_out[o] = si;
         }
     }
-    const int n = s_n;
+    int n = 0, total = 0;
+    uint32_t mx = 0u;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+        n += s_red_n[w];
+        total += s_red_total[w];
+        mx = max(mx, s_red_max[w]);
+    }
     const int got = max(0, min(size, n - from));
     for (int r = got + tid; r < size; r += kBlock) {
         const size_t o = (size_t)b * size + r;
@@ -657,8 +678,8 @@ __global__ __launch_bounds__(kBlock) void merge_coord(const uint64_t* __restrict
     }
     if (tid == 0) {
         count[b] = got;
-        total_hits[b] = (int64_t)s_total;
-        max_score[b] = s_total > 0 ? sortable_to_float(s_max) : __builtin_nanf("");
+        total_hits[b] = (int64_t)total;
+        max_score[b] = total > 0 ? sortable_to_float(mx) : __builtin_nanf("");
     }
 }
 

@@ -22,6 +22,8 @@
 // re-scanned tile) and scores ≥ L: the shard's k-th exact score T ≥ L.  A row that is neither
 // re-scored nor in an exact tile has score ≤ ub < L ≤ T, so it cannot enter the top k; strictness
 // (ub < L) makes doc-order ties irrelevant.
+#include <hip/hip_ext.h>
+
 #include "osk_internal.h"
 #include "osk_wave.h"
 
@@ -584,11 +586,15 @@ using Sq8Fn = void (*)(Sq8Params);
 static const Sq8Fn kSq8[8][4] = {OSK_SQ8_ROW(4, 1),  OSK_SQ8_ROW(8, 1),  OSK_SQ8_ROW(16, 1), OSK_SQ8_ROW(16, 2),
                                  OSK_SQ8_ROW(16, 3), OSK_SQ8_ROW(16, 4), OSK_SQ8_ROW(32, 4), OSK_SQ8_ROW(64, 4)};
 
-hipError_t launch_sq8_scan(int nq, const Sq8Params& p, hipStream_t s) {
+hipError_t launch_sq8_scan(int nq, const Sq8Params& p, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
     const int slot = nq <= 1 ? 0 : nq <= 2 ? 1 : nq <= 4 ? 2 : 3;
     // NQ > 1: the queries and the 4 waves' per-query lists in LDS
     const size_t lds = slot == 0 ? 0 : (size_t)(1 << slot) * (p.units8 * 16 + 4 * kKQ * 12);
-    hipLaunchKernelGGL(kSq8[sq8_cfg(p.units8)][slot], dim3(p.n_tiles), dim3(kBlock), lds, s, p);
+    const auto fn = kSq8[sq8_cfg(p.units8)][slot];
+    if (ev_start || ev_stop)
+        hipExtLaunchKernelGGL(fn, dim3(p.n_tiles), dim3(kBlock), lds, s, ev_start, ev_stop, 0, p);
+    else
+        hipLaunchKernelGGL(fn, dim3(p.n_tiles), dim3(kBlock), lds, s, p);
     return hipGetLastError();
 }
 
@@ -816,12 +822,39 @@ __global__ __launch_bounds__(kSettleThreads) void sq8_settle_merge(SettleParams 
     const uint64_t* __restrict__ src = p.part + ((size_t)q * p.n_slices + g0) * k;
     const int nl = g1 - g0, n = nl * k;
     if (tid == 0) { s_ns = 0; s_t = 0ull; }
-    if (tid < 64) { s_top[tid] = 0ull; s_b[tid] = 0ull; }
-    __syncthreads();
-    // bucket maxima of the lists' first keys (list l → bucket l mod 64)
-    for (int l = tid; l < nl; l += kSettleThreads) {
-        const uint64_t f = src[(size_t)l * k];
-        if (f) atomicMax(reinterpret_cast<unsigned long long*>(&s_b[l & 63]), (unsigned long long)f);
+    if (tid < 64) s_top[tid] = 0ull;
+    if (n <= kSettleThreads) {
+        // few keys (a shard of ≤ 25 slice lists at k = 10): rank them all directly, one per thread.
+        // Keys are distinct (they carry the doc) or 0 = empty.
+        const uint64_t key = tid < n ? src[tid] : 0ull;
+        s_surv[tid] = key;
+        __syncthreads();
+        if (key) {
+            int rank = 0;
+            const int n2 = (n + 1) & ~1;   // s_surv[n] is a 0 key when n is odd
+#pragma unroll 4
+            for (int j = 0; j < n2; j += 2) {
+                const ulonglong2 v2 = *reinterpret_cast<const ulonglong2*>(s_surv + j);
+                rank += (v2.x > key) + (v2.y > key);
+            }
+            if (rank < k) s_top[rank] = key;
+        }
+        __syncthreads();
+        if (wave == 0) {
+            const uint64_t kk = lane < k ? s_top[lane] : 0ull;
+            const size_t o = (size_t)q * S + sh;
+            if (lane < k) p.shard_keys[o * k + lane] = kk;
+            const int cnt = __popcll(__ballot(kk != 0ull));
+            if (lane == 0) p.shard_counts[o] = cnt;
+        }
+        return;
+    }
+    // bucket maxima of the lists' first keys (list l → bucket l mod 64), one bucket per lane of wave 0
+    // (no 64-bit LDS atomics: tools/mc_micro.hip measured them at several µs per block)
+    if (tid < 64) {
+        uint64_t m = 0ull;
+        for (int l = tid; l < nl; l += 64) m = max(m, src[(size_t)l * k]);
+        s_b[tid] = m;
     }
     __syncthreads();
     if (tid < 64) {
