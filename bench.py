@@ -15,9 +15,13 @@ the whole hot path with inputs resident in HBM: per-shard exact scan + top-k on 
 merge, RCCL all-gather of the per-shard top-k lists, device coordinator merge (TopDocs.merge).
 value = queries answered by the whole job per second.
 
-roofline: the scan kernel (scan_f32<16,12,…>) is HBM-bound; algorithmic bytes per launch =
-rows scanned × 768 × 4 B (each corpus byte read once per launch of ≤ 8 queries).  Its average
-duration is measured live with HIP events on the launch stream (osk_view_profile).
+Path: batches below 16 take the certified int8 prefilter (sq8_scan over an int8 copy of the rows,
+exact fp32 re-score of the rows the bound cannot exclude; results bit-identical to the fp32 scan,
+which the bench re-runs on the same queries and compares); batches ≥ 16 the batched MFMA path.
+roofline: the dominant kernel is HBM-bound; algorithmic bytes per launch = rows scanned × (768 + 16) B
+for sq8_scan (int8 row + 16-B bound terms; rows × 768 × 4 B for the fp32 scan), each read once per
+launch of ≤ 8 queries.  Its average duration is measured live inside the timed region from the
+kernel's own dispatch-packet timestamps (hipExtLaunchKernelGGL events, osk_view_profile).
 cpu_baseline: rank 0 at N = 1 only — the oracle's Lucene-equivalent restatement (Panama-512 order,
 not Lucene: no JDK/jar on the box) on a bounded sample, scaled to the full corpus by rows.
 """
@@ -100,6 +104,10 @@ def main():
     ap.add_argument("--rows-per-shard", type=int, default=ROWS_PER_SHARD)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sq8", action="store_true", help="measure the fp32 streaming scan as the main path")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL over xGMI, one GPU per rank); gloo only to rehearse N > 1 ranks on one GPU")
+    ap.add_argument("--dump", default="", help="rank 0 writes the merged results of batches 0..7 to this .npz "
+                    "(cross-N parity: the N-rank result must equal the 1-GPU result)")
     ap.add_argument("--tiles", type=int, default=0, help="A/B: workgroup tiles per view (osk_tune tiles_target)")
     # ≈10 s of CPU work on 16 host threads (≈1e8 row·queries/s measured): a bounded sample of C3
     ap.add_argument("--cpu-sample-rows", type=int, default=524_288)
@@ -111,9 +119,14 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    if a.dist_backend == "gloo":   # rehearsal: several ranks may share the box's one GPU
+        local_rank %= torch.cuda.device_count()
     torch.cuda.set_device(local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(a.dist_backend)
 
     if a.tiles:
         _lib.tune("tiles_target", a.tiles)
@@ -241,6 +254,13 @@ def main():
             "identical_to_prefilter_on_8_batches": mism == 0,
         }
         assert mism == 0, f"prefilter and fp32 scan results differ in {mism} tensors"
+
+    if a.dump:
+        outs = [[t.cpu().numpy().copy() for t in step(i)] for i in range(min(8, n_pool))]
+        if rank == 0:
+            np.savez(a.dump, scores=np.stack([o[0] for o in outs]), docs=np.stack([o[1] for o in outs]),
+                     shard=np.stack([o[2] for o in outs]), count=np.stack([o[3] for o in outs]),
+                     total=np.stack([o[4] for o in outs]), max_score=np.stack([o[5] for o in outs]))
 
     traffic, traffic_src = pmc_traffic(rows_local, B, prefilter)
     if rank == 0:
