@@ -108,6 +108,10 @@ def main():
                     help="nccl (= RCCL over xGMI, one GPU per rank); gloo only to rehearse N > 1 ranks on one GPU")
     ap.add_argument("--dump", default="", help="rank 0 writes the merged results of batches 0..7 to this .npz "
                     "(cross-N parity: the N-rank result must equal the 1-GPU result)")
+    ap.add_argument("--mfma-min-batch", type=int, default=0,
+                    help="A/B: batches ≥ this take the bf16×3 MFMA path (osk_tune mfma_min_batch; 0 = library default)")
+    ap.add_argument("--sq8-mfma-min", type=int, default=-1,
+                    help="A/B: prefilter batches ≥ this scan on int8 MFMA (osk_tune sq8_mfma_min; -1 = library default)")
     ap.add_argument("--tiles", type=int, default=0, help="A/B: workgroup tiles per view (osk_tune tiles_target)")
     # ≈10 s of CPU work on 16 host threads (≈1e8 row·queries/s measured): a bounded sample of C3
     ap.add_argument("--cpu-sample-rows", type=int, default=524_288)
@@ -130,6 +134,10 @@ def main():
 
     if a.tiles:
         _lib.tune("tiles_target", a.tiles)
+    mfma_min_batch = a.mfma_min_batch or 96   # the library default (osk_internal.h)
+    _lib.tune("mfma_min_batch", mfma_min_batch)
+    sq8_mfma_min = 2 if a.sq8_mfma_min < 0 else a.sq8_mfma_min
+    _lib.tune("sq8_mfma_min", sq8_mfma_min)
     t0 = time.perf_counter()
     shards = D.LocalShards(rank, world, N_SHARDS, a.rows_per_shard, DIM, _lib.COSINE, _lib.FLOAT32, 42,
                            _lib.DIST_NORMALISH_UNIT, local_rank)
@@ -192,8 +200,9 @@ def main():
         _lib.check(_lib.lib().osk_view_counter(shards.view, name.encode(), C.byref(v)))
         return v.value
 
-    prefilter = B < 16 and K <= 12 and not a.no_sq8
-    batched = B >= 16 and K <= 12           # the library's batched MFMA path (osk_tune "mfma_min_batch")
+    batched = B >= mfma_min_batch and K <= 12   # the library's batched bf16×3 MFMA path
+    prefilter = not batched and K <= 12 and not a.no_sq8
+    sq8_mfma = prefilter and sq8_mfma_min > 0 and B >= sq8_mfma_min
     _lib.tune("sq8", 0 if a.no_sq8 else 1)
     fb0, rs0, calls0 = counter("sq8_fallback_queries"), counter("sq8_rescored_rows"), counter("sq8_calls")
     elapsed_max, scan_avg_ms, ev_ms, out = timed(a.steps, a.warmup)
@@ -202,7 +211,12 @@ def main():
     assert np.all(cnt == SIZE), cnt
 
     u8 = (DIM + 15) // 16
-    if prefilter:
+    if sq8_mfma:
+        passes = (B + 15) // 16
+        bytes_per_launch = rows_local * (u8 * 16 + 16) * passes
+        kernel_name = ("sq8_mfma<KS=12> certified int8 prefilter on v_mfma_i32_16x16x64_i8 (bytes = int8 rows + "
+                       "16-B bound terms per row, once per launch of ≤ 16 queries)")
+    elif prefilter:
         passes = (B + 7) // 8
         bytes_per_launch = rows_local * (u8 * 16 + 16) * passes
         kernel_name = (f"sq8_scan<L=16,V=3,NQ={min(8, 1 << max(0, (B - 1).bit_length()))}> certified int8 prefilter "
@@ -245,7 +259,7 @@ def main():
                         log(f"mismatch batch {i} output {j}: prefilter {x.flatten()[:10].tolist()} "
                             f"fp32 {y.flatten()[:10].tolist()}")
         _lib.tune("sq8", 1)
-        s_bytes = rows_local * DIM * 4 * passes
+        s_bytes = rows_local * DIM * 4 * ((B + 7) // 8)
         extra["fp32_stream"] = {
             "value": min(a.steps, 50) * B / s_el, "scan_ms_avg": s_scan,
             "roofline_achieved_GBps": s_bytes / (s_scan * 1e-3) / 1e9,

@@ -230,6 +230,7 @@ struct osk_view {
     // empty slice so that its result is still written)
     int n_slices = 0;
     DevBuf d_slices, d_shard_slice_begin, ws_part;
+    DevBuf ws_pilot, ws_thr, ws_thr_counts;   // int8 MFMA prefilter: pilot keys, per-(query, shard) floors
     int64_t sq8_calls = 0;
     std::mutex mu;
     // scan-kernel timing (osk_view_profile): a ring of (start, stop) event pairs, one per search call,
@@ -367,6 +368,9 @@ int32_t osk_tune_set(const char* key, int64_t value) {
     } else if (k == "tiles_target") {
         OSK_REQUIRE(value >= 0 && value <= (1 << 22), "tiles_target out of range");
         g_tuning.tiles_target = (int)value;
+    } else if (k == "sq8_mfma_min") {
+        OSK_REQUIRE(value >= 0 && value <= (1 << 20), "sq8_mfma_min out of range");
+        g_tuning.sq8_mfma_min = (int)value;
     } else if (k == "tile_slots_per_cu") {
         OSK_REQUIRE(value >= 1 && value <= 64, "tile_slots_per_cu out of range");
         g_tuning.tile_slots_per_cu = (int)value;
@@ -1015,13 +1019,40 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     p.gam = v->sq8_gam;
     p.g2 = v->sq8_g2;
     p.cos_slack = v->sq8_cos_slack;
-    for (int q0 = 0; q0 < nq; q0 += kMaxNQ) {
+    // batches of ≥ sq8_mfma_min queries: the int8 MFMA scan, 16 queries per launch; else the VALU
+    // scan, ≤ 8 per launch
+    const bool use_mfma = g_tuning.sq8_mfma_min > 0 && nq >= g_tuning.sq8_mfma_min && sq8_mfma_supported(u8);
+    const int chunk = use_mfma ? kMfmaQueries : kMaxNQ;
+    if (use_mfma) {
+        OSK_HIP(v->ws_pilot.reserve(sizeof(uint64_t) * (size_t)kMfmaQueries * v->n_tiles * 64));
+        OSK_HIP(v->ws_thr.reserve(sizeof(uint64_t) * (size_t)kMfmaQueries * S * 64));
+        OSK_HIP(v->ws_thr_counts.reserve(sizeof(int32_t) * (size_t)kMfmaQueries * S));
+    }
+    for (int q0 = 0; q0 < nq; q0 += chunk) {
         p.q0 = q0;
-        p.q_count = std::min(kMaxNQ, nq - q0);
+        p.q_count = std::min(chunk, nq - q0);
         p.q8 = v->ws_q8.as<int4>() + (size_t)q0 * u8;
         p.qc = v->ws_qc.as<float4>() + q0;
         p.qn_dev = v->ws_qnorm.as<float>() + q0;
-        OSK_HIP(launch_sq8_scan(p.q_count, p, st, launch_ev_start(v, q0), launch_ev_stop(v, q0, nq)));
+        hipEvent_t e0 = v->profile && q0 == 0 ? v->ev0 : nullptr;
+        hipEvent_t e1 = v->profile && q0 + chunk >= nq ? v->ev1 : nullptr;
+        if (use_mfma) {
+            // pilot: 16 sampled rows per wave → per (query, shard) the top 64 sampled lower bounds;
+            // the k-th of them floors the main pass's quick thresholds (sq8_mfma comment)
+            p.k = k;
+            p.n_shards = S;
+            p.pilot = 1;
+            p.pilot_keys = v->ws_pilot.as<uint64_t>();
+            OSK_HIP(launch_sq8_mfma(p, st, e0, nullptr));
+            OSK_HIP(launch_merge_shards(v->ws_pilot.as<uint64_t>(), v->n_tiles, v->d_shard_tile_begin.as<int32_t>(),
+                                        S, p.q_count, 64, v->ws_thr.as<uint64_t>(), v->ws_thr_counts.as<int32_t>(), st));
+            p.pilot = 0;
+            p.thr_keys = v->ws_thr.as<uint64_t>();
+            p.thr_counts = v->ws_thr_counts.as<int32_t>();
+            OSK_HIP(launch_sq8_mfma(p, st, nullptr, e1));
+        } else {
+            OSK_HIP(launch_sq8_scan(p.q_count, p, st, e0, e1));
+        }
     }
     rc = profile_end(v, st, false);
     if (rc) return rc;
@@ -1045,7 +1076,7 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     sp.flags = v->ws_flags.as<int>();
     sp.counters = v->d_counters.as<unsigned long long>();
     sp.n_lists = 4 * v->n_tiles;
-    sp.scan_R = 64 / sq8_lanes(u8);
+    sp.scan_R = use_mfma ? kMfmaScanR : 64 / sq8_lanes(u8);
     sp.n_shards = S;
     sp.n_segs = (int)v->segs.size();
     sp.units = v->units;

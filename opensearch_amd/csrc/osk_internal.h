@@ -138,6 +138,17 @@ struct Sq8Params {
     float gam;                       // fp32 dot rounding: |dot_dev − x·b| ≤ gam·(|x|² + |b|²)
     float g2;                        // fp32 d² rounding:  |d²_dev − d²| ≤ g2·d²
     float cos_slack;                 // COSINE quick test: norm-order slack
+    // sq8_mfma only.  pilot = 1: each wave scores just its first 16 (accepted) rows and writes their
+    // lower-bound keys to pilot_keys [q_count][n_tiles][64] (slot wave·16 + row); merged per (query,
+    // shard) into thr_keys [q_count][n_shards][64] / thr_counts.  pilot = 0: the k-th best sampled
+    // lower bound T of the (query, shard) is a floor under every wave list's quick threshold: a row
+    // with ub < T ≤ the shard's k-th best lower bound scores below the shard's k-th exact score.
+    int pilot;
+    int k;
+    int n_shards;
+    uint64_t* pilot_keys;
+    const uint64_t* thr_keys;
+    const int32_t* thr_counts;
 };
 
 struct SettleParams {
@@ -177,6 +188,12 @@ hipError_t launch_sq8_quantize(const float4* x, int64_t n, int units, int pitch,
 hipError_t launch_sq8_scan(int nq, const Sq8Params& p, hipStream_t s, hipEvent_t ev_start = nullptr,
                            hipEvent_t ev_stop = nullptr);
 int sq8_lanes(int units8);         // lanes per row of the int8 scan
+// int8 MFMA prefilter scan: ≤ kMfmaQueries queries per launch, rows ≤ 1024 int8 dims (sq8_mfma_supported)
+constexpr int kMfmaQueries = 16;
+constexpr int kMfmaScanR = 16;      // its rows per wave-iteration (the settle's scan_R)
+int sq8_mfma_supported(int units8);
+hipError_t launch_sq8_mfma(const Sq8Params& p, hipStream_t s, hipEvent_t ev_start = nullptr,
+                           hipEvent_t ev_stop = nullptr);
 hipError_t launch_sq8_prep(int cfg, const float* src, int dim, int nq, int nq_pad, int UP, int units8, float4* qpad,
                            float* qnorm, void* q8, float4* qc, int* flags, hipStream_t s);
 hipError_t launch_sq8_settle(int cfg, int nq, const SettleParams& p, hipStream_t s);
@@ -192,9 +209,11 @@ struct Tuning {
     int tile_max_rounds = 4;      // at most this many rounds (10M rows: 4096 tiles, profiles/r01e)
     int tile_min_rows = 1024; // ...and at least this many rows per tile (1.25M rows: 1024 tiles of 1221
                               // rows, 4360 QPS vs 3968 for 4096 tiles of 305 rows — profiles/r01e/tiles_ab.txt)
-    int mfma_min_batch = 16;  // batches ≥ this use the MFMA candidate path (0 = never)
+    int mfma_min_batch = 96;  // batches ≥ this use the bf16×3 MFMA candidate path (0 = never); below it the
+                              // int8 prefilter (sq8_mfma: 8.1k QPS at C3 b16–b64 vs ~5k for bf16×3 at b64)
     int mfma_units = 512;     // workgroup units of the MFMA candidate pass per view
     int sq8 = 1;              // certified int8 prefilter for float32 batches below mfma_min_batch
+    int sq8_mfma_min = 2;     // prefilter batches ≥ this scan on int8 MFMA, 16 queries per launch (0 = never)
     int sq8_force_fallback = 0;   // tests: every list of a prefiltered search is re-scanned exactly
     int settle_trace = 0;     // A/B only: record settle phase timestamps (debug copy "settle_trace")
     int mfma_ablate = 0;      // A/B only: 1 skip the epilogue, 2 skip query staging, 4 skip corpus staging,

@@ -599,6 +599,243 @@ hipError_t launch_sq8_scan(int nq, const Sq8Params& p, hipStream_t s, hipEvent_t
 }
 
 // ------------------------------------------------------------------------------------------------
+// prefilter scan on int8 MFMA: up to 16 queries per launch (batches of 2 and more).  The VALU scan's
+// per-(row, query) int32 dot is v_dot4 + cross-lane reductions, so at 8 queries it is VALU-bound
+// (2.1 TB/s).  Here a wave takes 16 rows at a time and one v_mfma_i32_16x16x64_i8 per 64 dims gives
+// the 16 × 16 exact int32 dots: lane l loads 16 B of row (l & 15) per k-step (chunk l >> 4 of the
+// 64-B slab) and reads the same chunk of query (l & 15) from LDS; the product pairs row byte j with
+// query byte j of the same chunk, whatever the unit's internal k order (A and B share the layout).
+// Lane l then holds dots of rows 4(l >> 4) + i (i = 0..3) × query l & 15 and runs the same bound,
+// quick test and list insertion as sq8_scan (lists per (wave, query) in LDS).  Row split and list
+// numbering are sq8_scan's with R = 16 rows per wave-iteration (the settle re-scans with scan_R = 16).
+// Filter pushdown: accepted rows are compacted 64 at a time; any row can feed any MFMA row slot.
+// ------------------------------------------------------------------------------------------------
+constexpr int kMfmaNQ = 16;
+template <int KS>
+__global__ __launch_bounds__(kBlock, 4) void sq8_mfma(Sq8Params p) {
+    typedef int i32x4 __attribute__((ext_vector_type(4)));
+    constexpr int NQ = kMfmaNQ, R = 16, UQ = 4 * KS;   // UQ: 16-B units per query in LDS
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int col = lane & 15, grp = lane >> 4;
+    const TileDev tile = p.tiles[blockIdx.x];
+    const SegDev seg = p.segs[tile.seg];
+    const int4* __restrict__ X = p.rows8[tile.seg];
+    const float4* __restrict__ AX = p.aux[tile.seg];
+    const uint32_t vbase = (uint32_t)p.seg_vrow[tile.seg];
+    const int u8 = p.units8, sim = p.sim;
+    extern __shared__ __attribute__((aligned(16))) int4 sq[];   // [NQ][UQ] (zero past u8 / q_count)
+    uint64_t* s_lk = reinterpret_cast<uint64_t*>(sq + NQ * UQ);
+    uint32_t* s_lp = reinterpret_cast<uint32_t*>(s_lk + 4 * NQ * kKQ);
+    for (int i = tid; i < NQ * UQ; i += kBlock) {
+        const int b = i / UQ, f = i - b * UQ;
+        sq[i] = (b < p.q_count && f < u8) ? p.q8[b * u8 + f] : make_int4(0, 0, 0, 0);
+    }
+    for (int i = tid; i < 4 * NQ * kKQ; i += kBlock) {
+        s_lk[i] = 0ull;
+        s_lp[i] = 0u;
+    }
+    const bool qv = col < p.q_count;
+    const float4 qc = qv ? p.qc[col] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float qnd = (sim == SIM_COSINE && qv) ? p.qn_dev[col] : 0.0f;
+    const float sqn = sqrtf(qnd);
+    // the pilot's floor key T of (query col, this tile's shard): 0 = none (fewer than k sampled rows)
+    uint64_t tkey = 0ull;
+    if (!p.pilot && p.thr_keys && qv) {
+        const size_t o = (size_t)col * p.n_shards + tile.shard;
+        if (p.thr_counts[o] >= p.k) tkey = p.thr_keys[o * 64 + p.k - 1];
+        // a floor of score 0 (DOT_PRODUCT / COSINE clamp every negative similarity to 0) would drop
+        // rows that tie with it: sq8_quick's test is strict only above the clamp
+        if (!(key_score(tkey) > 0.0f)) tkey = 0ull;
+    }
+    float tq = sq8_quick(sim, tkey, sqn, p.cos_slack);
+    const bool pilot = p.pilot != 0;
+    bool sampled = false;   // pilot: this wave's first group is done
+
+    const int64_t rows = tile.row_end - tile.row_begin;
+    const int64_t per_wave = ((rows + 4 * R - 1) / (4 * R)) * R;
+    const int64_t wb = tile.row_begin + wave * per_wave;
+    const int64_t we = min(wb + per_wave, tile.row_end);
+    const uint64_t* abits = p.accept ? p.accept[tile.seg] : nullptr;
+    uint32_t nvis = 0;
+    __syncthreads();
+
+    auto process = [&](int64_t rowA, bool vA, const int64_t (&ro)[4], const bool (&vo)[4]) {
+        const int4* xr = X + (vA ? rowA : tile.row_begin) * u8;
+        i32x4 a[KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const int f = s * 4 + grp;
+            const int4 v = (vA && f < u8) ? load_i4_nt(xr + f) : make_int4(0, 0, 0, 0);
+            a[s] = i32x4{v.x, v.y, v.z, v.w};
+        }
+        float4 ax[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ax[i] = vo[i] ? AX[ro[i]] : make_float4(0.f, 0.f, 0.f, 0.f);
+        nvis += __popcll(__ballot(lane < 16 && vA));
+        i32x4 acc = {0, 0, 0, 0};
+        const int4* qrow = sq + col * UQ + grp;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const int4 bv = qrow[s * 4];
+            acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[s], i32x4{bv.x, bv.y, bv.z, bv.w}, acc, 0, 0, 0);
+        }
+        bool pass[4];
+        float lo[4], hi[4];
+        bool anyp = false;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float sx = sim == SIM_COSINE ? sqrtf(ax[i].w) : 0.0f;
+            sq8_bounds(sim, (float)acc[i], ax[i], qc, p.gam, p.g2, lo[i], hi[i]);
+            pass[i] = vo[i] && qv && sq8_pass(sim, lo[i], hi[i], tq, sx);
+            anyp |= pass[i];
+        }
+        if (pilot) {   // the sampled rows' lower-bound keys (distinct: they carry the view row)
+            if (qv) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    float xnd = 0.0f;
+                    if (sim == SIM_COSINE && vo[i]) xnd = seg.xnorm_f[ro[i]];
+                    const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi[i]) : score_f32(sim, lo[i], qnd, xnd);
+                    p.pilot_keys[((size_t)col * p.n_tiles + blockIdx.x) * 64 + wave * 16 + 4 * grp + i] =
+                        vo[i] ? make_key(lb, vbase + (uint32_t)ro[i]) : 0ull;
+                }
+            }
+            sampled = true;
+            return;
+        }
+        const uint64_t bl = __ballot(anyp);
+        if (bl) {   // wave-uniform: rare once the lists have filled
+            uint32_t qm = (uint32_t)((bl | (bl >> 16) | (bl >> 32) | (bl >> 48)) & 0xFFFFull);
+            while (qm) {
+                const int b = __builtin_ctz(qm);
+                qm &= qm - 1u;
+                const int o0 = (wave * NQ + b) * kKQ;
+                uint64_t lkb = lane < kKQ ? s_lk[o0 + lane] : 0ull;
+                uint32_t lpb = lane < kKQ ? s_lp[o0 + lane] : 0u;
+                uint64_t thrb = readlane64(lkb, kKQ - 1);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const bool o = pass[i] && col == b;
+                    float xnd = 0.0f;
+                    if (sim == SIM_COSINE && o) xnd = seg.xnorm_f[ro[i]];
+                    const float ub = sim == SIM_EUCLIDEAN ? score_f32_l2(lo[i]) : score_f32(sim, hi[i], qnd, xnd);
+                    const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi[i]) : score_f32(sim, lo[i], qnd, xnd);
+                    const uint64_t key = o ? make_key(ub, vbase + (uint32_t)ro[i]) : 0ull;
+                    wave_offer2(key, float_to_sortable(lb), o, lkb, lpb, thrb, lane, kKQ);
+                }
+                if (lane < kKQ) {
+                    s_lk[o0 + lane] = lkb;
+                    s_lp[o0 + lane] = lpb;
+                }
+                if (col == b) tq = sq8_quick(sim, thrb > tkey ? thrb : tkey, sqn, p.cos_slack);
+            }
+        }
+    };
+
+    if (abits && !seg.ord_to_doc) {
+        // filter pushdown: the accepted rows of each 64-row window, compacted (positions in `pos`)
+        for (int64_t w0 = wb; w0 < we && !sampled; w0 += 64) {
+            const int64_t word = w0 >> 6;
+            const int sh = (int)(w0 & 63);
+            uint64_t m = abits[word] >> sh;
+            if (sh && (word + 1) * 64 < we) m |= abits[word + 1] << (64 - sh);
+            if (we - w0 < 64) m &= (1ull << (we - w0)) - 1ull;
+            const int n = __popcll(m);
+            if (n == 0) continue;
+            const bool bit = (m >> lane) & 1ull;
+            const int below = __popcll(m & ((1ull << lane) - 1ull));
+            const int dst = bit ? below : n + (lane - below);
+            const int pos = __builtin_amdgcn_ds_permute(dst << 2, lane);
+            for (int i0 = 0; i0 < n && !sampled; i0 += R) {
+                const int ia = i0 + col;
+                const bool vA = ia < n;
+                const int64_t rowA = w0 + __shfl(pos, vA ? ia : 0);
+                int64_t ro[4];
+                bool vo[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int io = i0 + 4 * grp + i;
+                    vo[i] = io < n;
+                    ro[i] = w0 + __shfl(pos, vo[i] ? io : 0);
+                }
+                process(rowA, vA, ro, vo);
+            }
+        }
+    } else {
+        for (int64_t r0 = wb; r0 < we && !sampled; r0 += R) {
+            const int64_t rowA = r0 + col;
+            const bool vA = rowA < we;
+            int64_t ro[4];
+            bool vo[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                ro[i] = r0 + 4 * grp + i;
+                vo[i] = ro[i] < we;
+                if (vo[i] && abits) {   // sparse field: accept by doc
+                    const int32_t doc = seg.ord_to_doc ? seg.ord_to_doc[ro[i]] : (int32_t)ro[i];
+                    vo[i] = (abits[doc >> 6] >> (doc & 63)) & 1ull;
+                }
+            }
+            process(rowA, vA, ro, vo);
+        }
+    }
+
+    if (pilot) {   // waves with no sampled row leave empty slots
+        if (!sampled && qv)
+            for (int i = 0; i < 4; ++i)
+                p.pilot_keys[((size_t)col * p.n_tiles + blockIdx.x) * 64 + wave * 16 + 4 * grp + i] = 0ull;
+        return;
+    }
+    // visited counts accepted rows: with a filter over a sparse field the unaccepted rows were
+    // loaded (vA) but do not count
+    if (abits && seg.ord_to_doc) {
+        nvis = 0;
+        for (int64_t r0 = wb + lane; r0 < we; r0 += 64) {
+            const int32_t doc = seg.ord_to_doc[r0];
+            nvis += (abits[doc >> 6] >> (doc & 63)) & 1ull;
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) nvis += __shfl_xor(nvis, o);
+    }
+    if (p.visited && p.q0 == 0 && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
+
+    for (int b = 0; b < NQ; ++b) {
+        const uint64_t lkb = lane < kKQ ? s_lk[(wave * NQ + b) * kKQ + lane] : 0ull;
+        const uint32_t lpb = lane < kKQ ? s_lp[(wave * NQ + b) * kKQ + lane] : 0u;
+        uint32_t m = (lane < kKQ && lkb) ? lpb : 0u;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+        if (b < p.q_count) {
+            const size_t l = (size_t)(p.q0 + b) * p.n_lists + blockIdx.x * 4 + wave;
+            if (lane < kKQ) {
+                p.cand[l * kKQ + lane] = lkb;
+                p.cand_lb[l * kKQ + lane] = lpb;
+            }
+            if (lane == 0) p.list_lbmax[l] = m;
+        }
+    }
+}
+
+using Sq8MfmaFn = void (*)(Sq8Params);
+static const int kMfmaKS[6] = {2, 4, 6, 8, 12, 16};
+static const Sq8MfmaFn kSq8Mfma[6] = {sq8_mfma<2>, sq8_mfma<4>, sq8_mfma<6>, sq8_mfma<8>, sq8_mfma<12>, sq8_mfma<16>};
+
+int sq8_mfma_supported(int u8) { return u8 <= 4 * kMfmaKS[5]; }
+
+hipError_t launch_sq8_mfma(const Sq8Params& p, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
+    int c = 0;
+    while (c < 5 && 4 * kMfmaKS[c] < p.units8) ++c;
+    if (4 * kMfmaKS[c] < p.units8) return hipErrorInvalidValue;
+    const size_t lds = (size_t)kMfmaNQ * 4 * kMfmaKS[c] * 16 + (size_t)4 * kMfmaNQ * kKQ * 12;
+    const auto fn = kSq8Mfma[c];
+    if (ev_start || ev_stop)
+        hipExtLaunchKernelGGL(fn, dim3(p.n_tiles), dim3(kBlock), lds, s, ev_start, ev_stop, 0, p);
+    else
+        hipLaunchKernelGGL(fn, dim3(p.n_tiles), dim3(kBlock), lds, s, p);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
 // settle, in slices of kSliceLists wave lists (≤ 512 entries), one workgroup per (slice, query), so
 // every (query, shard) spreads over many workgroups (one workgroup per (query, shard) is
 // latency-bound: ~50 µs):

@@ -22,6 +22,14 @@ def bits(a):
     return np.asarray(a, np.float32).view(np.uint32)
 
 
+@pytest.fixture(autouse=True)
+def bf16x3_from_16():
+    """Batches ≥ 16 take the bf16×3 path in this module (the library default crossover is 96)."""
+    _lib.tune("mfma_min_batch", 16)
+    yield
+    _lib.tune("mfma_min_batch", 96)
+
+
 def streaming(ds_or_reader, fn):
     _lib.tune("mfma_min_batch", 0)
     try:

@@ -6,6 +6,8 @@ the same tie order — which the oracle's ORDER_DEVICE restatement pins.  These 
 two paths (tune "sq8" 1 vs 0) and the oracle over similarities, ragged dims, batch sizes, k,
 filters, sparse doc maps, multi-segment multi-shard views, heavy ties and adversarial data where
 the certificate cannot exclude a whole tile and the settle re-scans that tile exactly instead.
+Every test runs twice: batches scanned by the int8 MFMA kernel (sq8_mfma, tune "sq8_mfma_min" 2,
+the default) and by the VALU kernel (sq8_scan, "sq8_mfma_min" 0).
 """
 import numpy as np
 import pytest
@@ -17,6 +19,14 @@ pytestmark = pytest.mark.gpu
 
 SIMS = [LU.VectorSimilarityFunction(s) for s in range(4)]
 COS = LU.VectorSimilarityFunction.COSINE
+
+
+@pytest.fixture(autouse=True, params=["mfma", "valu"])
+def scan_kernel(request):
+    """The int8 scan kernel of batched prefilter searches (single queries always take sq8_scan)."""
+    _lib.tune("sq8_mfma_min", 2 if request.param == "mfma" else 0)
+    yield request.param
+    _lib.tune("sq8_mfma_min", 2)
 
 
 def corpus(n, dim, sim, seed):
