@@ -112,6 +112,8 @@ def main():
                     help="A/B: batches ≥ this take the bf16×3 MFMA path (osk_tune mfma_min_batch; 0 = library default)")
     ap.add_argument("--sq8-mfma-min", type=int, default=-1,
                     help="A/B: prefilter batches ≥ this scan on int8 MFMA (osk_tune sq8_mfma_min; -1 = library default)")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="A/B: extra osk_tune knobs (e.g. sq8_mfma_nt=0)")
     ap.add_argument("--tiles", type=int, default=0, help="A/B: workgroup tiles per view (osk_tune tiles_target)")
     # ≈10 s of CPU work on 16 host threads (≈1e8 row·queries/s measured): a bounded sample of C3
     ap.add_argument("--cpu-sample-rows", type=int, default=524_288)
@@ -134,6 +136,9 @@ def main():
 
     if a.tiles:
         _lib.tune("tiles_target", a.tiles)
+    for kv in a.tune:
+        key, val = kv.split("=")
+        _lib.tune(key, int(val))
     mfma_min_batch = a.mfma_min_batch or 96   # the library default (osk_internal.h)
     _lib.tune("mfma_min_batch", mfma_min_batch)
     sq8_mfma_min = 2 if a.sq8_mfma_min < 0 else a.sq8_mfma_min

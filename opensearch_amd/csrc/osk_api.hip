@@ -368,6 +368,8 @@ int32_t osk_tune_set(const char* key, int64_t value) {
     } else if (k == "tiles_target") {
         OSK_REQUIRE(value >= 0 && value <= (1 << 22), "tiles_target out of range");
         g_tuning.tiles_target = (int)value;
+    } else if (k == "sq8_mfma_nt") {
+        g_tuning.sq8_mfma_nt = value != 0;
     } else if (k == "sq8_mfma_min") {
         OSK_REQUIRE(value >= 0 && value <= (1 << 20), "sq8_mfma_min out of range");
         g_tuning.sq8_mfma_min = (int)value;
@@ -1041,6 +1043,7 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             // the k-th of them floors the main pass's quick thresholds (sq8_mfma comment)
             p.k = k;
             p.n_shards = S;
+            p.nt = g_tuning.sq8_mfma_nt;
             p.pilot = 1;
             p.pilot_keys = v->ws_pilot.as<uint64_t>();
             OSK_HIP(launch_sq8_mfma(p, st, e0, nullptr));

@@ -144,6 +144,7 @@ struct Sq8Params {
     // lower bound T of the (query, shard) is a floor under every wave list's quick threshold: a row
     // with ub < T ≤ the shard's k-th best lower bound scores below the shard's k-th exact score.
     int pilot;
+    int nt;                          // sq8_mfma: non-temporal row loads (A/B knob sq8_mfma_nt)
     int k;
     int n_shards;
     uint64_t* pilot_keys;
@@ -213,6 +214,7 @@ struct Tuning {
                               // int8 prefilter (sq8_mfma: 8.1k QPS at C3 b16–b64 vs ~5k for bf16×3 at b64)
     int mfma_units = 512;     // workgroup units of the MFMA candidate pass per view
     int sq8 = 1;              // certified int8 prefilter for float32 batches below mfma_min_batch
+    int sq8_mfma_nt = 1;      // A/B: non-temporal row loads in sq8_mfma
     int sq8_mfma_min = 2;     // prefilter batches ≥ this scan on int8 MFMA, 16 queries per launch (0 = never)
     int sq8_force_fallback = 0;   // tests: every list of a prefiltered search is re-scanned exactly
     int settle_trace = 0;     // A/B only: record settle phase timestamps (debug copy "settle_trace")

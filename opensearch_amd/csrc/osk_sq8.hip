@@ -665,7 +665,7 @@ __global__ __launch_bounds__(kBlock, 4) void sq8_mfma(Sq8Params p) {
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             const int f = s * 4 + grp;
-            const int4 v = (vA && f < u8) ? load_i4_nt(xr + f) : make_int4(0, 0, 0, 0);
+            const int4 v = (vA && f < u8) ? (p.nt ? load_i4_nt(xr + f) : xr[f]) : make_int4(0, 0, 0, 0);
             a[s] = i32x4{v.x, v.y, v.z, v.w};
         }
         float4 ax[4];
