@@ -192,6 +192,7 @@ struct osk_seg {
     // certified int8 prefilter (built on first prefiltered search): int8 rows + per-row bound terms
     void* d_q8 = nullptr;
     float4* d_q8aux = nullptr;
+    void* d_q8t = nullptr;    // the int8 rows in sq8_mfma's tiled layout (built on first batched prefilter)
     int units8 = 0;
     std::mutex mu;
     osk_view* self_view = nullptr;   // single-segment view behind osk_seg_search
@@ -225,6 +226,8 @@ struct osk_view {
     int units8 = 0;
     float sq8_gam = 0.f, sq8_g2 = 0.f, sq8_cos_slack = 0.f;
     DevBuf d_sq8_rows, d_sq8_aux, d_counters;   // counters: SettleParams::counters
+    DevBuf d_sq8_rows_t;                         // per segment: tiled int8 copy (sq8_mfma)
+    bool sq8t_ready = false;
     DevBuf ws_q8, ws_qc, ws_sq8cand, ws_sq8lb, ws_lbmax, ws_trace;
     // settle slices: kSliceLists wave lists each, never spanning shards (an empty shard gets one
     // empty slice so that its result is still written)
@@ -274,6 +277,7 @@ osk_seg::~osk_seg() {
     if (d_xsqrt) (void)hipFree(d_xsqrt);
     if (d_q8) (void)hipFree(d_q8);
     if (d_q8aux) (void)hipFree(d_q8aux);
+    if (d_q8t) (void)hipFree(d_q8t);
 }
 
 namespace {
@@ -368,6 +372,8 @@ int32_t osk_tune_set(const char* key, int64_t value) {
     } else if (k == "tiles_target") {
         OSK_REQUIRE(value >= 0 && value <= (1 << 22), "tiles_target out of range");
         g_tuning.tiles_target = (int)value;
+    } else if (k == "sq8_mfma_ablate") {
+        g_tuning.sq8_mfma_ablate = (int)value;
     } else if (k == "sq8_mfma_nt") {
         g_tuning.sq8_mfma_nt = value != 0;
     } else if (k == "sq8_mfma_min") {
@@ -578,8 +584,11 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
             const int64_t n = segs[i]->n_rows;
             if (n == 0) continue;
             const int64_t nt = seg_tiles[i];
-            for (int64_t t = 0; t < nt; ++t)   // balanced split: tile t = rows [n·t/nt, n·(t+1)/nt)
-                tiles.push_back(TileDev{i, sh, n * t / nt, n * (t + 1) / nt});
+            // balanced split at multiples of 16 rows (sq8_mfma's row groups then start on its tiled
+            // copy's 16-row blocks): tile t = rows [⌊n·t/nt⌋₁₆, ⌊n·(t+1)/nt⌋₁₆), the last one ends at n
+            auto cut = [&](int64_t t) { return t >= nt ? n : (n * t / nt) & ~(int64_t)15; };
+            for (int64_t t = 0; t < nt; ++t)
+                if (cut(t + 1) > cut(t)) tiles.push_back(TileDev{i, sh, cut(t), cut(t + 1)});
         }
     }
     v->shard_tile_begin[n_shards] = (int32_t)tiles.size();
@@ -935,6 +944,43 @@ int32_t ensure_sq8_seg(osk_seg* s, hipStream_t st) {
     return OSK_OK;
 }
 
+// The segment's int8 copy in sq8_mfma's tiled layout: blocks of 16 rows, per 64-dim k-step one
+// contiguous 1 KiB slab (row r of the block at r·64 B), so each of the scan's load instructions
+// reads 1 KiB contiguous.  Built once, from the row-major int8 copy.
+int32_t ensure_sq8t_seg(osk_seg* s, hipStream_t st) {
+    std::lock_guard<std::mutex> lk(s->mu);
+    if (s->d_q8t) return OSK_OK;
+    const int u8 = (s->dim + 15) / 16;
+    const int ks = sq8_mfma_ks(u8);
+    const int64_t blocks = std::max<int64_t>(1, (s->n_rows + 15) / 16);
+    void* q8t = nullptr;
+    hipError_t e = hipMalloc(&q8t, (size_t)blocks * ks * 1024);
+    if (e != hipSuccess) {
+        set_error(std::string("hipMalloc of the tiled int8 copy failed: ") + hipGetErrorString(e));
+        return OSK_ERR_OOM;
+    }
+    OSK_HIP(launch_sq8_tile(s->d_q8, s->n_rows, u8, ks, q8t, st));
+    OSK_HIP(hipStreamSynchronize(st));
+    s->d_q8t = q8t;
+    return OSK_OK;
+}
+
+int32_t ensure_sq8t(osk_view* v, hipStream_t st) {
+    if (v->sq8t_ready) return OSK_OK;
+    const int ns = (int)v->segs.size();
+    std::vector<const void*> rows(ns);
+    for (int i = 0; i < ns; ++i) {
+        int32_t rc = ensure_sq8t_seg(v->segs[i], st);
+        if (rc) return rc;
+        rows[i] = v->segs[i]->d_q8t;
+    }
+    OSK_HIP(v->d_sq8_rows_t.reserve(sizeof(void*) * ns));
+    OSK_HIP(hipMemcpyAsync(v->d_sq8_rows_t.p, rows.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
+    OSK_HIP(hipStreamSynchronize(st));
+    v->sq8t_ready = true;
+    return OSK_OK;
+}
+
 int32_t ensure_sq8(osk_view* v, hipStream_t st) {
     if (v->sq8_ready) return OSK_OK;
     const int ns = (int)v->segs.size();
@@ -1026,6 +1072,9 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     const bool use_mfma = g_tuning.sq8_mfma_min > 0 && nq >= g_tuning.sq8_mfma_min && sq8_mfma_supported(u8);
     const int chunk = use_mfma ? kMfmaQueries : kMaxNQ;
     if (use_mfma) {
+        rc = ensure_sq8t(v, st);
+        if (rc) return rc;
+        p.rows8t = v->d_sq8_rows_t.as<const int4*>();
         OSK_HIP(v->ws_pilot.reserve(sizeof(uint64_t) * (size_t)kMfmaQueries * v->n_tiles * 64));
         OSK_HIP(v->ws_thr.reserve(sizeof(uint64_t) * (size_t)kMfmaQueries * S * 64));
         OSK_HIP(v->ws_thr_counts.reserve(sizeof(int32_t) * (size_t)kMfmaQueries * S));
@@ -1039,16 +1088,18 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
         hipEvent_t e0 = v->profile && q0 == 0 ? v->ev0 : nullptr;
         hipEvent_t e1 = v->profile && q0 + chunk >= nq ? v->ev1 : nullptr;
         if (use_mfma) {
-            // pilot: 16 sampled rows per wave → per (query, shard) the top 64 sampled lower bounds;
-            // the k-th of them floors the main pass's quick thresholds (sq8_mfma comment)
+            // pilot: 16 sampled rows per wave → per (query, tile) the top k sampled lower bounds →
+            // per (query, shard) the top k; its k-th floors the main pass's quick thresholds
+            // (sq8_mfma comment)
             p.k = k;
             p.n_shards = S;
             p.nt = g_tuning.sq8_mfma_nt;
+            p.ablate = g_tuning.sq8_mfma_ablate;
             p.pilot = 1;
             p.pilot_keys = v->ws_pilot.as<uint64_t>();
             OSK_HIP(launch_sq8_mfma(p, st, e0, nullptr));
             OSK_HIP(launch_merge_shards(v->ws_pilot.as<uint64_t>(), v->n_tiles, v->d_shard_tile_begin.as<int32_t>(),
-                                        S, p.q_count, 64, v->ws_thr.as<uint64_t>(), v->ws_thr_counts.as<int32_t>(), st));
+                                        S, p.q_count, k, v->ws_thr.as<uint64_t>(), v->ws_thr_counts.as<int32_t>(), st));
             p.pilot = 0;
             p.thr_keys = v->ws_thr.as<uint64_t>();
             p.thr_counts = v->ws_thr_counts.as<int32_t>();

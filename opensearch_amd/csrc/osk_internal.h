@@ -138,13 +138,15 @@ struct Sq8Params {
     float gam;                       // fp32 dot rounding: |dot_dev − x·b| ≤ gam·(|x|² + |b|²)
     float g2;                        // fp32 d² rounding:  |d²_dev − d²| ≤ g2·d²
     float cos_slack;                 // COSINE quick test: norm-order slack
-    // sq8_mfma only.  pilot = 1: each wave scores just its first 16 (accepted) rows and writes their
-    // lower-bound keys to pilot_keys [q_count][n_tiles][64] (slot wave·16 + row); merged per (query,
-    // shard) into thr_keys [q_count][n_shards][64] / thr_counts.  pilot = 0: the k-th best sampled
+    // sq8_mfma only.  pilot = 1: each wave scores just its first 16 (accepted) rows; the tile's top k
+    // lower-bound keys per query go to pilot_keys [q_count][n_tiles][k]; merged per (query, shard)
+    // into thr_keys [q_count][n_shards][k] / thr_counts.  pilot = 0: the k-th best sampled
     // lower bound T of the (query, shard) is a floor under every wave list's quick threshold: a row
     // with ub < T ≤ the shard's k-th best lower bound scores below the shard's k-th exact score.
     int pilot;
+    const int4* const* rows8t;       // sq8_mfma: per segment, the tiled int8 copy (launch_sq8_tile)
     int nt;                          // sq8_mfma: non-temporal row loads (A/B knob sq8_mfma_nt)
+    int ablate;                      // A/B timing only (results wrong): 1 skip the epilogue, 2 skip the MFMAs
     int k;
     int n_shards;
     uint64_t* pilot_keys;
@@ -193,6 +195,10 @@ int sq8_lanes(int units8);         // lanes per row of the int8 scan
 constexpr int kMfmaQueries = 16;
 constexpr int kMfmaScanR = 16;      // its rows per wave-iteration (the settle's scan_R)
 int sq8_mfma_supported(int units8);
+int sq8_mfma_ks(int units8);        // its 64-dim k-steps per row for this row width
+// row-major int8 rows → blocks of 16 rows × ks slabs of 1 KiB (row r of a block at r·64 B; zero past
+// the last row and past units8)
+hipError_t launch_sq8_tile(const void* q8, int64_t n_rows, int units8, int ks, void* out, hipStream_t s);
 hipError_t launch_sq8_mfma(const Sq8Params& p, hipStream_t s, hipEvent_t ev_start = nullptr,
                            hipEvent_t ev_stop = nullptr);
 hipError_t launch_sq8_prep(int cfg, const float* src, int dim, int nq, int nq_pad, int UP, int units8, float4* qpad,
@@ -215,6 +221,7 @@ struct Tuning {
     int mfma_units = 512;     // workgroup units of the MFMA candidate pass per view
     int sq8 = 1;              // certified int8 prefilter for float32 batches below mfma_min_batch
     int sq8_mfma_nt = 1;      // A/B: non-temporal row loads in sq8_mfma
+    int sq8_mfma_ablate = 0;  // A/B timing only: 1 skip sq8_mfma's epilogue, 2 its MFMAs (results wrong)
     int sq8_mfma_min = 2;     // prefilter batches ≥ this scan on int8 MFMA, 16 queries per launch (0 = never)
     int sq8_force_fallback = 0;   // tests: every list of a prefiltered search is re-scanned exactly
     int settle_trace = 0;     // A/B only: record settle phase timestamps (debug copy "settle_trace")

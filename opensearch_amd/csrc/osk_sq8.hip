@@ -619,7 +619,7 @@ __global__ __launch_bounds__(kBlock, 4) void sq8_mfma(Sq8Params p) {
     const int col = lane & 15, grp = lane >> 4;
     const TileDev tile = p.tiles[blockIdx.x];
     const SegDev seg = p.segs[tile.seg];
-    const int4* __restrict__ X = p.rows8[tile.seg];
+    const int4* __restrict__ XT = p.rows8t[tile.seg];   // tiled: [row / 16][KS][16 rows][4 chunks]
     const float4* __restrict__ AX = p.aux[tile.seg];
     const uint32_t vbase = (uint32_t)p.seg_vrow[tile.seg];
     const int u8 = p.units8, sim = p.sim;
@@ -642,7 +642,7 @@ __global__ __launch_bounds__(kBlock, 4) void sq8_mfma(Sq8Params p) {
     uint64_t tkey = 0ull;
     if (!p.pilot && p.thr_keys && qv) {
         const size_t o = (size_t)col * p.n_shards + tile.shard;
-        if (p.thr_counts[o] >= p.k) tkey = p.thr_keys[o * 64 + p.k - 1];
+        if (p.thr_counts[o] >= p.k) tkey = p.thr_keys[o * p.k + p.k - 1];
         // a floor of score 0 (DOT_PRODUCT / COSINE clamp every negative similarity to 0) would drop
         // rows that tie with it: sq8_quick's test is strict only above the clamp
         if (!(key_score(tkey) > 0.0f)) tkey = 0ull;
@@ -660,12 +660,13 @@ __global__ __launch_bounds__(kBlock, 4) void sq8_mfma(Sq8Params p) {
     __syncthreads();
 
     auto process = [&](int64_t rowA, bool vA, const int64_t (&ro)[4], const bool (&vo)[4]) {
-        const int4* xr = X + (vA ? rowA : tile.row_begin) * u8;
+        // row rowA's chunk grp of slab s: an aligned 16-row group reads 1 KiB contiguous per slab
+        const int64_t ra = vA ? rowA : tile.row_begin;
+        const int4* xr = XT + (ra >> 4) * (KS * 64) + (ra & 15) * 4 + grp;
         i32x4 a[KS];
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
-            const int f = s * 4 + grp;
-            const int4 v = (vA && f < u8) ? (p.nt ? load_i4_nt(xr + f) : xr[f]) : make_int4(0, 0, 0, 0);
+            const int4 v = vA ? (p.nt ? load_i4_nt(xr + s * 64) : xr[s * 64]) : make_int4(0, 0, 0, 0);
             a[s] = i32x4{v.x, v.y, v.z, v.w};
         }
         float4 ax[4];
@@ -674,10 +675,19 @@ __global__ __launch_bounds__(kBlock, 4) void sq8_mfma(Sq8Params p) {
         nvis += __popcll(__ballot(lane < 16 && vA));
         i32x4 acc = {0, 0, 0, 0};
         const int4* qrow = sq + col * UQ + grp;
+        if (p.ablate & 2) {
 #pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            const int4 bv = qrow[s * 4];
-            acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[s], i32x4{bv.x, bv.y, bv.z, bv.w}, acc, 0, 0, 0);
+            for (int s = 0; s < KS; ++s) acc ^= a[s];
+        } else {
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const int4 bv = qrow[s * 4];
+                acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[s], i32x4{bv.x, bv.y, bv.z, bv.w}, acc, 0, 0, 0);
+            }
+        }
+        if (p.ablate & 1) {
+            if (acc[0] + acc[1] + acc[2] + acc[3] == 0x7FFFFFFF && ax[0].x == 1.0f) nvis += 1;
+            return;
         }
         bool pass[4];
         float lo[4], hi[4];
@@ -696,8 +706,7 @@ __global__ __launch_bounds__(kBlock, 4) void sq8_mfma(Sq8Params p) {
                     float xnd = 0.0f;
                     if (sim == SIM_COSINE && vo[i]) xnd = seg.xnorm_f[ro[i]];
                     const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi[i]) : score_f32(sim, lo[i], qnd, xnd);
-                    p.pilot_keys[((size_t)col * p.n_tiles + blockIdx.x) * 64 + wave * 16 + 4 * grp + i] =
-                        vo[i] ? make_key(lb, vbase + (uint32_t)ro[i]) : 0ull;
+                    s_lk[col * 64 + wave * 16 + 4 * grp + i] = vo[i] ? make_key(lb, vbase + (uint32_t)ro[i]) : 0ull;
                 }
             }
             sampled = true;
@@ -780,10 +789,23 @@ __global__ __launch_bounds__(kBlock, 4) void sq8_mfma(Sq8Params p) {
         }
     }
 
-    if (pilot) {   // waves with no sampled row leave empty slots
+    if (pilot) {
+        // the tile's 64 sampled keys per query (s_lk as [NQ][64]; waves with no sampled row leave
+        // zeros) → its top k per query → pilot_keys [q][tile][k]: the k-th best of the union of the
+        // tiles' top k is the k-th best sampled lower bound of the shard
         if (!sampled && qv)
-            for (int i = 0; i < 4; ++i)
-                p.pilot_keys[((size_t)col * p.n_tiles + blockIdx.x) * 64 + wave * 16 + 4 * grp + i] = 0ull;
+            for (int i = 0; i < 4; ++i) s_lk[col * 64 + wave * 16 + 4 * grp + i] = 0ull;
+        __syncthreads();
+        for (int b = wave; b < p.q_count; b += 4) {
+            const uint64_t key = s_lk[b * 64 + lane];
+            int rank = 0;
+#pragma unroll 8
+            for (int j = 0; j < 64; ++j) rank += s_lk[b * 64 + j] > key;
+            const int nz = __popcll(__ballot(key != 0ull));
+            uint64_t* o = p.pilot_keys + ((size_t)b * p.n_tiles + blockIdx.x) * p.k;
+            if (key != 0ull && rank < p.k) o[rank] = key;
+            if (lane >= nz && lane < p.k) o[lane] = 0ull;
+        }
         return;
     }
     // visited counts accepted rows: with a filter over a sparse field the unaccepted rows were
@@ -821,6 +843,34 @@ static const int kMfmaKS[6] = {2, 4, 6, 8, 12, 16};
 static const Sq8MfmaFn kSq8Mfma[6] = {sq8_mfma<2>, sq8_mfma<4>, sq8_mfma<6>, sq8_mfma<8>, sq8_mfma<12>, sq8_mfma<16>};
 
 int sq8_mfma_supported(int u8) { return u8 <= 4 * kMfmaKS[5]; }
+int sq8_mfma_ks(int u8) {
+    int c = 0;
+    while (c < 5 && 4 * kMfmaKS[c] < u8) ++c;
+    return kMfmaKS[c];
+}
+
+__global__ __launch_bounds__(kBlock) void sq8_tile(const int4* __restrict__ q8, int64_t n_rows, int u8, int ks,
+                                                   int4* __restrict__ out) {
+    // one thread per 16-B unit of the tiled copy: block b, slab s, row r, chunk c
+    const int64_t n_units = ((n_rows + 15) / 16) * ks * 64;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n_units; i += (int64_t)gridDim.x * kBlock) {
+        const int64_t b = i / (ks * 64);
+        const int rem = (int)(i - b * ks * 64);
+        const int s = rem >> 6, r = (rem >> 2) & 15, c = rem & 3;
+        const int64_t row = b * 16 + r;
+        const int f = s * 4 + c;
+        out[i] = (row < n_rows && f < u8) ? q8[row * u8 + f] : make_int4(0, 0, 0, 0);
+    }
+}
+
+hipError_t launch_sq8_tile(const void* q8, int64_t n_rows, int u8, int ks, void* out, hipStream_t s) {
+    const int64_t n_units = std::max<int64_t>(1, ((n_rows + 15) / 16) * ks * 64);
+    int64_t blocks = (n_units + kBlock - 1) / kBlock;
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(sq8_tile, dim3((unsigned)blocks), dim3(kBlock), 0, s, static_cast<const int4*>(q8), n_rows,
+                       u8, ks, static_cast<int4*>(out));
+    return hipGetLastError();
+}
 
 hipError_t launch_sq8_mfma(const Sq8Params& p, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
     int c = 0;
