@@ -205,22 +205,24 @@ def main():
         _lib.check(_lib.lib().osk_view_counter(shards.view, name.encode(), C.byref(v)))
         return v.value
 
-    batched = B >= mfma_min_batch and K <= 12   # the library's batched bf16×3 MFMA path
-    prefilter = not batched and K <= 12 and not a.no_sq8
-    sq8_mfma = prefilter and sq8_mfma_min > 0 and B >= sq8_mfma_min
     _lib.tune("sq8", 0 if a.no_sq8 else 1)
     fb0, rs0, calls0 = counter("sq8_fallback_queries"), counter("sq8_rescored_rows"), counter("sq8_calls")
     elapsed_max, scan_avg_ms, ev_ms, out = timed(a.steps, a.warmup)
+    # the path the library chose (prefilter searches count sq8_calls; else bf16×3 from batch 16, else fp32)
+    prefilter = counter("sq8_calls") > calls0
+    batched = not prefilter and B >= 16 and K <= 12
+    sq8_mfma = prefilter and sq8_mfma_min > 0 and B >= sq8_mfma_min
     # sanity on the last step: every query got `SIZE` hits from the 10M corpus
     cnt = out[3].cpu().numpy()
     assert np.all(cnt == SIZE), cnt
 
     u8 = (DIM + 15) // 16
     if sq8_mfma:
-        passes = (B + 15) // 16
+        passes = (B + 31) // 32
         bytes_per_launch = rows_local * (u8 * 16 + 16) * passes
-        kernel_name = ("sq8_mfma<KS=12> certified int8 prefilter on v_mfma_i32_16x16x64_i8 (bytes = int8 rows + "
-                       "16-B bound terms per row, once per launch of ≤ 16 queries)")
+        kernel_name = ("sq8_mfma<KS=12,QB=2> certified int8 prefilter on v_mfma_i32_16x16x64_i8 (bytes = int8 rows "
+                       "(tiled copy) + 16-B bound terms per row, once per launch of ≤ 32 queries; time = pilot + "
+                       "pilot merge + main pass)")
     elif prefilter:
         passes = (B + 7) // 8
         bytes_per_launch = rows_local * (u8 * 16 + 16) * passes

@@ -374,6 +374,12 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         g_tuning.tiles_target = (int)value;
     } else if (k == "sq8_mfma_ablate") {
         g_tuning.sq8_mfma_ablate = (int)value;
+    } else if (k == "sq8_mfma_queries") {
+        OSK_REQUIRE(value == 16 || value == 32, "sq8_mfma_queries must be 16 or 32");
+        g_tuning.sq8_mfma_queries = (int)value;
+    } else if (k == "sq8_cost_pct") {
+        OSK_REQUIRE(value >= 0 && value <= 100000, "sq8_cost_pct out of range");
+        g_tuning.sq8_cost_pct = (int)value;
     } else if (k == "sq8_mfma_nt") {
         g_tuning.sq8_mfma_nt = value != 0;
     } else if (k == "sq8_mfma_min") {
@@ -1070,7 +1076,7 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     // batches of ≥ sq8_mfma_min queries: the int8 MFMA scan, 16 queries per launch; else the VALU
     // scan, ≤ 8 per launch
     const bool use_mfma = g_tuning.sq8_mfma_min > 0 && nq >= g_tuning.sq8_mfma_min && sq8_mfma_supported(u8);
-    const int chunk = use_mfma ? kMfmaQueries : kMaxNQ;
+    const int chunk = use_mfma ? g_tuning.sq8_mfma_queries : kMaxNQ;
     if (use_mfma) {
         rc = ensure_sq8t(v, st);
         if (rc) return rc;
@@ -1168,8 +1174,12 @@ int32_t view_search_device(osk_view* v, const void* d_queries, int nq, int k,
     OSK_HIP(v->ws_cand.reserve(sizeof(uint64_t) * (size_t)nq * v->n_tiles * k));
     OSK_HIP(v->ws_q.reserve((size_t)nq_pad * UP * 16));
     OSK_HIP(v->ws_qnorm.reserve(sizeof(float) * nq_pad));
+    // bf16×3 works in blocks of 256 queries; the int8 prefilter (k ≤ kKQ − 4) costs ≈ sq8_cost_pct % of a
+    // bf16×3 block per 256 queries (C3: 32 queries per 2.5 ms launch vs 11.5 ms per 256-query block)
+    const bool sq8_ok = v->enc == ENC_FLOAT32 && g_tuning.sq8 && k <= kKQ - 4;
+    const bool blocks_cheaper = (int64_t)((nq + 255) / 256) * 256 * 100 <= (int64_t)nq * g_tuning.sq8_cost_pct;
     const bool batched = v->enc == ENC_FLOAT32 && g_tuning.mfma_min_batch > 0 &&
-                         nq >= g_tuning.mfma_min_batch && k <= kKC - 4;
+                         nq >= g_tuning.mfma_min_batch && k <= kKC - 4 && (!sq8_ok || blocks_cheaper);
     // k ≤ kKQ − 4: a tile list holds 4 more rows than k, so it rarely overflows past the certificate
     const bool prefilter = !batched && v->enc == ENC_FLOAT32 && g_tuning.sq8 && k <= kKQ - 4;
     // queries → padded unit layout (zeros past dim and for the dummy queries of the last launch); the

@@ -192,7 +192,7 @@ hipError_t launch_sq8_scan(int nq, const Sq8Params& p, hipStream_t s, hipEvent_t
                            hipEvent_t ev_stop = nullptr);
 int sq8_lanes(int units8);         // lanes per row of the int8 scan
 // int8 MFMA prefilter scan: ≤ kMfmaQueries queries per launch, rows ≤ 1024 int8 dims (sq8_mfma_supported)
-constexpr int kMfmaQueries = 16;
+constexpr int kMfmaQueries = 32;
 constexpr int kMfmaScanR = 16;      // its rows per wave-iteration (the settle's scan_R)
 int sq8_mfma_supported(int units8);
 int sq8_mfma_ks(int units8);        // its 64-dim k-steps per row for this row width
@@ -216,11 +216,14 @@ struct Tuning {
     int tile_max_rounds = 4;      // at most this many rounds (10M rows: 4096 tiles, profiles/r01e)
     int tile_min_rows = 1024; // ...and at least this many rows per tile (1.25M rows: 1024 tiles of 1221
                               // rows, 4360 QPS vs 3968 for 4096 tiles of 305 rows — profiles/r01e/tiles_ab.txt)
-    int mfma_min_batch = 96;  // batches ≥ this use the bf16×3 MFMA candidate path (0 = never); below it the
-                              // int8 prefilter (sq8_mfma: 8.1k QPS at C3 b16–b64 vs ~5k for bf16×3 at b64)
+    int mfma_min_batch = 96;  // batches ≥ this may take the bf16×3 MFMA candidate path (0 = never)...
+    int sq8_cost_pct = 174;   // ...when ⌈nq/256⌉·256 ≤ nq · this / 100 (prefilter cost per 256 queries over a
+                              // bf16×3 block's: C3 20 ms vs 11.5 ms; b128 11.8k vs 6.0k QPS, b256 11.8k vs
+                              // 22.1k), else the int8 prefilter
     int mfma_units = 512;     // workgroup units of the MFMA candidate pass per view
     int sq8 = 1;              // certified int8 prefilter for float32 batches below mfma_min_batch
     int sq8_mfma_nt = 1;      // A/B: non-temporal row loads in sq8_mfma
+    int sq8_mfma_queries = 32;    // queries per sq8_mfma launch: 16 or 32 (two MFMA chains per row operand)
     int sq8_mfma_ablate = 0;  // A/B timing only: 1 skip sq8_mfma's epilogue, 2 its MFMAs (results wrong)
     int sq8_mfma_min = 2;     // prefilter batches ≥ this scan on int8 MFMA, 16 queries per launch (0 = never)
     int sq8_force_fallback = 0;   // tests: every list of a prefiltered search is re-scanned exactly

@@ -610,11 +610,11 @@ hipError_t launch_sq8_scan(int nq, const Sq8Params& p, hipStream_t s, hipEvent_t
 // numbering are sq8_scan's with R = 16 rows per wave-iteration (the settle re-scans with scan_R = 16).
 // Filter pushdown: accepted rows are compacted 64 at a time; any row can feed any MFMA row slot.
 // ------------------------------------------------------------------------------------------------
-constexpr int kMfmaNQ = 16;
-template <int KS>
-__global__ __launch_bounds__(kBlock, 4) void sq8_mfma(Sq8Params p) {
+// QB query blocks of 16 per launch (QB = 2: 32 queries, two MFMA chains sharing the row operand).
+template <int KS, int QB>
+__global__ __launch_bounds__(kBlock, QB == 1 ? 4 : 3) void sq8_mfma(Sq8Params p) {
     typedef int i32x4 __attribute__((ext_vector_type(4)));
-    constexpr int NQ = kMfmaNQ, R = 16, UQ = 4 * KS;   // UQ: 16-B units per query in LDS
+    constexpr int NQ = 16 * QB, R = 16, UQ = 4 * KS;   // UQ: 16-B units per query in LDS
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int col = lane & 15, grp = lane >> 4;
     const TileDev tile = p.tiles[blockIdx.x];
@@ -634,20 +634,30 @@ __global__ __launch_bounds__(kBlock, 4) void sq8_mfma(Sq8Params p) {
         s_lk[i] = 0ull;
         s_lp[i] = 0u;
     }
-    const bool qv = col < p.q_count;
-    const float4 qc = qv ? p.qc[col] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float qnd = (sim == SIM_COSINE && qv) ? p.qn_dev[col] : 0.0f;
-    const float sqn = sqrtf(qnd);
-    // the pilot's floor key T of (query col, this tile's shard): 0 = none (fewer than k sampled rows)
-    uint64_t tkey = 0ull;
-    if (!p.pilot && p.thr_keys && qv) {
-        const size_t o = (size_t)col * p.n_shards + tile.shard;
-        if (p.thr_counts[o] >= p.k) tkey = p.thr_keys[o * p.k + p.k - 1];
-        // a floor of score 0 (DOT_PRODUCT / COSINE clamp every negative similarity to 0) would drop
-        // rows that tie with it: sq8_quick's test is strict only above the clamp
-        if (!(key_score(tkey) > 0.0f)) tkey = 0ull;
+    // this lane's queries: qb·16 + col
+    bool qv[QB];
+    float4 qc[QB];
+    float qnd[QB], sqn[QB], tq[QB];
+    uint64_t tkey[QB];
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+        const int qi = qb * 16 + col;
+        qv[qb] = qi < p.q_count;
+        qc[qb] = qv[qb] ? p.qc[qi] : make_float4(0.f, 0.f, 0.f, 0.f);
+        qnd[qb] = (sim == SIM_COSINE && qv[qb]) ? p.qn_dev[qi] : 0.0f;
+        sqn[qb] = sqrtf(qnd[qb]);
+        // the pilot's floor key T of (query qi, this tile's shard): 0 = none (< k sampled rows)
+        uint64_t t = 0ull;
+        if (!p.pilot && p.thr_keys && qv[qb]) {
+            const size_t o = (size_t)qi * p.n_shards + tile.shard;
+            if (p.thr_counts[o] >= p.k) t = p.thr_keys[o * p.k + p.k - 1];
+            // a floor of score 0 (DOT_PRODUCT / COSINE clamp every negative similarity to 0) would
+            // drop rows that tie with it: sq8_quick's test is strict only above the clamp
+            if (!(key_score(t) > 0.0f)) t = 0ull;
+        }
+        tkey[qb] = t;
+        tq[qb] = sq8_quick(sim, t, sqn[qb], p.cos_slack);
     }
-    float tq = sq8_quick(sim, tkey, sqn, p.cos_slack);
     const bool pilot = p.pilot != 0;
     bool sampled = false;   // pilot: this wave's first group is done
 
@@ -673,70 +683,89 @@ __global__ __launch_bounds__(kBlock, 4) void sq8_mfma(Sq8Params p) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) ax[i] = vo[i] ? AX[ro[i]] : make_float4(0.f, 0.f, 0.f, 0.f);
         nvis += __popcll(__ballot(lane < 16 && vA));
-        i32x4 acc = {0, 0, 0, 0};
-        const int4* qrow = sq + col * UQ + grp;
+        i32x4 acc[QB];
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) acc[qb] = i32x4{0, 0, 0, 0};
         if (p.ablate & 2) {
 #pragma unroll
-            for (int s = 0; s < KS; ++s) acc ^= a[s];
+            for (int s = 0; s < KS; ++s) acc[0] ^= a[s];
         } else {
 #pragma unroll
-            for (int s = 0; s < KS; ++s) {
-                const int4 bv = qrow[s * 4];
-                acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[s], i32x4{bv.x, bv.y, bv.z, bv.w}, acc, 0, 0, 0);
-            }
+            for (int s = 0; s < KS; ++s)
+#pragma unroll
+                for (int qb = 0; qb < QB; ++qb) {
+                    const int4 bv = sq[(qb * 16 + col) * UQ + s * 4 + grp];
+                    acc[qb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[s], i32x4{bv.x, bv.y, bv.z, bv.w}, acc[qb],
+                                                                    0, 0, 0);
+                }
         }
         if (p.ablate & 1) {
-            if (acc[0] + acc[1] + acc[2] + acc[3] == 0x7FFFFFFF && ax[0].x == 1.0f) nvis += 1;
+            if (acc[0][0] + acc[0][1] + acc[0][2] + acc[0][3] == 0x7FFFFFFF && ax[0].x == 1.0f) nvis += 1;
             return;
         }
-        bool pass[4];
-        float lo[4], hi[4];
-        bool anyp = false;
+        bool pass[QB][4];
+        float lo[QB][4], hi[QB][4];
+        uint32_t qm = 0u;   // queries with a passing lane (wave-uniform after the ballots)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const float sx = sim == SIM_COSINE ? sqrtf(ax[i].w) : 0.0f;
-            sq8_bounds(sim, (float)acc[i], ax[i], qc, p.gam, p.g2, lo[i], hi[i]);
-            pass[i] = vo[i] && qv && sq8_pass(sim, lo[i], hi[i], tq, sx);
-            anyp |= pass[i];
+        for (int qb = 0; qb < QB; ++qb) {
+            bool anyp = false;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float sx = sim == SIM_COSINE ? sqrtf(ax[i].w) : 0.0f;
+                sq8_bounds(sim, (float)acc[qb][i], ax[i], qc[qb], p.gam, p.g2, lo[qb][i], hi[qb][i]);
+                pass[qb][i] = vo[i] && qv[qb] && sq8_pass(sim, lo[qb][i], hi[qb][i], tq[qb], sx);
+                anyp |= pass[qb][i];
+            }
+            if (!pilot) {
+                const uint64_t bl = __ballot(anyp);
+                qm |= (uint32_t)((bl | (bl >> 16) | (bl >> 32) | (bl >> 48)) & 0xFFFFull) << (16 * qb);
+            }
         }
         if (pilot) {   // the sampled rows' lower-bound keys (distinct: they carry the view row)
-            if (qv) {
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb) {
+                if (!qv[qb]) continue;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     float xnd = 0.0f;
                     if (sim == SIM_COSINE && vo[i]) xnd = seg.xnorm_f[ro[i]];
-                    const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi[i]) : score_f32(sim, lo[i], qnd, xnd);
-                    s_lk[col * 64 + wave * 16 + 4 * grp + i] = vo[i] ? make_key(lb, vbase + (uint32_t)ro[i]) : 0ull;
+                    const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi[qb][i])
+                                                          : score_f32(sim, lo[qb][i], qnd[qb], xnd);
+                    s_lk[(qb * 16 + col) * 64 + wave * 16 + 4 * grp + i] =
+                        vo[i] ? make_key(lb, vbase + (uint32_t)ro[i]) : 0ull;
                 }
             }
             sampled = true;
             return;
         }
-        const uint64_t bl = __ballot(anyp);
-        if (bl) {   // wave-uniform: rare once the lists have filled
-            uint32_t qm = (uint32_t)((bl | (bl >> 16) | (bl >> 32) | (bl >> 48)) & 0xFFFFull);
-            while (qm) {
-                const int b = __builtin_ctz(qm);
-                qm &= qm - 1u;
-                const int o0 = (wave * NQ + b) * kKQ;
-                uint64_t lkb = lane < kKQ ? s_lk[o0 + lane] : 0ull;
-                uint32_t lpb = lane < kKQ ? s_lp[o0 + lane] : 0u;
-                uint64_t thrb = readlane64(lkb, kKQ - 1);
+        while (qm) {   // rare once the lists have filled
+            const int b = __builtin_ctz(qm);
+            qm &= qm - 1u;
+            const int bq = b >> 4, bc = b & 15;
+            const int o0 = (wave * NQ + b) * kKQ;
+            uint64_t lkb = lane < kKQ ? s_lk[o0 + lane] : 0ull;
+            uint32_t lpb = lane < kKQ ? s_lp[o0 + lane] : 0u;
+            uint64_t thrb = readlane64(lkb, kKQ - 1);
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb) {
+                if (qb != bq) continue;   // (wave-uniform)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const bool o = pass[i] && col == b;
+                    const bool o = pass[qb][i] && col == bc;
                     float xnd = 0.0f;
                     if (sim == SIM_COSINE && o) xnd = seg.xnorm_f[ro[i]];
-                    const float ub = sim == SIM_EUCLIDEAN ? score_f32_l2(lo[i]) : score_f32(sim, hi[i], qnd, xnd);
-                    const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi[i]) : score_f32(sim, lo[i], qnd, xnd);
+                    const float ub = sim == SIM_EUCLIDEAN ? score_f32_l2(lo[qb][i])
+                                                          : score_f32(sim, hi[qb][i], qnd[qb], xnd);
+                    const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi[qb][i])
+                                                          : score_f32(sim, lo[qb][i], qnd[qb], xnd);
                     const uint64_t key = o ? make_key(ub, vbase + (uint32_t)ro[i]) : 0ull;
                     wave_offer2(key, float_to_sortable(lb), o, lkb, lpb, thrb, lane, kKQ);
                 }
-                if (lane < kKQ) {
-                    s_lk[o0 + lane] = lkb;
-                    s_lp[o0 + lane] = lpb;
-                }
-                if (col == b) tq = sq8_quick(sim, thrb > tkey ? thrb : tkey, sqn, p.cos_slack);
+                if (col == bc) tq[qb] = sq8_quick(sim, thrb > tkey[qb] ? thrb : tkey[qb], sqn[qb], p.cos_slack);
+            }
+            if (lane < kKQ) {
+                s_lk[o0 + lane] = lkb;
+                s_lp[o0 + lane] = lpb;
             }
         }
     };
@@ -793,8 +822,9 @@ __global__ __launch_bounds__(kBlock, 4) void sq8_mfma(Sq8Params p) {
         // the tile's 64 sampled keys per query (s_lk as [NQ][64]; waves with no sampled row leave
         // zeros) → its top k per query → pilot_keys [q][tile][k]: the k-th best of the union of the
         // tiles' top k is the k-th best sampled lower bound of the shard
-        if (!sampled && qv)
-            for (int i = 0; i < 4; ++i) s_lk[col * 64 + wave * 16 + 4 * grp + i] = 0ull;
+        if (!sampled)
+            for (int qb = 0; qb < QB; ++qb)
+                for (int i = 0; i < 4; ++i) s_lk[(qb * 16 + col) * 64 + wave * 16 + 4 * grp + i] = 0ull;
         __syncthreads();
         for (int b = wave; b < p.q_count; b += 4) {
             const uint64_t key = s_lk[b * 64 + lane];
@@ -840,7 +870,9 @@ __global__ __launch_bounds__(kBlock, 4) void sq8_mfma(Sq8Params p) {
 
 using Sq8MfmaFn = void (*)(Sq8Params);
 static const int kMfmaKS[6] = {2, 4, 6, 8, 12, 16};
-static const Sq8MfmaFn kSq8Mfma[6] = {sq8_mfma<2>, sq8_mfma<4>, sq8_mfma<6>, sq8_mfma<8>, sq8_mfma<12>, sq8_mfma<16>};
+#define OSK_MFMA_ROW(KS) {sq8_mfma<KS, 1>, sq8_mfma<KS, 2>}
+static const Sq8MfmaFn kSq8Mfma[6][2] = {OSK_MFMA_ROW(2), OSK_MFMA_ROW(4), OSK_MFMA_ROW(6),
+                                         OSK_MFMA_ROW(8), OSK_MFMA_ROW(12), OSK_MFMA_ROW(16)};
 
 int sq8_mfma_supported(int u8) { return u8 <= 4 * kMfmaKS[5]; }
 int sq8_mfma_ks(int u8) {
@@ -876,8 +908,9 @@ hipError_t launch_sq8_mfma(const Sq8Params& p, hipStream_t s, hipEvent_t ev_star
     int c = 0;
     while (c < 5 && 4 * kMfmaKS[c] < p.units8) ++c;
     if (4 * kMfmaKS[c] < p.units8) return hipErrorInvalidValue;
-    const size_t lds = (size_t)kMfmaNQ * 4 * kMfmaKS[c] * 16 + (size_t)4 * kMfmaNQ * kKQ * 12;
-    const auto fn = kSq8Mfma[c];
+    const int qb = p.q_count > 16 ? 2 : 1;
+    const size_t lds = (size_t)16 * qb * 4 * kMfmaKS[c] * 16 + (size_t)4 * 16 * qb * kKQ * 12;
+    const auto fn = kSq8Mfma[c][qb - 1];
     if (ev_start || ev_stop)
         hipExtLaunchKernelGGL(fn, dim3(p.n_tiles), dim3(kBlock), lds, s, ev_start, ev_stop, 0, p);
     else

@@ -24,10 +24,13 @@ def bits(a):
 
 @pytest.fixture(autouse=True)
 def bf16x3_from_16():
-    """Batches ≥ 16 take the bf16×3 path in this module (the library default crossover is 96)."""
+    """Batches ≥ 16 take the bf16×3 path in this module (the library default: from batch 96 when its
+    256-query blocks are cheaper than the int8 prefilter, tune sq8_cost_pct)."""
     _lib.tune("mfma_min_batch", 16)
+    _lib.tune("sq8_cost_pct", 100000)
     yield
     _lib.tune("mfma_min_batch", 96)
+    _lib.tune("sq8_cost_pct", 174)
 
 
 def streaming(ds_or_reader, fn):

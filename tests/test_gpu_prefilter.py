@@ -6,8 +6,9 @@ the same tie order — which the oracle's ORDER_DEVICE restatement pins.  These 
 two paths (tune "sq8" 1 vs 0) and the oracle over similarities, ragged dims, batch sizes, k,
 filters, sparse doc maps, multi-segment multi-shard views, heavy ties and adversarial data where
 the certificate cannot exclude a whole tile and the settle re-scans that tile exactly instead.
-Every test runs twice: batches scanned by the int8 MFMA kernel (sq8_mfma, tune "sq8_mfma_min" 2,
-the default) and by the VALU kernel (sq8_scan, "sq8_mfma_min" 0).
+Every test runs three times: batches scanned by the int8 MFMA kernel (sq8_mfma, tune "sq8_mfma_min"
+2, the default) with 32 and with 16 queries per launch, and by the VALU kernel (sq8_scan,
+"sq8_mfma_min" 0).
 """
 import numpy as np
 import pytest
@@ -21,12 +22,15 @@ SIMS = [LU.VectorSimilarityFunction(s) for s in range(4)]
 COS = LU.VectorSimilarityFunction.COSINE
 
 
-@pytest.fixture(autouse=True, params=["mfma", "valu"])
+@pytest.fixture(autouse=True, params=["mfma32", "mfma16", "valu"])
 def scan_kernel(request):
-    """The int8 scan kernel of batched prefilter searches (single queries always take sq8_scan)."""
-    _lib.tune("sq8_mfma_min", 2 if request.param == "mfma" else 0)
+    """The int8 scan kernel of batched prefilter searches (single queries always take sq8_scan):
+    sq8_mfma with 32 or 16 queries per launch, or the VALU sq8_scan."""
+    _lib.tune("sq8_mfma_min", 0 if request.param == "valu" else 2)
+    _lib.tune("sq8_mfma_queries", 16 if request.param == "mfma16" else 32)
     yield request.param
     _lib.tune("sq8_mfma_min", 2)
+    _lib.tune("sq8_mfma_queries", 32)
 
 
 def corpus(n, dim, sim, seed):
@@ -96,7 +100,7 @@ def test_prefilter_equals_exact_scan_and_oracle(dim, sim):
         r.close()
 
 
-@pytest.mark.parametrize("nq", [1, 2, 3, 5, 8, 9, 15])
+@pytest.mark.parametrize("nq", [1, 2, 3, 5, 8, 9, 15, 17, 32, 40])
 @pytest.mark.parametrize("k", [1, 7, 10, 12, 16])
 def test_prefilter_batches_and_k(nq, k):
     sim = COS
