@@ -179,13 +179,22 @@ int32_t osk_view_scan_time(osk_view* view, double* total_ms, int64_t* calls);
 
 /* Process-wide tuning knobs for benchmarks / A-B runs:
  *   "scan_nt"         0|1 non-temporal corpus loads in the streaming scan (default 1)
- *   "tiles_target"    workgroup tiles per view for the streaming scan (default 4096; at view create)
+ *   "tiles_target"    workgroup tiles per view for the scans (default 0 = whole rounds of the chip's
+ *                     resident slots; at view create)
+ *   "tile_slots_per_cu", "tile_max_rounds"  ...its resident workgroups per CU (4) and rounds cap (4)
  *   "tile_min_rows"   ...with at least this many rows per tile (default 1024; at view create)
- *   "mfma_min_batch"  batches of at least this many float32 queries (and k ≤ 12) take the batched
- *                     MFMA path (default 16; 0 = never)
+ *   "mfma_min_batch"  batches of at least this many float32 queries (and k ≤ 12) may take the bf16×3
+ *                     MFMA path (default 96; 0 = never)...
+ *   "sq8_cost_pct"    ...when its 256-query blocks cost ≤ this % of the int8 prefilter's time for the
+ *                     same queries (default 174, measured at C3)
  *   "mfma_units"      workgroup units of the MFMA candidate pass per view (default 512)
- *   "sq8"             0|1 certified int8 prefilter for float32 searches below mfma_min_batch with
- *                     k ≤ 12 (default 1; results are bit-identical either way)
+ *   "sq8"             0|1 certified int8 prefilter for float32 searches with k ≤ 12 that do not take
+ *                     the bf16×3 path (default 1; results are bit-identical either way)
+ *   "sq8_mfma_min"    prefilter batches of at least this many queries scan on int8 MFMA (sq8_mfma,
+ *                     default 2; 0 = always the VALU sq8_scan)
+ *   "sq8_mfma_queries"  16 | 32 queries per sq8_mfma launch (default 32)
+ *   "sq8_mfma_nt"     0|1 non-temporal row loads in sq8_mfma (default 1)
+ *   "sq8_mfma_ablate" A/B timing only, results wrong: 1 skip sq8_mfma's epilogue, 2 its MFMAs
  *   "sq8_force_fallback"  tests: every tile of a prefiltered search is re-scanned exactly */
 int32_t osk_tune_set(const char* key, int64_t value);
 

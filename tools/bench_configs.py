@@ -90,7 +90,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="C1,C2,C3,C4,C5f,C5i")
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--c4-batches", default="1,1024")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE")
     a = ap.parse_args()
+    for kv in a.tune:
+        key, val = kv.split("=")
+        _lib.tune(key, int(val))
     only = set(a.only.split(","))
     torch.cuda.set_device(0)
     st, wu = a.steps, 3
@@ -132,10 +137,9 @@ def main():
     if "C4" in only:
         v = View(8, 12_500_000, 96, _lib.DOT_PRODUCT, _lib.FLOAT32, _lib.DIST_NORMALISH_UNIT)
         q = qpool(2048, 96, _lib.DIST_NORMALISH_UNIT)
-        ms, km = run(v, q, 1, st, wu)
-        emit("C4", v, 1, ms, km, 100_000_000 * 96 * 4)
-        ms, km = run(v, q, 1024, max(3, st // 4), 2)
-        emit("C4", v, 1024, ms, km, 100_000_000 * 96 * 4 * 4)
+        for b in [int(x) for x in a.c4_batches.split(",")]:
+            ms, km = run(v, q, b, st if b < 64 else max(3, st // 4), wu if b < 64 else 2)
+            emit("C4", v, b, ms, km, 100_000_000 * 96 * 4 * ((b + 255) // 256))
         v.close()
     if "C5i" in only:
         v = View(8, 1_250_000, 768, _lib.EUCLIDEAN, _lib.BYTE, _lib.DIST_INT8)
