@@ -391,6 +391,9 @@ int32_t osk_tune_set(const char* key, int64_t value) {
     } else if (k == "tile_max_rounds") {
         OSK_REQUIRE(value >= 1 && value <= 1024, "tile_max_rounds out of range");
         g_tuning.tile_max_rounds = (int)value;
+    } else if (k == "tile_large_slots") {
+        OSK_REQUIRE(value >= 0 && value <= 1024, "tile_large_slots out of range");
+        g_tuning.tile_large_slots = (int)value;
     } else if (k == "tile_min_rows") {
         OSK_REQUIRE(value >= 1 && value <= (1 << 24), "tile_min_rows out of range");
         g_tuning.tile_min_rows = (int)value;
@@ -558,6 +561,13 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
         const int64_t rounds = std::min<int64_t>(std::max(1, g_tuning.tile_max_rounds),
                                                  std::max<int64_t>(1, total / (slots * min_rows)));
         target = rounds * slots;
+        // large views: whole rounds of BOTH scan kernels' residency.  sq8_scan holds 4 workgroups per
+        // CU but sq8_mfma at 32 queries only 3 (LDS), so 4 rounds of 4 slots leave sq8_mfma a third
+        // of a tail round.  cus × tile_large_slots tiles (24 = 2 · lcm(3, 4)) are 6 full sq8_scan rounds
+        // and 8 full sq8_mfma rounds (profiles/r01l/tiles_ab.txt: C3 b32 2.72 -> 2.47 ms, C4 b32
+        // 7.2 -> 6.5 ms, C3 b1 within 1%).
+        const int64_t large = (int64_t)cus * g_tuning.tile_large_slots;
+        if (g_tuning.tile_large_slots > 0 && total >= large * min_rows) target = large;
     }
     // split the target over segments in proportion to their rows (largest remainder), each segment's
     // share capped so its tiles keep ≥ min_rows rows

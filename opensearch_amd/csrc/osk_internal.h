@@ -213,6 +213,7 @@ struct Tuning {
     int tiles_target = 0;     // workgroup tiles per view (scan grid size); 0 = whole rounds of the chip's
                               // resident slots (osk_view_create)
     int tile_slots_per_cu = 4;    // resident scan workgroups per CU (4 waves/SIMD, 256-thread groups)
+    int tile_large_slots = 24;    // views of ≥ CUs × this × tile_min_rows rows: CUs × this tiles (0 = off)
     int tile_max_rounds = 4;      // at most this many rounds (10M rows: 4096 tiles, profiles/r01e)
     int tile_min_rows = 1024; // ...and at least this many rows per tile (1.25M rows: 1024 tiles of 1221
                               // rows, 4360 QPS vs 3968 for 4096 tiles of 305 rows — profiles/r01e/tiles_ab.txt)

@@ -271,6 +271,21 @@ __device__ __forceinline__ bool sq8_pass(int sim, float lo, float hi, float tq, 
     return !(hi < tq);
 }
 
+// Global-address-space loads (global_load, not flat_load): a flat load also counts in lgkmcnt, so
+// the first LDS read after it would wait for every row load in flight, prefetched ones included.
+__device__ __forceinline__ int4 load_i4_g(const int4* p, bool nt) {
+    typedef int i4v __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) const i4v gi4v;
+    const gi4v* g = (const gi4v*)p;
+    const i4v v = nt ? __builtin_nontemporal_load(g) : *g;
+    return make_int4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float4 load_f4_g(const float4* p) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) const f4v gf4v;
+    const f4v v = *(const gf4v*)p;
+    return make_float4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ int4 load_i4_nt(const int4* p) {
     typedef int i4v __attribute__((ext_vector_type(4)));
     const i4v v = __builtin_nontemporal_load(reinterpret_cast<const i4v*>(p));
@@ -669,19 +684,22 @@ __global__ __launch_bounds__(kBlock, QB == 1 ? 4 : 3) void sq8_mfma(Sq8Params p)
     uint32_t nvis = 0;
     __syncthreads();
 
-    auto process = [&](int64_t rowA, bool vA, const int64_t (&ro)[4], const bool (&vo)[4]) {
+    auto load_group = [&](int64_t rowA, bool vA, i32x4 (&a)[KS]) {
         // row rowA's chunk grp of slab s: an aligned 16-row group reads 1 KiB contiguous per slab
         const int64_t ra = vA ? rowA : tile.row_begin;
         const int4* xr = XT + (ra >> 4) * (KS * 64) + (ra & 15) * 4 + grp;
-        i32x4 a[KS];
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
-            const int4 v = vA ? (p.nt ? load_i4_nt(xr + s * 64) : xr[s * 64]) : make_int4(0, 0, 0, 0);
+            const int4 v = vA ? load_i4_g(xr + s * 64, p.nt) : make_int4(0, 0, 0, 0);
             a[s] = i32x4{v.x, v.y, v.z, v.w};
         }
-        float4 ax[4];
+    };
+    auto load_aux = [&](const int64_t (&ro)[4], const bool (&vo)[4], float4 (&ax)[4]) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ax[i] = vo[i] ? AX[ro[i]] : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int i = 0; i < 4; ++i) ax[i] = vo[i] ? load_f4_g(AX + ro[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    auto process_loaded = [&](const i32x4 (&a)[KS], const float4 (&ax)[4], bool vA, const int64_t (&ro)[4],
+                              const bool (&vo)[4]) {
         nvis += __popcll(__ballot(lane < 16 && vA));
         i32x4 acc[QB];
 #pragma unroll
@@ -768,6 +786,13 @@ __global__ __launch_bounds__(kBlock, QB == 1 ? 4 : 3) void sq8_mfma(Sq8Params p)
                 s_lp[o0 + lane] = lpb;
             }
         }
+    };
+    auto process = [&](int64_t rowA, bool vA, const int64_t (&ro)[4], const bool (&vo)[4]) {
+        i32x4 a[KS];
+        load_group(rowA, vA, a);
+        float4 ax[4];
+        load_aux(ro, vo, ax);
+        process_loaded(a, ax, vA, ro, vo);
     };
 
     if (abits && !seg.ord_to_doc) {

@@ -11,17 +11,24 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from opensearch_amd import _lib, distributed as D  # noqa: E402
 from opensearch_amd._lib import check, lib  # noqa: E402
 
+# argv: [C3|C4] [batch]  (C3: 8 × 1.25M × 768 COSINE; C4: 8 × 12.5M × 96 DOT_PRODUCT)
+cfg = sys.argv[1] if len(sys.argv) > 1 else "C3"
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+K = 10
+RPS, DIM, SIM = (1_250_000, 768, _lib.COSINE) if cfg == "C3" else (12_500_000, 96, _lib.DOT_PRODUCT)
+# TUNE="key=value,..." sets library knobs (osk_tune_set) before staging
+for kv in filter(None, os.environ.get("TUNE", "").split(",")):
+    _lib.tune(kv.split("=")[0], int(kv.split("=")[1]))
 torch.cuda.set_device(0)
 s = torch.cuda.Stream()
 torch.cuda.set_stream(s)
 st = s.cuda_stream
-B, K = 16, 10
-shards = D.LocalShards(0, 1, 8, 1_250_000, 768, _lib.COSINE, _lib.FLOAT32, 42, _lib.DIST_NORMALISH_UNIT, 0)
-q = torch.randn(B, 768, device="cuda")
+shards = D.LocalShards(0, 1, 8, RPS, DIM, SIM, _lib.FLOAT32, 42, _lib.DIST_NORMALISH_UNIT, 0)
+q = torch.randn(B, DIM, device="cuda")
 q = q / q.norm(dim=1, keepdim=True)
 kk = torch.empty((B, 8, K), dtype=torch.int64, device="cuda")
 cc = torch.empty((B, 8), dtype=torch.int32, device="cuda")
-for ab in (0, 1, 2, 3, 0):
+for ab in [int(x) for x in os.environ.get("ABLATE", "0,1,2,3,0").split(",")]:
     _lib.tune("sq8_mfma_ablate", ab)
     for _ in range(3):
         shards.search(q.data_ptr(), B, K, kk, cc, st)
@@ -33,6 +40,6 @@ for ab in (0, 1, 2, 3, 0):
     ms, n = C.c_double(), C.c_int64()
     check(lib().osk_view_scan_time(shards.view, C.byref(ms), C.byref(n)))
     check(lib().osk_view_profile(shards.view, 0))
-    print(f"ablate={ab}: {ms.value / max(1, n.value):.3f} ms per 16-query scan (pilot+merge+main)", flush=True)
+    print(f"{cfg} b{B} {os.environ.get('TUNE', '')} ablate={ab}: {ms.value / max(1, n.value):.3f} ms per scan (pilot+merge+main)", flush=True)
 _lib.tune("sq8_mfma_ablate", 0)
 shards.close()
