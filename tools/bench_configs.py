@@ -3,8 +3,10 @@
 
   python tools/bench_configs.py [--only C2,C3,...] [--steps N]
 
-Prints one JSON line per (config, batch): QPS, ms per batch, the dominant kernel's mean duration
-(HIP events, osk_view_profile) and its algorithmic HBM rate.  Synthetic data from the device generator:
+Prints one JSON line per (config, batch): QPS, ms per batch, the scan's mean duration per batch
+(HIP events, osk_view_profile), the fp32-equivalent rate (rows × dim × 4 B per 256 queries ÷ that time:
+what an fp32 scan would have to stream, so it exceeds HBM peak on the int8 prefilter path) and, on the
+prefilter path, the rate of the bytes it actually reads (int8_prefilter_GBps).  Synthetic data from the device generator:
   C1  100k × 128 fp32 L2, 1 shard, k=10                      (the CPU plumbing config, run here on the GPU)
   C2  1M × 128 fp32 L2 (U[0,1)·128, SIFT-like), 1 shard       batch 1 and 256
   C3  10M × 768 fp32 COSINE, 8 shards                         batch 1 and 256
@@ -79,8 +81,15 @@ def run(view, queries, batch, steps, warmup, accept_ptrs=None, k=10):
 
 def emit(name, view, batch, ms_step, kernel_ms, bytes_per_launch, extra=None):
     rec = {"config": name, "batch": batch, "qps": batch / (ms_step * 1e-3), "ms_per_batch": ms_step,
-           "kernel_ms": kernel_ms, "kernel_algorithmic_GBps": bytes_per_launch / (kernel_ms * 1e-3) / 1e9,
+           "kernel_ms": kernel_ms, "fp32_equiv_GBps": bytes_per_launch / (kernel_ms * 1e-3) / 1e9,
            "rows": view.n_shards * view.rows, "dim": view.dim, "shards": view.n_shards}
+    rows = view.n_shards * view.rows
+    if view.enc == _lib.FLOAT32 and batch < 96 and not (extra or {}).get("selectivity"):
+        # the certified int8 prefilter's own bytes: int8 rows (16-B units) + 16-B bound terms, read
+        # once per launch of ≤ 8 (sq8_scan, batch 1) or ≤ 32 (sq8_mfma) queries
+        per = 8 if batch < 2 else 32
+        b8 = rows * (-(-view.dim // 16) * 16 + 16) * -(-batch // per)
+        rec["int8_prefilter_GBps"] = b8 / (kernel_ms * 1e-3) / 1e9
     if extra:
         rec.update(extra)
     print(json.dumps(rec), flush=True)
