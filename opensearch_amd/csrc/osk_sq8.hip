@@ -339,8 +339,8 @@ __device__ __forceinline__ int rs_base(int t) {
 // dots are reduce-scattered (rs_reduce) so each lane finishes the bound and quick test of P
 // (row, query) pairs instead of all NQ.
 // ------------------------------------------------------------------------------------------------
-template <int L, int V, int NQ, int U>
-__global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
+template <int L, int V, int NQ, int U, bool FQ = false>
+__global__ __launch_bounds__(kBlock, FQ ? 4 : 1) void sq8_scan(Sq8Params p) {
     constexpr int R = 64 / L;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int t = lane & (L - 1), g = lane / L;
@@ -542,7 +542,41 @@ __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
         }
     };
 
-    if (abits && !seg.ord_to_doc) {
+    if (FQ && abits && !seg.ord_to_doc) {
+        // filter pushdown, FQ instance: the accepted rows of successive sparse 64-row windows are
+        // queued across windows (lane l holds entry l: the row's offset from wb) and scanned 64 at a
+        // time, so a sparse filter does not pay one load round trip per window.  Its own instance:
+        // the queue costs 4 VGPRs, which would take the unfiltered kernel below 4 waves/SIMD.
+        int qpos = 0, qn = 0;
+        for (int64_t w0 = wb; w0 < we; w0 += 64) {
+            const int64_t word = w0 >> 6;
+            const int sh = (int)(w0 & 63);
+            uint64_t m = abits[word] >> sh;
+            if (sh && (word + 1) * 64 < we) m |= abits[word + 1] << (64 - sh);
+            if (we - w0 < 64) m &= (1ull << (we - w0)) - 1ull;
+            const int n = __popcll(m);
+            if (n == 0) continue;
+            const bool bit = (m >> lane) & 1ull;
+            const int below = __popcll(m & ((1ull << lane) - 1ull));
+            if (qn == 0 && n >= R * U) {   // a dense window with nothing queued: scan it in place
+                const int dst = bit ? below : n + (lane - below);
+                const int pos = __builtin_amdgcn_ds_permute(dst << 2, lane);
+                for (int i0 = 0; i0 < n; i0 += R * U) process(w0, true, i0, n, pos);
+                continue;
+            }
+            if (qn + n > 64) {
+                for (int i0 = 0; i0 < qn; i0 += R * U) process(wb, true, i0, qn, qpos);
+                qn = 0;
+            }
+            // append: set lanes to entries qn + below, the others to the remaining entries (a
+            // bijection mod 64); only entries [qn, qn + n) take the permuted value
+            const int dst = (bit ? qn + below : qn + n + (lane - below)) & 63;
+            const int v = __builtin_amdgcn_ds_permute(dst << 2, (int)(w0 - wb) + lane);
+            if (lane >= qn && lane < qn + n) qpos = v;
+            qn += n;
+        }
+        for (int i0 = 0; i0 < qn; i0 += R * U) process(wb, true, i0, qn, qpos);
+    } else if (abits && !seg.ord_to_doc) {
         // filter pushdown: accepted rows of 64 compacted to the front of the wave (see walk_rows)
         for (int64_t w0 = wb; w0 < we; w0 += 64) {
             const int64_t word = w0 >> 6;
@@ -600,12 +634,17 @@ using Sq8Fn = void (*)(Sq8Params);
 #define OSK_SQ8_ROW(L, V) {sq8_scan<L, V, 1, 4>, sq8_scan<L, V, 2, 4>, sq8_scan<L, V, 4, 4>, sq8_scan<L, V, 8, 2>}
 static const Sq8Fn kSq8[8][4] = {OSK_SQ8_ROW(4, 1),  OSK_SQ8_ROW(8, 1),  OSK_SQ8_ROW(16, 1), OSK_SQ8_ROW(16, 2),
                                  OSK_SQ8_ROW(16, 3), OSK_SQ8_ROW(16, 4), OSK_SQ8_ROW(32, 4), OSK_SQ8_ROW(64, 4)};
+// single-query filtered scans: the FQ instance (cross-window queue of accepted rows)
+static const Sq8Fn kSq8Filtered[8] = {sq8_scan<4, 1, 1, 4, true>,  sq8_scan<8, 1, 1, 4, true>,
+                                      sq8_scan<16, 1, 1, 4, true>, sq8_scan<16, 2, 1, 4, true>,
+                                      sq8_scan<16, 3, 1, 4, true>, sq8_scan<16, 4, 1, 4, true>,
+                                      sq8_scan<32, 4, 1, 4, true>, sq8_scan<64, 4, 1, 4, true>};
 
 hipError_t launch_sq8_scan(int nq, const Sq8Params& p, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
     const int slot = nq <= 1 ? 0 : nq <= 2 ? 1 : nq <= 4 ? 2 : 3;
     // NQ > 1: the queries and the 4 waves' per-query lists in LDS
     const size_t lds = slot == 0 ? 0 : (size_t)(1 << slot) * (p.units8 * 16 + 4 * kKQ * 12);
-    const auto fn = kSq8[sq8_cfg(p.units8)][slot];
+    const auto fn = (slot == 0 && p.accept) ? kSq8Filtered[sq8_cfg(p.units8)] : kSq8[sq8_cfg(p.units8)][slot];
     if (ev_start || ev_stop)
         hipExtLaunchKernelGGL(fn, dim3(p.n_tiles), dim3(kBlock), lds, s, ev_start, ev_stop, 0, p);
     else

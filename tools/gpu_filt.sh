@@ -6,3 +6,4 @@ run() { local secs=$1 log=$2; shift 2; echo "== $(date +%T) $*" | tee -a $OUT/st
 run 600 $OUT/pytest_gpu.log python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
 run 600 $OUT/filt.jsonl python -u tools/bench_configs.py --only C3,C5f
 cat $OUT/filt.jsonl
+run 600 $OUT/bench_default.log python bench.py
