@@ -247,7 +247,13 @@ struct osk_view {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;   // the current call's pair
     double scan_ms = 0.0;
     int64_t scan_calls = 0;
+    const uint64_t* h_accept_ptr = nullptr;   // source of osk_seg_search's one-pointer accept table copy
+    // cross-stream ordering of the workspace: the stream of the previous search, and an event recorded
+    // on it when a search arrives on another stream (order_after_last)
+    hipStream_t last_stream = nullptr;
+    hipEvent_t xs_event = nullptr;
     ~osk_view() {
+        if (xs_event) (void)hipEventDestroy(xs_event);
         for (int i = 0; i < kEvRing; ++i) {
             if (ev_start[i]) (void)hipEventDestroy(ev_start[i]);
             if (ev_stop[i]) (void)hipEventDestroy(ev_stop[i]);
@@ -1162,13 +1168,30 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     return OSK_OK;
 }
 
-// Core of osk_view_search_device (caller holds no lock; device already set).
+// Every search on a view reuses its workspace.  Calls are serialised by the view mutex on the host,
+// but a call on stream B could still overtake a call on stream A on the device, so a search whose
+// stream differs from the previous one first waits for everything enqueued on that stream so far
+// (an event recorded there now).  Same-stream calls — the common case — pay nothing.  A caller stream
+// must therefore stay valid until the next search on the view has been issued (osknn.h).
+int32_t order_after_last(osk_view* v, hipStream_t st) {
+    if (v->last_stream != nullptr && v->last_stream != st) {
+        if (!v->xs_event) OSK_HIP(hipEventCreateWithFlags(&v->xs_event, hipEventDisableTiming));
+        OSK_HIP(hipEventRecord(v->xs_event, v->last_stream));
+        OSK_HIP(hipStreamWaitEvent(st, v->xs_event, 0));
+    }
+    v->last_stream = st;
+    return OSK_OK;
+}
+
+// Core of osk_view_search_device (caller holds the view mutex; device already set).
 int32_t view_search_device(osk_view* v, const void* d_queries, int nq, int k,
                            const uint64_t* const* d_accept, uint64_t* d_shard_keys,
                            int32_t* d_shard_counts, int64_t* d_visited, hipStream_t st) {
     OSK_REQUIRE(nq >= 1, "n_queries must be >= 1");
     OSK_REQUIRE(k >= 1 && k <= OSK_MAX_K, "k must be in [1, OSK_MAX_K]");
     OSK_REQUIRE(d_queries && d_shard_keys && d_shard_counts, "null device buffer");
+    int32_t rc0 = order_after_last(v, st);
+    if (rc0) return rc0;
     static const int kLV[9][2] = {{4, 2}, {8, 2}, {8, 4}, {16, 4}, {16, 8}, {16, 12},
                                   {32, 8}, {64, 8}, {64, 16}};
     const int UP = kLV[v->cfg][0] * kLV[v->cfg][1];
@@ -1396,13 +1419,17 @@ int32_t osk_view_search(osk_view* v, const void* queries, int32_t n_queries, int
     if (rc) return rc;
     hipStream_t st = device_stream(v->device);
     std::lock_guard<std::mutex> lk(v->mu);
+    rc = order_after_last(v, st);
+    if (rc) return rc;
     const int nq = n_queries, S = v->n_shards, ns = (int)v->segs.size();
     const int64_t elem = v->enc == ENC_FLOAT32 ? 4 : 1;
     const size_t qbytes = (size_t)nq * v->dim * elem;
 
     // accept bitsets → device
     const uint64_t* const* d_acc = nullptr;
-    if (accept) {
+    bool any_bits = false;   // no leaf with a bitset = no filter (the unfiltered scan instances)
+    for (int i = 0; accept && i < ns; ++i) any_bits |= accept[i] != nullptr;
+    if (any_bits) {
         size_t words = 0;
         for (int i = 0; i < ns; ++i)
             if (accept[i]) words += (size_t)(v->segs[i]->max_doc + 63) / 64;
@@ -1483,6 +1510,8 @@ int32_t osk_seg_search(osk_seg* seg, const void* queries, int32_t n_queries, int
     (void)hipSetDevice(seg->device);
     hipStream_t st = device_stream(seg->device);
     std::lock_guard<std::mutex> lk(v->mu);
+    rc = order_after_last(v, st);
+    if (rc) return rc;
     const int nq = n_queries;
     const int64_t elem = seg->enc == ENC_FLOAT32 ? 4 : 1;
     const size_t qbytes = (size_t)nq * seg->dim * elem;
@@ -1492,8 +1521,9 @@ int32_t osk_seg_search(osk_seg* seg, const void* queries, int32_t n_queries, int
         OSK_HIP(v->ws_accept.reserve(std::max<size_t>(8, w * 8)));
         OSK_HIP(v->ws_accept_ptrs.reserve(sizeof(void*)));
         if (w) OSK_HIP(hipMemcpyAsync(v->ws_accept.p, accept_bits, w * 8, hipMemcpyHostToDevice, st));
-        const uint64_t* ptr = v->ws_accept.as<uint64_t>();
-        OSK_HIP(hipMemcpyAsync(v->ws_accept_ptrs.p, &ptr, sizeof(void*), hipMemcpyHostToDevice, st));
+        // the source of the async copy must outlive it: a view member (the call synchronises below)
+        v->h_accept_ptr = v->ws_accept.as<uint64_t>();
+        OSK_HIP(hipMemcpyAsync(v->ws_accept_ptrs.p, &v->h_accept_ptr, sizeof(void*), hipMemcpyHostToDevice, st));
         d_acc = v->ws_accept_ptrs.as<const uint64_t*>();
     }
     OSK_HIP(v->ws_qin.reserve(std::max<size_t>(16, qbytes)));

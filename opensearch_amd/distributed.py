@@ -125,7 +125,8 @@ class LocalShards:
         self.view = C.c_void_p()
         check(lib().osk_view_create(arr, len(self.segs), ptr(seg_shard), ptr(seg_base), len(self.segs),
                                     ptr(sidx), C.byref(self.view)))
-        # global shardIndex of every gathered slot: rank r's slot j ↔ owned_shards(r)[j] (pads → −1)
+        # global shardIndex of every gathered slot: rank r's slot j ↔ owned_shards(r)[j]; pad slots (a rank
+        # owning fewer shards) get INT32_MAX — their lists are all-zero keys, so they never contribute a hit
         gi = []
         for r in range(world):
             own = owned_shards(r, n_shards, world)

@@ -340,3 +340,49 @@ def test_merge_device_ranked_matches_host_reduce(world, sl, k, from_, size, ties
             assert torch.equal(w.view(torch.int32), g.view(torch.int32)), (w, g)
         else:
             assert torch.equal(w, g), (w, g)
+
+
+def test_merge_device_reference_known_answers():
+    """The reference's own merge known answers fed straight into the device coordinator reduce
+    (osk_merge_device): SearchPhaseControllerTests.testReduceTopNWithFromOffset (:1347-1392),
+    FetchSearchPhaseTests.testFetchTwoDocument (:124-218) and the constant-score shardIndex/doc
+    tie order of testSortDocsIsIdempotent (:255-298); tests/golden/merge_known_answers.json."""
+    import json
+    from pathlib import Path
+    import torch
+    cases = json.loads((Path(__file__).parent / "golden" / "merge_known_answers.json").read_text())
+    for case in cases:
+        shards = case["shards"]
+        S = len(shards)
+        k = max([len(s["scores"]) for s in shards] + [1])
+        keys = np.zeros((1, S, k), np.uint64)
+        counts = np.zeros((1, S), np.int32)
+        for j, s in enumerate(shards):
+            c = len(s["scores"])
+            counts[0, j] = c
+            sc = np.asarray(s["scores"], np.float32).view(np.uint32).astype(np.uint64)
+            sortable = np.where(sc & 0x80000000, (~sc) & 0xFFFFFFFF, sc | 0x80000000)
+            keys[0, j, :c] = (sortable << np.uint64(32)) | (np.uint64(0xFFFFFFFF) - np.asarray(s["docs"], np.uint64))
+        si = np.asarray([s["shard_index"] for s in shards], np.int32)
+        size = case["size"]
+        d_keys = torch.from_numpy(keys.view(np.int64)).cuda()
+        d_counts = torch.from_numpy(counts).cuda()
+        d_si = torch.from_numpy(si).cuda()
+        o_s = torch.empty((1, size), dtype=torch.float32, device="cuda")
+        o_d = torch.empty((1, size), dtype=torch.int32, device="cuda")
+        o_sh = torch.empty((1, size), dtype=torch.int32, device="cuda")
+        o_c = torch.empty(1, dtype=torch.int32, device="cuda")
+        o_t = torch.empty(1, dtype=torch.int64, device="cuda")
+        o_m = torch.empty(1, dtype=torch.float32, device="cuda")
+        _lib.check(_lib.lib().osk_merge_device(0, d_keys.data_ptr(), d_counts.data_ptr(), d_si.data_ptr(), 1, S, k,
+                                               case["from"], size, o_s.data_ptr(), o_d.data_ptr(), o_sh.data_ptr(),
+                                               o_c.data_ptr(), o_t.data_ptr(), o_m.data_ptr(), None))
+        torch.cuda.synchronize()
+        n = int(o_c.item())
+        if "expected_scores" in case:
+            assert o_s[0, :n].cpu().tolist() == case["expected_scores"], (case["name"], o_s)
+        if "expected_docs" in case:
+            assert o_d[0, :n].cpu().tolist() == case["expected_docs"], (case["name"], o_d)
+            assert o_sh[0, :n].cpu().tolist() == case["expected_shards"], (case["name"], o_sh)
+        assert int(o_t.item()) == case["expected_total_hits"]
+        assert float(o_m.item()) == case["expected_max_score"]
