@@ -12,7 +12,8 @@ rank s·N/8, so the total corpus is fixed and each GPU scans 10M/N rows ("strong
 
 One step = one batch of B queries (default 1: the single-query path the north star targets) through
 the whole hot path with inputs resident in HBM: per-shard exact scan + top-k on every GPU, per-shard
-merge, RCCL all-gather of the per-shard top-k lists, device coordinator merge (TopDocs.merge).
+merge, RCCL all-gather of the per-shard top-k lists, device coordinator merge (TopDocs.merge) — one
+C-ABI call per rank (osk_shards_search_merge_device; libosknn owns the RCCL communicator).
 value = queries answered by the whole job per second.
 
 Path: batches below 16 take the certified int8 prefilter (sq8_scan over an int8 copy of the rows,
@@ -104,8 +105,13 @@ def main():
     ap.add_argument("--rows-per-shard", type=int, default=ROWS_PER_SHARD)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sq8", action="store_true", help="measure the fp32 streaming scan as the main path")
+    ap.add_argument("--exchange", choices=["osk", "torch"], default="osk",
+                    help="osk: the C-ABI step osk_shards_search_merge_device (RCCL all-gather inside libosknn; "
+                         "torch.distributed/gloo only carries the communicator id and the timing barriers); "
+                         "torch: torch.distributed.all_gather_into_tensor + osk_merge_device_ranked")
     ap.add_argument("--dist-backend", default="nccl",
-                    help="nccl (= RCCL over xGMI, one GPU per rank); gloo only to rehearse N > 1 ranks on one GPU")
+                    help="--exchange torch only: nccl (= RCCL over xGMI, one GPU per rank); gloo to rehearse "
+                         "N > 1 ranks on one GPU")
     ap.add_argument("--dump", default="", help="rank 0 writes the merged results of batches 0..7 to this .npz "
                     "(cross-N parity: the N-rank result must equal the 1-GPU result)")
     ap.add_argument("--mfma-min-batch", type=int, default=0,
@@ -125,14 +131,14 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
-    if a.dist_backend == "gloo":   # rehearsal: several ranks may share the box's one GPU
+    if a.dist_backend == "gloo" and a.exchange == "torch":   # rehearsal: several ranks may share one GPU
         local_rank %= torch.cuda.device_count()
     torch.cuda.set_device(local_rank)
     if world > 1:
-        if a.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if a.exchange == "osk" or a.dist_backend == "gloo":
+            dist.init_process_group("gloo")   # host-side coordination only (id broadcast, barriers, max)
         else:
-            dist.init_process_group(a.dist_backend)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     if a.tiles:
         _lib.tune("tiles_target", a.tiles)
@@ -155,16 +161,25 @@ def main():
     B = a.batch
     keys = torch.empty((B, shards.s_pad, K), dtype=torch.int64, device="cuda")
     counts = torch.empty((B, shards.s_pad), dtype=torch.int32, device="cuda")
-    xchg = D.ShardExchange(world, shards.s_pad, B, K, FROM, SIZE, shards.global_shard_index, device=local_rank)
     # One explicit stream for the library calls and torch's own ops (gather copy, events): the null
     # stream's handle is 0, which the C-ABI reads as "the library's own (non-blocking) stream".
     torch.cuda.set_stream(torch.cuda.Stream())
     stream = torch.cuda.current_stream().cuda_stream
+    comm = None
+    if a.exchange == "osk":
+        # libosknn's own RCCL communicator (world 1: no collective runs, the local lists are the image)
+        comm = (D.DeviceComm.from_process_group(local_rank) if world > 1
+                else D.DeviceComm.init_rank(local_rank, 0, 1, D.DeviceComm.unique_id()))
+        xstep = D.ShardSearchMerge(comm, shards.view, shards.s_pad, B, K, FROM, SIZE, device=local_rank)
+    else:
+        xchg = D.ShardExchange(world, shards.s_pad, B, K, FROM, SIZE, shards.global_shard_index, device=local_rank)
 
     def step(i):
         q = qpool[(i % n_pool) * B:(i % n_pool + 1) * B]
+        if comm is not None:   # scan + ONE RCCL all-gather of the per-shard top-k + device TopDocs.merge
+            return xstep(q.data_ptr(), stream)
         shards.search(q.data_ptr(), B, K, keys, counts, stream)
-        return xchg(keys, stream)   # one all-gather of the per-shard top-k + device TopDocs.merge
+        return xchg(keys, stream)   # torch all-gather of the per-shard top-k + device TopDocs.merge
 
     def timed(steps, warmup, offset=0):
         """W untimed steps, then K steps between barrier + synchronize; returns the max-over-ranks wall
@@ -195,9 +210,9 @@ def main():
         scan_ms, calls = C.c_double(), C.c_int64()
         _lib.check(_lib.lib().osk_view_scan_time(shards.view, C.byref(scan_ms), C.byref(calls)))
         _lib.check(_lib.lib().osk_view_profile(shards.view, 0))
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64)
         if world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)   # max over ranks (host tensor: gloo or nccl)
         return float(t.item()), scan_ms.value / max(1, calls.value), ev0.elapsed_time(ev1), out
 
     def counter(name):
@@ -301,7 +316,10 @@ def main():
             "config": {"workload": "C3 Cohere-shaped exact k-NN: 10M×768 fp32 COSINE, 8 shards, k=10, from=0, size=10",
                        "batch": B, "rows": N_SHARDS * a.rows_per_shard, "dim": DIM, "shards": N_SHARDS,
                        "path": "prefilter" if prefilter else "mfma" if batched else "fp32_stream",
-                       "parallelism": f"shards over {world} GPU(s), RCCL all-gather + device merge"},
+                       "parallelism": (f"8 shards over {world} GPU(s); " + (
+                           ("one C-ABI step per rank: scan + libosknn RCCL all-gather + device merge" if world > 1
+                            else "one GPU: scan + device merge, no collective")
+                           if a.exchange == "osk" else f"torch.distributed {a.dist_backend} all-gather + device merge"))},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kernel_name, "scan_ms_avg": scan_avg_ms,
@@ -315,6 +333,8 @@ def main():
             res["cpu_baseline"] = cpu_baseline(a.cpu_sample_rows, a.cpu_queries, threads)
         print(json.dumps(res), flush=True)
     shards.close()
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -8,6 +8,11 @@
  * A Java caller maps a negative code to an IOException, which OpenSearch turns into a shard
  * failure (S/search/query/QueryPhase.java:307-309) — the library never brings the node down.
  *
+ * Concurrency: calls on one view (or segment) are serialised by its mutex, and a search whose stream
+ * differs from the previous search's first waits for the work already enqueued on that stream (the
+ * view's workspace is reused), so a caller stream must stay valid until the next search on the view
+ * has been issued, or the view released.
+ *
  * Citation convention: `S/` = /root/reference/server/src/main/java/org/opensearch/ ;
  * [L] = behaviour of the un-vendored lucene-core 10.3.0 jar (gradle/libs.versions.toml:3) whose
  * interface is evidenced by the reference call site given next to it.
@@ -48,7 +53,7 @@
 extern "C" {
 #endif
 
-#define OSK_ABI_VERSION 1
+#define OSK_ABI_VERSION 2
 #define OSK_MAX_K       64   /* largest k (and from+size) the device path serves in this build */
 #define OSK_MAX_DIM     4096
 
@@ -102,7 +107,23 @@ int32_t osk_seg_stage_device(int32_t device, const void* d_rows, int64_t src_pit
 int32_t osk_seg_synth(int32_t device, int64_t n_rows, int32_t dim, int32_t encoding,
                       int32_t similarity, uint64_t seed, int32_t dist, int64_t row0,
                       osk_seg** out);
+/* Segments are reference counted: the stage/synth call returns one reference, every view created over
+ * the segment holds another (so a segment merged away or closed under a live view stays valid until
+ * the view is released).  osk_seg_retain adds a reference; osk_seg_release drops one and frees the
+ * HBM copy at zero. */
 int32_t osk_seg_release(osk_seg* seg);
+int32_t osk_seg_retain(osk_seg* seg);
+/* HBM bytes the segment owns now: rows, norms, doc map and every derived copy built so far. */
+int32_t osk_seg_footprint(const osk_seg* seg, int64_t* hbm_bytes);
+/* Build derived copies ahead of the first search that needs them (the warmer's job,
+ * S/index/engine/InternalEngine.java:2409-2432, S/index/IndexWarmer.java:132-135).  Float32 segments
+ * get the prefilter copy at staging; the other two are built here or, if never warmed, by the first
+ * search that takes their path.  No-op for byte fields. */
+#define OSK_WARM_PREFILTER      1   /* int8 copy + 16-B bound terms per row (¼ + 16 B of the rows)      */
+#define OSK_WARM_PREFILTER_MFMA 2   /* its 16-row tiled twin read by the batched int8 MFMA prefilter    */
+#define OSK_WARM_BATCHED        4   /* bf16 hi/lo split copy of the batched bf16×3 MFMA path (= rows)   */
+#define OSK_WARM_ALL            7
+int32_t osk_seg_warm(osk_seg* seg, int32_t what);
 int32_t osk_seg_info(const osk_seg* seg, int64_t* n_rows, int32_t* dim, int32_t* encoding,
                      int32_t* similarity, int32_t* max_doc, int32_t* device);
 
@@ -133,6 +154,8 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
                         const int32_t* seg_doc_base, int32_t n_shards,
                         const int32_t* shard_index, osk_view** out);
 int32_t osk_view_release(osk_view* view);
+/* osk_seg_warm of every segment plus the view's own tables for those paths. */
+int32_t osk_view_warm(osk_view* view, int32_t what);
 
 /* Per-shard exact top-k on the device, asynchronous on `stream` (NULL = the library's stream for
  * the device). All buffers are DEVICE pointers:
@@ -177,7 +200,8 @@ int32_t osk_merge_device_ranked(int32_t device, const uint64_t* d_keys, int32_t 
 int32_t osk_view_profile(osk_view* view, int32_t enable);
 int32_t osk_view_scan_time(osk_view* view, double* total_ms, int64_t* calls);
 
-/* Process-wide tuning knobs for benchmarks / A-B runs:
+/* Process-wide tuning knobs (atomic; a search reads each knob once, and every setting returns the same
+ * exact results — only speed changes):
  *   "scan_nt"         0|1 non-temporal corpus loads in the streaming scan (default 1)
  *   "tiles_target"    workgroup tiles per view for the scans (default 0 = whole rounds of the chip's
  *                     resident slots; at view create)
@@ -195,8 +219,9 @@ int32_t osk_view_scan_time(osk_view* view, double* total_ms, int64_t* calls);
  *                     default 2; 0 = always the VALU sq8_scan)
  *   "sq8_mfma_queries"  16 | 32 queries per sq8_mfma launch (default 32)
  *   "sq8_mfma_nt"     0|1 non-temporal row loads in sq8_mfma (default 1)
- *   "sq8_mfma_ablate" A/B timing only, results wrong: 1 skip sq8_mfma's epilogue, 2 its MFMAs
- *   "sq8_force_fallback"  tests: every tile of a prefiltered search is re-scanned exactly */
+ * The testing build (libosknn_testing.so) also accepts "sq8_mfma_ablate", "mfma_ablate" (A/B timing,
+ * results wrong), "sq8_force_fallback" (every prefilter list re-scanned exactly) and "settle_trace";
+ * the shipped library returns OSK_ERR_UNSUPPORTED for them. */
 int32_t osk_tune_set(const char* key, int64_t value);
 
 /* Batched-path counters of a view: searches that took the MFMA path, and queries among them whose
@@ -207,9 +232,9 @@ int32_t osk_view_stats(osk_view* view, int64_t* batched_calls, int64_t* fallback
  * list overflowed past the certificate and the tile was re-scanned exactly), "sq8_exact_tiles"
  * (such tiles), "sq8_rescored_rows" (rows re-scored exactly, all calls). */
 int32_t osk_view_counter(osk_view* view, const char* name, int64_t* value);
-/* Tests / debugging only: copy `bytes` of an internal buffer of the view's last search
- * ("akeys", "cand_a", "flags", "qsplit", "qnorm", "sq8cand",
- * "sq8lb", "qc") to host memory. */
+/* Testing build only (the shipped library returns OSK_ERR_UNSUPPORTED): copy `bytes` of an internal
+ * buffer of the view's last search ("akeys", "cand_a", "flags", "qsplit", "qnorm", "sq8cand", "sq8lb",
+ * "qc", "settle_trace") to host memory. */
 int32_t osk_view_debug_copy(osk_view* view, const char* name, void* host, int64_t bytes);
 
 /* Host-buffer convenience: shard search + coordinator merge on one device, synchronous.
@@ -252,6 +277,48 @@ int32_t osk_topdocs_write(int64_t total_hits, int32_t relation, float max_score,
 int32_t osk_topdocs_read(const uint8_t* buf, int64_t len, int64_t* total_hits, int32_t* relation,
                          float* max_score, int32_t cap_hits, int32_t* n, int32_t* docs, float* scores,
                          int64_t* consumed);
+
+/* ---- multi-GPU (one node): shards ↔ GPUs, ONE RCCL all-gather of per-shard top-k, device merge ----
+ * Replaces the coordinator's shard fan-out and reduce for shards that live on this node's GPUs:
+ * S/action/search/AbstractSearchAsyncAction.java:262-268 (one request per shard copy, loop index =
+ * shardIndex), S/action/search/SearchPhaseController.java:224-253 (mergeTopDocs → [L] TopDocs.merge
+ * over the shards' results, setShardIndex) and :839-901 (TopDocsStats).  RCCL (librccl.so.1) is
+ * loaded at first use; without it these entry points return OSK_ERR_UNSUPPORTED. */
+#define OSK_COMM_ID_BYTES 128
+typedef struct osk_comm osk_comm;
+
+/* A fresh communicator id: call on ONE rank and hand the bytes to every rank out of band. */
+int32_t osk_comm_unique_id(uint8_t* id /* OSK_COMM_ID_BYTES */);
+/* One process per GPU: this process's rank of `world` on `device` (ncclCommInitRank; blocks until
+ * every rank has joined). */
+int32_t osk_comm_init_rank(int32_t device, int32_t rank, int32_t world, const uint8_t* id, osk_comm** out);
+/* One process driving several GPUs (a JVM owning the node's GPUs): local device i is rank i. */
+int32_t osk_comm_init_all(const int32_t* devices, int32_t n, osk_comm** out);
+int32_t osk_comm_release(osk_comm* comm);
+int32_t osk_comm_info(const osk_comm* comm, int32_t* rank, int32_t* world, int32_t* n_local);
+/* Raw all-gather of `bytes` per rank (device buffers; one-device-per-process communicators). */
+int32_t osk_comm_all_gather(osk_comm* comm, const void* d_send, void* d_recv, int64_t bytes, void* stream);
+
+/* The whole multi-GPU query, host buffers, synchronous: every local view (views[i] on the
+ * communicator's local device i) scans its shards, the per-shard top-k lists of every rank are
+ * all-gathered once, and the coordinator reduce (from, size) runs on the device.  Every rank gets the
+ * merged result.  shardIndex of a hit = the shard_index its view was created with (use the global
+ * rank of the shard in sorted ShardId order).  accept: NULL or one host bitset pointer per segment
+ * of every view, view 0's segments first.  All ranks must hold the same number of shards per rank
+ * (the largest view's), or use the device entry below. */
+int32_t osk_shards_search_merge(osk_comm* comm, osk_view* const* views, int32_t n_views, const void* queries,
+                                int32_t n_queries, int32_t k, const uint64_t* const* accept, int32_t from,
+                                int32_t size, float* out_scores, int32_t* out_docs, int32_t* out_shard_index,
+                                int32_t* out_count, int64_t* out_total_hits, float* out_max_score);
+/* The same for one GPU per process with device buffers, asynchronous on `stream`: d_queries
+ * n_queries × dim on the view's device, d_accept as osk_view_search_device, shards_per_rank the
+ * (common) number of list slots per rank (≥ the view's shards; slots past them are empty), outputs as
+ * osk_merge_device. */
+int32_t osk_shards_search_merge_device(osk_comm* comm, osk_view* view, const void* d_queries, int32_t n_queries,
+                                       int32_t k, const uint64_t* const* d_accept, int32_t shards_per_rank,
+                                       int32_t from, int32_t size, float* d_scores, int32_t* d_docs,
+                                       int32_t* d_shard_out, int32_t* d_count, int64_t* d_total_hits,
+                                       float* d_max_score, void* stream);
 
 #ifdef __cplusplus
 }

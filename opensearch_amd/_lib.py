@@ -6,11 +6,15 @@ there is no CPU fallback for the search path.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
+import os
 import threading
 from pathlib import Path
 
 LIB_PATH = Path(__file__).resolve().with_name("libosknn.so")
+# same ABI plus the test/A-B-only knobs (osknn.h): loaded only inside `with testing():`
+TESTING_LIB_PATH = Path(__file__).resolve().with_name("libosknn_testing.so")
 
 OSK_OK = 0
 OSK_ERR_INVALID = -1
@@ -20,6 +24,12 @@ OSK_ERR_UNSUPPORTED = -4
 OSK_ERR_NO_DEVICE = -5
 OSK_MAX_K = 64
 OSK_MAX_DIM = 4096
+OSK_COMM_ID_BYTES = 128
+
+OSK_WARM_PREFILTER = 1
+OSK_WARM_PREFILTER_MFMA = 2
+OSK_WARM_BATCHED = 4
+OSK_WARM_ALL = 7
 
 FLOAT32 = 0
 BYTE = 1
@@ -52,6 +62,19 @@ SIGNATURES = {
     "osk_seg_stage_device": (_I32, [_I32, _P, _I64, _I64, _I32, _I32, _I32, _P, _I32, C.POINTER(_P)]),
     "osk_seg_synth": (_I32, [_I32, _I64, _I32, _I32, _I32, _U64, _I32, _I64, C.POINTER(_P)]),
     "osk_seg_release": (_I32, [_P]),
+    "osk_seg_retain": (_I32, [_P]),
+    "osk_seg_footprint": (_I32, [_P, _PI64]),
+    "osk_seg_warm": (_I32, [_P, _I32]),
+    "osk_view_warm": (_I32, [_P, _I32]),
+    "osk_comm_unique_id": (_I32, [_P]),
+    "osk_comm_init_rank": (_I32, [_I32, _I32, _I32, _P, C.POINTER(_P)]),
+    "osk_comm_init_all": (_I32, [_P, _I32, C.POINTER(_P)]),
+    "osk_comm_release": (_I32, [_P]),
+    "osk_comm_info": (_I32, [_P, _PI32, _PI32, _PI32]),
+    "osk_comm_all_gather": (_I32, [_P, _P, _P, _I64, _P]),
+    "osk_shards_search_merge": (_I32, [_P, _P, _I32, _P, _I32, _I32, _P, _I32, _I32, _P, _P, _P, _P, _P, _P]),
+    "osk_shards_search_merge_device": (_I32, [_P, _P, _P, _I32, _I32, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P,
+                                              _P]),
     "osk_seg_info": (_I32, [_P, _PI64, _PI32, _PI32, _PI32, _PI32, _PI32]),
     "osk_synth_host": (_I32, [_P, _I64, _I64, _I32, _U64, _I32]),
     "osk_seg_search": (_I32, [_P, _P, _I32, _I32, _P, _P, _P, _P, _P]),
@@ -84,25 +107,52 @@ class OskError(RuntimeError):
 
 _lock = threading.Lock()
 _lib = None
+_product = None
+_testing = None
+
+
+def _load(path: Path) -> C.CDLL:
+    if not path.exists():
+        raise RuntimeError(
+            f"{path} is missing: build it with `python -m opensearch_amd.build` "
+            "(libosknn has no CPU fallback)")
+    L = C.CDLL(str(path))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    return L
 
 
 def lib() -> C.CDLL:
-    global _lib
+    """The library every call goes through: libosknn.so, or libosknn_testing.so inside `testing()`."""
+    global _lib, _product
     if _lib is not None:
         return _lib
     with _lock:
         if _lib is None:
-            if not LIB_PATH.exists():
-                raise RuntimeError(
-                    f"{LIB_PATH} is missing: build it with `python -m opensearch_amd.build` "
-                    "(libosknn has no CPU fallback)")
-            L = C.CDLL(str(LIB_PATH))
-            for name, (res, args) in SIGNATURES.items():
-                fn = getattr(L, name)
-                fn.restype = res
-                fn.argtypes = args
-            _lib = L
+            # tools that drive the A/B knobs (tools/mfma_ablate.py, settle_trace.py) set OSK_TESTING_LIB=1
+            path = TESTING_LIB_PATH if os.environ.get("OSK_TESTING_LIB") == "1" else LIB_PATH
+            _product = _product or _load(path)
+            _lib = _product
     return _lib
+
+
+@contextlib.contextmanager
+def testing():
+    """Route every call to libosknn_testing.so (same ABI plus the test-only knobs: sq8_force_fallback,
+    the A/B ablations, settle traces, workspace debug copies).  Objects made inside must be used and
+    released inside: the two libraries share no state."""
+    global _lib, _testing
+    lib()
+    with _lock:
+        _testing = _testing or _load(TESTING_LIB_PATH)
+        prev, _lib = _lib, _testing
+    try:
+        yield _testing
+    finally:
+        with _lock:
+            _lib = prev
 
 
 def check(rc: int) -> None:

@@ -3,8 +3,11 @@
     python -m opensearch_amd.build          # build if sources are newer than the .so
     python -m opensearch_amd.build --force  # always rebuild
 
-The library lands at opensearch_amd/libosknn.so (git-ignored, shipped to the GPU box by gpurun).
-Objects are compiled in parallel into build/osknn/ and linked once.
+The product library lands at opensearch_amd/libosknn.so (git-ignored, shipped to the GPU box by
+gpurun).  A second library, opensearch_amd/libosknn_testing.so, links the same objects except the C-ABI
+translation unit, which is compiled with -DOSK_TESTING: it adds the result-corrupting A/B and test
+knobs (ablations, forced exact fallback, settle traces, workspace debug copies) that the shipped
+library refuses.  Objects are compiled in parallel into build/osknn/.
 """
 from __future__ import annotations
 
@@ -20,10 +23,12 @@ ROOT = PKG.parent
 CSRC = PKG / "csrc"
 INCLUDE = ROOT / "include"
 LIB = PKG / "libosknn.so"
+LIB_TESTING = PKG / "libosknn_testing.so"
+TESTING_VARIANT = "osk_api.hip"   # the only source whose object differs in the testing build
 OBJDIR = ROOT / "build" / "osknn"
 
-SOURCES = ["osk_kernels.hip", "osk_mfma.hip", "osk_sq8.hip", "osk_api.hip", "osk_host.cpp"]
-HEADERS = ["osk_common.h", "osk_internal.h", "osk_wave.h"]
+SOURCES = ["osk_kernels.hip", "osk_mfma.hip", "osk_sq8.hip", "osk_api.hip", "osk_comm.hip", "osk_host.cpp"]
+HEADERS = ["osk_common.h", "osk_internal.h", "osk_wave.h", "osk_objects.h"]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
@@ -34,17 +39,18 @@ COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unus
 
 
 def _stale() -> bool:
-    if not LIB.exists():
+    if not LIB.exists() or not LIB_TESTING.exists():
         return True
-    t = LIB.stat().st_mtime
+    t = min(LIB.stat().st_mtime, LIB_TESTING.stat().st_mtime)
     deps = [CSRC / s for s in SOURCES + HEADERS] + [INCLUDE / "osknn.h", Path(__file__)]
     return any(d.stat().st_mtime > t for d in deps)
 
 
-def _compile(src: str) -> Path:
+def _compile(job) -> Path:
+    src, testing = job
     OBJDIR.mkdir(parents=True, exist_ok=True)
-    obj = OBJDIR / (src + ".o")
-    cmd = [HIPCC] + COMMON
+    obj = OBJDIR / (src + (".testing" if testing else "") + ".o")
+    cmd = [HIPCC] + COMMON + (["-DOSK_TESTING"] if testing else [])
     if src.endswith(".hip"):
         cmd += [f"--offload-arch={ARCH}", "-x", "hip"]
     cmd += ["-c", str(CSRC / src), "-o", str(obj)]
@@ -57,16 +63,19 @@ def _compile(src: str) -> Path:
 def build(force: bool = False, verbose: bool = True) -> Path:
     if not force and not _stale():
         return LIB
-    with cf.ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
-        objs = list(ex.map(_compile, SOURCES))
-    tmp = LIB.with_suffix(".so.tmp")
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp)] + [str(o) for o in objs]
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-        raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-    os.replace(tmp, LIB)
-    if verbose:
-        print(f"built {LIB}", file=sys.stderr)
+    jobs = [(s, False) for s in SOURCES] + [(TESTING_VARIANT, True)]
+    with cf.ThreadPoolExecutor(max_workers=len(jobs)) as ex:
+        objs = dict(zip(jobs, ex.map(_compile, jobs)))
+    for lib, testing in ((LIB, False), (LIB_TESTING, True)):
+        parts = [objs[(s, testing and s == TESTING_VARIANT)] for s in SOURCES]
+        tmp = lib.with_suffix(".so.tmp")
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp)] + [str(o) for o in parts]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, lib)
+        if verbose:
+            print(f"built {lib}", file=sys.stderr)
     return LIB
 
 

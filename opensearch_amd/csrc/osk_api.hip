@@ -1,13 +1,6 @@
-// osk_api.hip — the C-ABI of libosknn.so (declared in include/osknn.h).
-//
-// Object model:
-//   osk_seg   one segment's vector field in HBM (rows padded to 16-byte units, optional row norms,
-//             optional ord→doc map).  Staged once, released by osk_seg_release — the lifetime of a
-//             Lucene KnnVectorsReader ([L] KnnVectorsFormat.fieldsReader … close()).
-//   osk_view  the segments of one or more shards on one device plus the scan's tile table and a
-//             workspace.  A shard's exact top-k = per-leaf exact top-k merged by (score, doc)
-//             ([L] AbstractKnnVectorQuery.rewrite, driven from
-//             S/search/internal/ContextIndexSearcher.java:203-218).
+// osk_api.hip — the C-ABI of libosknn.so (declared in include/osknn.h): segments, views, the
+// single-device search paths and the coordinator merge.  The object model (osk_seg, osk_view) is in
+// osk_objects.h; the multi-GPU exchange (osk_comm, RCCL) in osk_comm.hip.
 // Every entry point catches all C++ exceptions and returns an error code (see osknn.h).
 #include <hip/hip_runtime.h>
 #include <algorithm>
@@ -19,57 +12,21 @@
 #include <string>
 #include <vector>
 
-#include "../../include/osknn.h"
-#include "osk_internal.h"
+#include "osk_objects.h"
 
 using namespace osk;
 
-namespace osk {
-void set_error(const std::string& msg);
-void clear_error();
-}  // namespace osk
-
-#define OSK_HIP(call)                                                                          \
-    do {                                                                                       \
-        hipError_t e_ = (call);                                                                \
-        if (e_ != hipSuccess) {                                                                \
-            set_error(std::string(#call) + ": " + hipGetErrorString(e_));                      \
-            return OSK_ERR_DEVICE;                                                             \
-        }                                                                                      \
-    } while (0)
-
-#define OSK_REQUIRE(cond, msg)                                                                 \
-    do {                                                                                       \
-        if (!(cond)) {                                                                         \
-            set_error(msg);                                                                    \
-            return OSK_ERR_INVALID;                                                            \
-        }                                                                                      \
-    } while (0)
-
-#define OSK_GUARD_BEGIN try {
-#define OSK_GUARD_END                                                                          \
-    }                                                                                          \
-    catch (const std::bad_alloc&) {                                                            \
-        set_error("host allocation failed");                                                   \
-        return OSK_ERR_OOM;                                                                    \
-    }                                                                                          \
-    catch (const std::exception& ex) {                                                         \
-        set_error(ex.what());                                                                  \
-        return OSK_ERR_INVALID;                                                                \
-    }                                                                                          \
-    catch (...) {                                                                              \
-        set_error("unknown exception");                                                        \
-        return OSK_ERR_INVALID;                                                                \
-    }
-
 namespace {
+std::mutex g_dev_mu;
+std::vector<hipStream_t> g_streams;
+int g_ndev = -1;
+}  // namespace
+
+namespace osk {
 
 // ------------------------------------------------------------------------------------------------
 // devices and streams
 // ------------------------------------------------------------------------------------------------
-std::mutex g_dev_mu;
-std::vector<hipStream_t> g_streams;
-int g_ndev = -1;
 
 int device_count_cached() {
     std::lock_guard<std::mutex> lk(g_dev_mu);
@@ -126,143 +83,9 @@ hipStream_t device_stream(int device) {
     return g_streams[device];
 }
 
-// device buffer that grows on demand (never inside a timed/captured call once warmed)
-struct DevBuf {
-    void* p = nullptr;
-    size_t cap = 0;
-    ~DevBuf() {
-        if (p) (void)hipFree(p);
-    }
-    hipError_t reserve(size_t bytes) {
-        if (bytes <= cap) return hipSuccess;
-        if (p) {
-            (void)hipFree(p);
-            p = nullptr;
-            cap = 0;
-        }
-        hipError_t e = hipMalloc(&p, bytes);
-        if (e == hipSuccess) cap = bytes;
-        return e;
-    }
-    template <class T> T* as() const { return static_cast<T*>(p); }
-};
-
-struct HostPinned {
-    void* p = nullptr;
-    size_t cap = 0;
-    ~HostPinned() {
-        if (p) (void)hipHostFree(p);
-    }
-    hipError_t reserve(size_t bytes) {
-        if (bytes <= cap) return hipSuccess;
-        if (p) {
-            (void)hipHostFree(p);
-            p = nullptr;
-            cap = 0;
-        }
-        hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
-        if (e == hipSuccess) cap = bytes;
-        return e;
-    }
-};
-
-int units_for(int dim, int enc) { return enc == ENC_FLOAT32 ? (dim + 3) / 4 : (dim + 15) / 16; }
-
-}  // namespace
-
-// ------------------------------------------------------------------------------------------------
-// objects
-// ------------------------------------------------------------------------------------------------
-struct osk_seg {
-    int device = 0;
-    int64_t n_rows = 0;
-    int dim = 0, enc = 0, sim = 0, max_doc = 0;
-    int units = 0, cfg = 0;
-    void* d_rows = nullptr;
-    float* d_xnorm_f = nullptr;
-    int32_t* d_xnorm_i = nullptr;
-    int32_t* d_ord_to_doc = nullptr;
-    // batched MFMA path (built on first batched search): bf16 hi/lo copy in MFMA fragment order,
-    // |x|² per row (device lane order) and max |x|² of the segment
-    void* d_split = nullptr;
-    int split_KS = 0;
-    unsigned* d_maxnorm2 = nullptr;
-    float* d_xsqrt = nullptr;          // |x| per row (MFMA path)
-    float h_maxnorm2 = 0.0f;
-    // certified int8 prefilter (built on first prefiltered search): int8 rows + per-row bound terms
-    void* d_q8 = nullptr;
-    float4* d_q8aux = nullptr;
-    void* d_q8t = nullptr;    // the int8 rows in sq8_mfma's tiled layout (built on first batched prefilter)
-    int units8 = 0;
-    std::mutex mu;
-    osk_view* self_view = nullptr;   // single-segment view behind osk_seg_search
-    ~osk_seg();
-};
-
-struct osk_view {
-    int device = 0, dim = 0, enc = 0, sim = 0, units = 0, cfg = 0;
-    std::vector<osk_seg*> segs;
-    std::vector<int32_t> seg_shard, seg_doc_base;
-    int n_shards = 0;
-    std::vector<int32_t> shard_index;
-    std::vector<int32_t> shard_tile_begin;
-    int n_tiles = 0;
-    DevBuf d_segs, d_tiles, d_shard_tile_begin, d_shard_index;
-    // workspace
-    DevBuf ws_cand, ws_q, ws_qnorm, ws_qin, ws_keys, ws_counts, ws_accept_ptrs, ws_accept,
-        ws_out, ws_visited;
-    HostPinned h_stage;
-    // batched MFMA path
-    bool mfma_ready = false;
-    int n_munits = 0;
-    int mfma_KS = 0;
-    double mfma_c = 0.0;
-    DevBuf d_munits, d_seg_split, d_seg_xsqrt, d_seg_vrow, d_shard_unit_begin, d_shard_maxnorm2;
-    DevBuf ws_qsplit, ws_cand_a, ws_akeys, ws_acounts, ws_pkeys, ws_pcounts, ws_flags, ws_fbq, ws_fbkeys, ws_fbcounts;
-    HostPinned h_flags;
-    int64_t mfma_calls = 0, mfma_fallback_queries = 0;
-    // certified int8 prefilter
-    bool sq8_ready = false;
-    int units8 = 0;
-    float sq8_gam = 0.f, sq8_g2 = 0.f, sq8_cos_slack = 0.f;
-    DevBuf d_sq8_rows, d_sq8_aux, d_counters;   // counters: SettleParams::counters
-    DevBuf d_sq8_rows_t;                         // per segment: tiled int8 copy (sq8_mfma)
-    bool sq8t_ready = false;
-    DevBuf ws_q8, ws_qc, ws_sq8cand, ws_sq8lb, ws_lbmax, ws_trace;
-    // settle slices: kSliceLists wave lists each, never spanning shards (an empty shard gets one
-    // empty slice so that its result is still written)
-    int n_slices = 0;
-    DevBuf d_slices, d_shard_slice_begin, ws_part;
-    DevBuf ws_pilot, ws_thr, ws_thr_counts;   // int8 MFMA prefilter: pilot keys, per-(query, shard) floors
-    int64_t sq8_calls = 0;
-    std::mutex mu;
-    // scan-kernel timing (osk_view_profile): a ring of (start, stop) event pairs, one per search call,
-    // folded into scan_ms when a slot is reused (kEvRing calls later: long complete, no host wait) or
-    // when the total is read — timing never blocks the host inside the timed loop
-    static constexpr int kEvRing = 64;
-    bool profile = false;
-    hipEvent_t ev_start[kEvRing] = {}, ev_stop[kEvRing] = {};
-    bool ev_pending[kEvRing] = {};
-    int64_t ev_next = 0;                  // calls started since enabling
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;   // the current call's pair
-    double scan_ms = 0.0;
-    int64_t scan_calls = 0;
-    const uint64_t* h_accept_ptr = nullptr;   // source of osk_seg_search's one-pointer accept table copy
-    // cross-stream ordering of the workspace: the stream of the previous search, and an event recorded
-    // on it when a search arrives on another stream (order_after_last)
-    hipStream_t last_stream = nullptr;
-    hipEvent_t xs_event = nullptr;
-    ~osk_view() {
-        if (xs_event) (void)hipEventDestroy(xs_event);
-        for (int i = 0; i < kEvRing; ++i) {
-            if (ev_start[i]) (void)hipEventDestroy(ev_start[i]);
-            if (ev_stop[i]) (void)hipEventDestroy(ev_stop[i]);
-        }
-    }
-};
 
 // The device view of a view's segments (pointers re-read: staging may add row norms later).
-static std::vector<SegDev> seg_devs(const osk_view* v) {
+std::vector<SegDev> seg_devs(const osk_view* v) {
     std::vector<SegDev> sd(v->segs.size());
     for (size_t i = 0; i < v->segs.size(); ++i) {
         const osk_seg* s = v->segs[i];
@@ -272,8 +95,10 @@ static std::vector<SegDev> seg_devs(const osk_view* v) {
     return sd;
 }
 
+}  // namespace osk
+
 osk_seg::~osk_seg() {
-    if (self_view) delete self_view;
+    if (self_view) delete self_view;   // holds no reference on this segment
     if (d_rows) (void)hipFree(d_rows);
     if (d_xnorm_f) (void)hipFree(d_xnorm_f);
     if (d_xnorm_i) (void)hipFree(d_xnorm_i);
@@ -286,7 +111,43 @@ osk_seg::~osk_seg() {
     if (d_q8t) (void)hipFree(d_q8t);
 }
 
+int64_t osk_seg::hbm_bytes() const {
+    const int64_t n = std::max<int64_t>(1, n_rows);
+    int64_t b = n * units * 16;
+    if (d_xnorm_f) b += n * 4;
+    if (d_xnorm_i) b += n * 4;
+    if (d_ord_to_doc) b += n * 4;
+    if (d_split) b += std::max<int64_t>(1, (n_rows + 127) / 128) * 8 * split_KS * 2 * 1024 + n * 4 + 4;
+    if (d_q8) b += n * units8 * 16 + n * 16;
+    if (d_q8t) b += std::max<int64_t>(1, (n_rows + 15) / 16) * sq8_mfma_ks(units8) * 1024;
+    return b;
+}
+
+osk_view::~osk_view() {
+    if (xs_event) (void)hipEventDestroy(xs_event);
+    for (int i = 0; i < kEvRing; ++i) {
+        if (ev_start[i]) (void)hipEventDestroy(ev_start[i]);
+        if (ev_stop[i]) (void)hipEventDestroy(ev_stop[i]);
+    }
+    if (holds_refs)
+        for (osk_seg* s : segs) osk::seg_unref(s);
+}
+
+void osk::seg_unref(osk_seg* s) {
+    if (s && s->refs.fetch_sub(1) == 1) {
+        (void)hipSetDevice(s->device);
+        delete s;
+    }
+}
+
 namespace {
+
+int32_t ensure_sq8_seg(osk_seg* s, hipStream_t st);
+int32_t ensure_sq8t_seg(osk_seg* s, hipStream_t st);
+int32_t ensure_split(osk_seg* s, hipStream_t st);
+int32_t ensure_sq8(osk_view* v, hipStream_t st);
+int32_t ensure_sq8t(osk_view* v, hipStream_t st);
+int32_t ensure_mfma(osk_view* v, hipStream_t st);
 
 int32_t seg_finish(osk_seg* s, const int32_t* ord_to_doc, hipStream_t st) {
     // row norms
@@ -315,6 +176,10 @@ int32_t seg_finish(osk_seg* s, const int32_t* ord_to_doc, hipStream_t st) {
                                hipMemcpyHostToDevice, st));
     }
     OSK_HIP(hipStreamSynchronize(st));
+    // the certified int8 prefilter copy is the default path of float32 searches: built with the segment
+    // (staging = the reader's constructor / warmer, S/index/engine/InternalEngine.java:2409-2432), so
+    // no search pays for it and the segment's HBM footprint is known at staging
+    if (s->enc == ENC_FLOAT32) return ensure_sq8_seg(s, st);
     return OSK_OK;
 }
 
@@ -360,54 +225,41 @@ int32_t osk_tune_set(const char* key, int64_t value) {
     OSK_GUARD_BEGIN
     OSK_REQUIRE(key != nullptr, "key is null");
     const std::string k(key);
-    if (k == "scan_nt") g_tuning.scan_nt = value != 0;
-    else if (k == "mfma_min_batch") {
-        OSK_REQUIRE(value >= 0, "mfma_min_batch must be >= 0");
-        g_tuning.mfma_min_batch = (int)value;
-    } else if (k == "mfma_ablate") {
-        g_tuning.mfma_ablate = (int)value;
-    } else if (k == "mfma_units") {
-        OSK_REQUIRE(value >= 1 && value <= 32768, "mfma_units out of range");
-        g_tuning.mfma_units = (int)value;
-    } else if (k == "sq8") {
-        g_tuning.sq8 = value != 0;
-    } else if (k == "sq8_force_fallback") {
-        g_tuning.sq8_force_fallback = value != 0;
-    } else if (k == "settle_trace") {
-        g_tuning.settle_trace = value != 0;
-    } else if (k == "tiles_target") {
-        OSK_REQUIRE(value >= 0 && value <= (1 << 22), "tiles_target out of range");
-        g_tuning.tiles_target = (int)value;
-    } else if (k == "sq8_mfma_ablate") {
-        g_tuning.sq8_mfma_ablate = (int)value;
-    } else if (k == "sq8_mfma_queries") {
-        OSK_REQUIRE(value == 16 || value == 32, "sq8_mfma_queries must be 16 or 32");
-        g_tuning.sq8_mfma_queries = (int)value;
-    } else if (k == "sq8_cost_pct") {
-        OSK_REQUIRE(value >= 0 && value <= 100000, "sq8_cost_pct out of range");
-        g_tuning.sq8_cost_pct = (int)value;
-    } else if (k == "sq8_mfma_nt") {
-        g_tuning.sq8_mfma_nt = value != 0;
-    } else if (k == "sq8_mfma_min") {
-        OSK_REQUIRE(value >= 0 && value <= (1 << 20), "sq8_mfma_min out of range");
-        g_tuning.sq8_mfma_min = (int)value;
-    } else if (k == "tile_slots_per_cu") {
-        OSK_REQUIRE(value >= 1 && value <= 64, "tile_slots_per_cu out of range");
-        g_tuning.tile_slots_per_cu = (int)value;
-    } else if (k == "tile_max_rounds") {
-        OSK_REQUIRE(value >= 1 && value <= 1024, "tile_max_rounds out of range");
-        g_tuning.tile_max_rounds = (int)value;
-    } else if (k == "tile_large_slots") {
-        OSK_REQUIRE(value >= 0 && value <= 1024, "tile_large_slots out of range");
-        g_tuning.tile_large_slots = (int)value;
-    } else if (k == "tile_min_rows") {
-        OSK_REQUIRE(value >= 1 && value <= (1 << 24), "tile_min_rows out of range");
-        g_tuning.tile_min_rows = (int)value;
-    } else {
-        set_error("unknown tuning key: " + k);
-        return OSK_ERR_INVALID;
+    struct Knob { const char* name; std::atomic<int>* v; int64_t lo, hi; bool testing; };
+    const Knob knobs[] = {
+        {"scan_nt", &g_tuning.scan_nt, 0, 1, false},
+        {"tiles_target", &g_tuning.tiles_target, 0, 1 << 22, false},
+        {"tile_slots_per_cu", &g_tuning.tile_slots_per_cu, 1, 64, false},
+        {"tile_max_rounds", &g_tuning.tile_max_rounds, 1, 1024, false},
+        {"tile_large_slots", &g_tuning.tile_large_slots, 0, 1024, false},
+        {"tile_min_rows", &g_tuning.tile_min_rows, 1, 1 << 24, false},
+        {"mfma_min_batch", &g_tuning.mfma_min_batch, 0, 1 << 30, false},
+        {"sq8_cost_pct", &g_tuning.sq8_cost_pct, 0, 100000, false},
+        {"mfma_units", &g_tuning.mfma_units, 1, 32768, false},
+        {"sq8", &g_tuning.sq8, 0, 1, false},
+        {"sq8_mfma_nt", &g_tuning.sq8_mfma_nt, 0, 1, false},
+        {"sq8_mfma_queries", &g_tuning.sq8_mfma_queries, 16, 32, false},
+        {"sq8_mfma_min", &g_tuning.sq8_mfma_min, 0, 1 << 20, false},
+        {"sq8_mfma_ablate", &g_tuning.sq8_mfma_ablate, 0, 3, true},
+        {"sq8_force_fallback", &g_tuning.sq8_force_fallback, 0, 1, true},
+        {"settle_trace", &g_tuning.settle_trace, 0, 1, true},
+        {"mfma_ablate", &g_tuning.mfma_ablate, 0, 31, true},
+    };
+    for (const Knob& kn : knobs) {
+        if (k != kn.name) continue;
+#ifndef OSK_TESTING
+        if (kn.testing) {
+            set_error("tuning key " + k + " exists only in the testing build (libosknn_testing.so)");
+            return OSK_ERR_UNSUPPORTED;
+        }
+#endif
+        OSK_REQUIRE(value >= kn.lo && value <= kn.hi, "tuning value out of range for " + k);
+        if (k == "sq8_mfma_queries") OSK_REQUIRE(value == 16 || value == 32, "sq8_mfma_queries must be 16 or 32");
+        kn.v->store((int)value);
+        return OSK_OK;
     }
-    return OSK_OK;
+    set_error("unknown tuning key: " + k);
+    return OSK_ERR_INVALID;
     OSK_GUARD_END
 }
 
@@ -493,8 +345,45 @@ int32_t osk_seg_synth(int32_t device, int64_t n_rows, int32_t dim, int32_t encod
 int32_t osk_seg_release(osk_seg* seg) {
     OSK_GUARD_BEGIN
     if (!seg) return OSK_OK;
-    (void)hipSetDevice(seg->device);
-    delete seg;
+    seg_unref(seg);   // freed when no view holds it any more
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_seg_retain(osk_seg* seg) {
+    OSK_GUARD_BEGIN
+    OSK_REQUIRE(seg != nullptr, "seg is null");
+    seg->refs.fetch_add(1);
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_seg_footprint(const osk_seg* seg, int64_t* hbm_bytes) {
+    OSK_GUARD_BEGIN
+    OSK_REQUIRE(seg != nullptr && hbm_bytes != nullptr, "null argument");
+    *hbm_bytes = seg->hbm_bytes();
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_seg_warm(osk_seg* seg, int32_t what) {
+    OSK_GUARD_BEGIN
+    clear_error();
+    OSK_REQUIRE(seg != nullptr, "seg is null");
+    OSK_REQUIRE((what & ~OSK_WARM_ALL) == 0, "unknown warm flags");
+    int32_t rc = check_device(seg->device);
+    if (rc) return rc;
+    if (seg->enc != ENC_FLOAT32) return OSK_OK;   // byte fields scan their rows directly
+    hipStream_t st = device_stream(seg->device);
+    if (what & (OSK_WARM_PREFILTER | OSK_WARM_PREFILTER_MFMA)) {
+        rc = ensure_sq8_seg(seg, st);
+        if (rc) return rc;
+    }
+    if ((what & OSK_WARM_PREFILTER_MFMA) && sq8_mfma_supported((seg->dim + 15) / 16)) {
+        rc = ensure_sq8t_seg(seg, st);
+        if (rc) return rc;
+    }
+    if (what & OSK_WARM_BATCHED) return ensure_split(seg, st);
     return OSK_OK;
     OSK_GUARD_END
 }
@@ -557,14 +446,14 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
     const int R = 64 / kL[v->cfg];
     int64_t total = 0;
     for (int i = 0; i < n_segs; ++i) total += segs[i]->n_rows;
-    const int64_t min_rows = std::max<int64_t>(4LL * R * 8, g_tuning.tile_min_rows);
+    const int64_t min_rows = std::max<int64_t>(4LL * R * 8, (int)g_tuning.tile_min_rows);
     int64_t target = g_tuning.tiles_target;
     if (target <= 0) {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s0->device) != hipSuccess || cus <= 0)
             cus = 256;
-        const int64_t slots = (int64_t)cus * std::max(1, g_tuning.tile_slots_per_cu);
-        const int64_t rounds = std::min<int64_t>(std::max(1, g_tuning.tile_max_rounds),
+        const int64_t slots = (int64_t)cus * std::max(1, (int)g_tuning.tile_slots_per_cu);
+        const int64_t rounds = std::min<int64_t>(std::max(1, (int)g_tuning.tile_max_rounds),
                                                  std::max<int64_t>(1, total / (slots * min_rows)));
         target = rounds * slots;
         // large views: whole rounds of BOTH scan kernels' residency.  sq8_scan holds 4 workgroups per
@@ -645,7 +534,37 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
     OSK_HIP(hipMemcpyAsync(v->d_shard_index.p, v->shard_index.data(), sizeof(int32_t) * n_shards,
                            hipMemcpyHostToDevice, st));
     OSK_HIP(hipStreamSynchronize(st));
+    for (osk_seg* sg : v->segs) sg->refs.fetch_add(1);   // released by ~osk_view
     *out = v.release();
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_view_warm(osk_view* view, int32_t what) {
+    OSK_GUARD_BEGIN
+    clear_error();
+    OSK_REQUIRE(view != nullptr, "view is null");
+    OSK_REQUIRE((what & ~OSK_WARM_ALL) == 0, "unknown warm flags");
+    for (osk_seg* s : view->segs) {
+        int32_t rc = osk_seg_warm(s, what);
+        if (rc) return rc;
+    }
+    if (view->enc != ENC_FLOAT32 || view->n_tiles == 0) return OSK_OK;
+    int32_t rc = check_device(view->device);
+    if (rc) return rc;
+    hipStream_t st = device_stream(view->device);
+    std::lock_guard<std::mutex> lk(view->mu);
+    rc = order_after_last(view, st);
+    if (rc) return rc;
+    if (what & (OSK_WARM_PREFILTER | OSK_WARM_PREFILTER_MFMA)) {
+        rc = ensure_sq8(view, st);
+        if (rc) return rc;
+    }
+    if ((what & OSK_WARM_PREFILTER_MFMA) && sq8_mfma_supported((view->dim + 15) / 16)) {
+        rc = ensure_sq8t(view, st);
+        if (rc) return rc;
+    }
+    if (what & OSK_WARM_BATCHED) return ensure_mfma(view, st);
     return OSK_OK;
     OSK_GUARD_END
 }
@@ -790,7 +709,7 @@ int32_t ensure_mfma(osk_view* v, hipStream_t st) {
         const std::vector<SegDev> sd = seg_devs(v);
         OSK_HIP(hipMemcpyAsync(v->d_segs.p, sd.data(), sizeof(SegDev) * sd.size(), hipMemcpyHostToDevice, st));
     }
-    const int64_t target = std::max(1, g_tuning.mfma_units);
+    const int64_t target = std::max(1, (int)g_tuning.mfma_units);
     const int64_t per = std::max<int64_t>(1, (total_tiles + target - 1) / target);
     std::vector<MfmaUnit> units;
     std::vector<int32_t> shard_list_begin(v->n_shards + 1, 0);
@@ -1092,7 +1011,7 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     // batches of ≥ sq8_mfma_min queries: the int8 MFMA scan, 16 queries per launch; else the VALU
     // scan, ≤ 8 per launch
     const bool use_mfma = g_tuning.sq8_mfma_min > 0 && nq >= g_tuning.sq8_mfma_min && sq8_mfma_supported(u8);
-    const int chunk = use_mfma ? g_tuning.sq8_mfma_queries : kMaxNQ;
+    const int chunk = use_mfma ? (int)g_tuning.sq8_mfma_queries : kMaxNQ;
     if (use_mfma) {
         rc = ensure_sq8t(v, st);
         if (rc) return rc;
@@ -1168,6 +1087,10 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     return OSK_OK;
 }
 
+}  // namespace
+
+namespace osk {
+
 // Every search on a view reuses its workspace.  Calls are serialised by the view mutex on the host,
 // but a call on stream B could still overtake a call on stream A on the device, so a search whose
 // stream differs from the previous one first waits for everything enqueued on that stream so far
@@ -1239,7 +1162,7 @@ int32_t view_search_device(osk_view* v, const void* d_queries, int nq, int k,
     return OSK_OK;
 }
 
-}  // namespace
+}  // namespace osk
 
 extern "C" {
 
@@ -1334,6 +1257,11 @@ int32_t osk_view_profile(osk_view* v, int32_t enable) {
 // Test/debug only: copy an internal workspace buffer of the last search to host memory.
 int32_t osk_view_debug_copy(osk_view* v, const char* name, void* host, int64_t bytes) {
     OSK_GUARD_BEGIN
+#ifndef OSK_TESTING
+    (void)v; (void)name; (void)host; (void)bytes;
+    set_error("osk_view_debug_copy exists only in the testing build (libosknn_testing.so)");
+    return OSK_ERR_UNSUPPORTED;
+#else
     OSK_REQUIRE(v && name && host && bytes >= 0, "null argument");
     int32_t rc = check_device(v->device);
     if (rc) return rc;
@@ -1346,8 +1274,10 @@ int32_t osk_view_debug_copy(osk_view* v, const char* name, void* host, int64_t b
                     : nullptr;
     OSK_REQUIRE(b != nullptr, "unknown buffer");
     OSK_REQUIRE((size_t)bytes <= b->cap, "bytes exceed the buffer");
+    OSK_HIP(hipDeviceSynchronize());   // the last search may be on any stream
     OSK_HIP(hipMemcpy(host, b->p, bytes, hipMemcpyDeviceToHost));
     return OSK_OK;
+#endif
     OSK_GUARD_END
 }
 
@@ -1504,6 +1434,9 @@ int32_t osk_seg_search(osk_seg* seg, const void* queries, int32_t n_queries, int
             osk_seg* one[1] = {seg};
             rc = osk_view_create(one, 1, nullptr, nullptr, 1, nullptr, &seg->self_view);
             if (rc) return rc;
+            // owned by the segment: it must not keep the segment alive
+            seg->self_view->holds_refs = false;
+            seg->refs.fetch_sub(1);
         }
         v = seg->self_view;
     }

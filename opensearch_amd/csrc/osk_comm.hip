@@ -1,0 +1,456 @@
+// osk_comm.hip — the multi-GPU exchange of libosknn: one index shard per GPU, ONE RCCL all-gather of
+// every GPU's per-shard top-k lists over xGMI, and the coordinator reduce on the device.
+//
+// Reference semantics mirrored:
+//   * shards are OpenSearch's partitioning (S/cluster/metadata/IndexMetadata.java:265-268); the
+//     coordinator fans a query out to one copy of every shard (S/action/search/
+//     AbstractSearchAsyncAction.java:262-268) whose loop index is the shardIndex
+//     (S/cluster/routing/GroupShardsIterator.java:59-62);
+//   * the per-shard results are reduced by SearchPhaseController.mergeTopDocs → [L] TopDocs.merge
+//     (S/action/search/SearchPhaseController.java:224-246, setShardIndex :248-253): score desc, then
+//     shardIndex asc, then doc asc, cut to from+size; TopDocsStats (:839-901) for total hits and max
+//     score.
+// Design: each GPU scans its shards in one launch and writes per-shard lists of 8-byte
+// hit keys [nq][shards_per_rank][k] (key 0 = empty); one ncclAllGather moves them to every GPU
+// (8·k·nq bytes per shard: latency-bound, µs next to a ms scan); merge_coord then runs straight over
+// the gathered rank-major image.  A list's hit count is its number of non-zero keys, so counts are not
+// exchanged.  The shardIndex of every gathered slot is exchanged once per (communicator, view).
+//
+// RCCL is loaded at run time (dlopen of librccl.so.1, preferring a copy the process already loaded,
+// e.g. PyTorch's), so the library itself has no link-time dependency on it and every other entry point
+// works where RCCL is absent; the communicator entry points then fail with OSK_ERR_UNSUPPORTED.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "osk_objects.h"
+
+using namespace osk;
+
+struct osk_comm {
+    uint64_t id = 0;                     // process-unique, never reused (views cache per-comm state by it)
+    int rank = 0, world = 1;             // rank of local device 0, communicator size
+    std::vector<int> devices;            // local devices: 1 (one process per GPU) or all (one process)
+    std::vector<ncclComm_t> comms;       // one per local device
+    std::mutex mu;                       // one collective sequence at a time
+};
+
+namespace {
+
+std::atomic<uint64_t> g_comm_ids{0};
+
+struct Rccl {
+    ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+std::once_flag g_rccl_once;
+Rccl g_rccl;
+bool g_rccl_ok = false;
+std::string g_rccl_err;
+
+void load_rccl() {
+    // a copy already in the process first (RTLD_NOLOAD), then the system one
+    void* h = nullptr;
+    for (const char* name : {"librccl.so.1", "librccl.so"})
+        if (!h) h = dlopen(name, RTLD_NOW | RTLD_LOCAL | RTLD_NOLOAD);
+    for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+        if (!h) h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+        const char* e = dlerror();
+        g_rccl_err = std::string("RCCL (librccl.so.1) could not be loaded: ") + (e ? e : "unknown error");
+        return;
+    }
+    auto sym = [&](const char* n) { return dlsym(h, n); };
+    g_rccl.GetUniqueId = reinterpret_cast<decltype(g_rccl.GetUniqueId)>(sym("ncclGetUniqueId"));
+    g_rccl.CommInitRank = reinterpret_cast<decltype(g_rccl.CommInitRank)>(sym("ncclCommInitRank"));
+    g_rccl.CommInitAll = reinterpret_cast<decltype(g_rccl.CommInitAll)>(sym("ncclCommInitAll"));
+    g_rccl.CommDestroy = reinterpret_cast<decltype(g_rccl.CommDestroy)>(sym("ncclCommDestroy"));
+    g_rccl.AllGather = reinterpret_cast<decltype(g_rccl.AllGather)>(sym("ncclAllGather"));
+    g_rccl.GroupStart = reinterpret_cast<decltype(g_rccl.GroupStart)>(sym("ncclGroupStart"));
+    g_rccl.GroupEnd = reinterpret_cast<decltype(g_rccl.GroupEnd)>(sym("ncclGroupEnd"));
+    g_rccl.GetErrorString = reinterpret_cast<decltype(g_rccl.GetErrorString)>(sym("ncclGetErrorString"));
+    if (!g_rccl.GetUniqueId || !g_rccl.CommInitRank || !g_rccl.CommInitAll || !g_rccl.CommDestroy ||
+        !g_rccl.AllGather || !g_rccl.GroupStart || !g_rccl.GroupEnd || !g_rccl.GetErrorString) {
+        g_rccl_err = "librccl is missing an nccl* entry point";
+        return;
+    }
+    g_rccl_ok = true;
+}
+
+const Rccl* rccl() {
+    std::call_once(g_rccl_once, load_rccl);
+    if (!g_rccl_ok) {
+        set_error(g_rccl_err);
+        return nullptr;
+    }
+    return &g_rccl;
+}
+
+#define OSK_NCCL(call)                                                                         \
+    do {                                                                                       \
+        ncclResult_t r_ = (call);                                                              \
+        if (r_ != ncclSuccess) {                                                               \
+            set_error(std::string(#call) + ": " + g_rccl.GetErrorString(r_));                  \
+            return OSK_ERR_DEVICE;                                                             \
+        }                                                                                      \
+    } while (0)
+
+// The per-shard lists of one view, padded to `spr` shards per rank: ws_xkeys [nq][spr][k].
+int32_t search_padded(osk_view* v, const void* d_queries, int nq, int k, const uint64_t* const* d_accept, int spr,
+                      hipStream_t st) {
+    const size_t per = (size_t)nq * spr * k;
+    OSK_HIP(v->ws_xkeys.reserve(sizeof(uint64_t) * per));
+    OSK_HIP(v->ws_counts.reserve(sizeof(int32_t) * (size_t)nq * v->n_shards));
+    uint64_t* xk = v->ws_xkeys.as<uint64_t>();
+    if (v->n_shards == spr)
+        return view_search_device(v, d_queries, nq, k, d_accept, xk, v->ws_counts.as<int32_t>(), nullptr, st);
+    OSK_HIP(v->ws_keys.reserve(sizeof(uint64_t) * (size_t)nq * v->n_shards * k));
+    int32_t rc = view_search_device(v, d_queries, nq, k, d_accept, v->ws_keys.as<uint64_t>(),
+                                    v->ws_counts.as<int32_t>(), nullptr, st);
+    if (rc) return rc;
+    // rows of n_shards·k keys → rows of spr·k keys, the pad slots zero (empty lists)
+    OSK_HIP(hipMemsetAsync(xk, 0, sizeof(uint64_t) * per, st));
+    OSK_HIP(hipMemcpy2DAsync(xk, sizeof(uint64_t) * spr * k, v->ws_keys.p, sizeof(uint64_t) * v->n_shards * k,
+                             sizeof(uint64_t) * v->n_shards * k, nq, hipMemcpyDeviceToDevice, st));
+    return OSK_OK;
+}
+
+// The shardIndex of every gathered slot (rank r's slot j ↔ its view's shard_index[j]; pads INT32_MAX),
+// exchanged once per (comm, spr) and kept in every local view's d_xsi.
+int32_t exchange_shard_index(osk_comm* c, osk_view* const* views, int spr, const hipStream_t* sts) {
+    bool fresh = true;
+    for (size_t i = 0; i < c->devices.size(); ++i)
+        fresh &= views[i]->xsi_comm == c->id && views[i]->xsi_spr == spr;
+    if (fresh) return OSK_OK;
+    const Rccl* R = &g_rccl;
+    for (size_t i = 0; i < c->devices.size(); ++i) {
+        osk_view* v = views[i];
+        OSK_HIP(hipSetDevice(v->device));
+        std::vector<int32_t> mine(spr, 0x7FFFFFFF);
+        for (int j = 0; j < v->n_shards; ++j) mine[j] = v->shard_index[j];
+        OSK_HIP(v->d_xsi.reserve(sizeof(int32_t) * (size_t)spr * (c->world + 1)));
+        int32_t* own = v->d_xsi.as<int32_t>() + (size_t)spr * c->world;   // the local part, after the image
+        OSK_HIP(hipMemcpyAsync(own, mine.data(), sizeof(int32_t) * spr, hipMemcpyHostToDevice, sts[i]));
+        OSK_HIP(hipStreamSynchronize(sts[i]));
+    }
+    OSK_NCCL(R->GroupStart());
+    for (size_t i = 0; i < c->devices.size(); ++i) {
+        osk_view* v = views[i];
+        int32_t* own = v->d_xsi.as<int32_t>() + (size_t)spr * c->world;
+        OSK_NCCL(R->AllGather(own, v->d_xsi.p, (size_t)spr, ncclInt32, c->comms[i], sts[i]));
+    }
+    OSK_NCCL(R->GroupEnd());
+    for (size_t i = 0; i < c->devices.size(); ++i) {
+        OSK_HIP(hipSetDevice(views[i]->device));
+        OSK_HIP(hipStreamSynchronize(sts[i]));
+        views[i]->xsi_comm = c->id;
+        views[i]->xsi_spr = spr;
+    }
+    return OSK_OK;
+}
+
+// One all-gather of every local view's ws_xkeys into its ws_xgath (grouped over local devices).
+int32_t gather_keys(osk_comm* c, osk_view* const* views, int nq, int k, int spr, const hipStream_t* sts) {
+    const size_t per = (size_t)nq * spr * k;
+    for (size_t i = 0; i < c->devices.size(); ++i) {
+        OSK_HIP(hipSetDevice(views[i]->device));
+        OSK_HIP(views[i]->ws_xgath.reserve(sizeof(uint64_t) * per * c->world));
+    }
+    OSK_NCCL(g_rccl.GroupStart());
+    for (size_t i = 0; i < c->devices.size(); ++i)
+        OSK_NCCL(g_rccl.AllGather(views[i]->ws_xkeys.p, views[i]->ws_xgath.p, per, ncclUint64, c->comms[i], sts[i]));
+    OSK_NCCL(g_rccl.GroupEnd());
+    return OSK_OK;
+}
+
+int32_t check_merge_args(const osk_comm* c, int nq, int k, int from, int size, int spr) {
+    OSK_REQUIRE(nq >= 1, "n_queries must be >= 1");
+    OSK_REQUIRE(k >= 1 && k <= OSK_MAX_K, "k must be in [1, OSK_MAX_K]");
+    OSK_REQUIRE(from >= 0 && size >= 1 && (int64_t)from + size <= 100000, "bad from/size");
+    OSK_REQUIRE(spr >= 1, "shards_per_rank must be >= 1");
+    OSK_REQUIRE((int64_t)c->world * spr * std::min(k, from + size) <= 4096,
+                "world * shards_per_rank * min(k, from+size) exceeds 4096 hits per query");
+    return OSK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t osk_comm_unique_id(uint8_t* id) {
+    OSK_GUARD_BEGIN
+    clear_error();
+    OSK_REQUIRE(id != nullptr, "id is null");
+    if (device_count_cached() <= 0) {   // RCCL needs a device even to make an id
+        set_error("no HIP device visible (libosknn has no CPU fallback)");
+        return OSK_ERR_NO_DEVICE;
+    }
+    const Rccl* R = rccl();
+    if (!R) return OSK_ERR_UNSUPPORTED;
+    ncclUniqueId u;
+    OSK_NCCL(R->GetUniqueId(&u));
+    static_assert(sizeof(u) == OSK_COMM_ID_BYTES, "ncclUniqueId size");
+    std::memcpy(id, &u, sizeof(u));
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_comm_init_rank(int32_t device, int32_t rank, int32_t world, const uint8_t* id, osk_comm** out) {
+    OSK_GUARD_BEGIN
+    clear_error();
+    OSK_REQUIRE(out != nullptr && id != nullptr, "null argument");
+    OSK_REQUIRE(world >= 1 && rank >= 0 && rank < world, "need 0 <= rank < world");
+    int32_t rc = check_device(device);
+    if (rc) return rc;
+    const Rccl* R = rccl();
+    if (!R) return OSK_ERR_UNSUPPORTED;
+    auto c = std::make_unique<osk_comm>();
+    c->id = ++g_comm_ids;
+    c->rank = rank;
+    c->world = world;
+    c->devices = {device};
+    c->comms.assign(1, nullptr);
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    OSK_NCCL(R->CommInitRank(&c->comms[0], world, u, rank));
+    *out = c.release();
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_comm_init_all(const int32_t* devices, int32_t n, osk_comm** out) {
+    OSK_GUARD_BEGIN
+    clear_error();
+    OSK_REQUIRE(out != nullptr && devices != nullptr && n >= 1, "null argument");
+    for (int i = 0; i < n; ++i) {
+        int32_t rc = check_device(devices[i]);
+        if (rc) return rc;
+        for (int j = 0; j < i; ++j) OSK_REQUIRE(devices[j] != devices[i], "duplicate device");
+    }
+    const Rccl* R = rccl();
+    if (!R) return OSK_ERR_UNSUPPORTED;
+    auto c = std::make_unique<osk_comm>();
+    c->id = ++g_comm_ids;
+    c->rank = 0;
+    c->world = n;
+    c->devices.assign(devices, devices + n);
+    c->comms.assign(n, nullptr);
+    OSK_NCCL(R->CommInitAll(c->comms.data(), n, devices));
+    *out = c.release();
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_comm_release(osk_comm* comm) {
+    OSK_GUARD_BEGIN
+    if (!comm) return OSK_OK;
+    for (size_t i = 0; i < comm->comms.size(); ++i)
+        if (comm->comms[i]) {
+            (void)hipSetDevice(comm->devices[i]);
+            (void)g_rccl.CommDestroy(comm->comms[i]);
+        }
+    delete comm;
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_comm_info(const osk_comm* comm, int32_t* rank, int32_t* world, int32_t* n_local) {
+    OSK_GUARD_BEGIN
+    OSK_REQUIRE(comm != nullptr, "comm is null");
+    if (rank) *rank = comm->rank;
+    if (world) *world = comm->world;
+    if (n_local) *n_local = (int32_t)comm->devices.size();
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_comm_all_gather(osk_comm* comm, const void* d_send, void* d_recv, int64_t bytes, void* stream) {
+    OSK_GUARD_BEGIN
+    clear_error();
+    OSK_REQUIRE(comm != nullptr && d_send && d_recv && bytes >= 0, "null argument");
+    OSK_REQUIRE(comm->devices.size() == 1, "osk_comm_all_gather needs a one-device-per-process communicator");
+    int32_t rc = check_device(comm->devices[0]);
+    if (rc) return rc;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : device_stream(comm->devices[0]);
+    std::lock_guard<std::mutex> lk(comm->mu);
+    OSK_NCCL(g_rccl.AllGather(d_send, d_recv, (size_t)bytes, ncclUint8, comm->comms[0], st));
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_shards_search_merge_device(osk_comm* comm, osk_view* view, const void* d_queries, int32_t n_queries,
+                                       int32_t k, const uint64_t* const* d_accept, int32_t shards_per_rank,
+                                       int32_t from, int32_t size, float* d_scores, int32_t* d_docs,
+                                       int32_t* d_shard_out, int32_t* d_count, int64_t* d_total_hits,
+                                       float* d_max_score, void* stream) {
+    OSK_GUARD_BEGIN
+    clear_error();
+    OSK_REQUIRE(comm != nullptr && view != nullptr && d_queries != nullptr, "null argument");
+    OSK_REQUIRE(d_scores && d_docs && d_shard_out && d_count && d_total_hits && d_max_score, "null output");
+    OSK_REQUIRE(comm->devices.size() == 1, "the device entry serves one-device-per-process communicators");
+    OSK_REQUIRE(view->device == comm->devices[0], "the view is not on the communicator's device");
+    OSK_REQUIRE(view->n_shards <= shards_per_rank, "the view holds more shards than shards_per_rank");
+    int32_t rc = check_merge_args(comm, n_queries, k, from, size, shards_per_rank);
+    if (rc) return rc;
+    rc = check_device(view->device);
+    if (rc) return rc;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : device_stream(view->device);
+    std::lock_guard<std::mutex> lc(comm->mu);
+    std::lock_guard<std::mutex> lv(view->mu);
+    rc = order_after_last(view, st);
+    if (rc) return rc;
+    osk_view* const vs[1] = {view};
+    if (comm->world > 1) {
+        rc = exchange_shard_index(comm, vs, shards_per_rank, &st);
+        if (rc) return rc;
+    } else if (view->xsi_comm != comm->id || view->xsi_spr != shards_per_rank) {
+        std::vector<int32_t> mine(shards_per_rank, 0x7FFFFFFF);
+        for (int j = 0; j < view->n_shards; ++j) mine[j] = view->shard_index[j];
+        OSK_HIP(view->d_xsi.reserve(sizeof(int32_t) * shards_per_rank));
+        OSK_HIP(hipMemcpyAsync(view->d_xsi.p, mine.data(), sizeof(int32_t) * shards_per_rank, hipMemcpyHostToDevice, st));
+        OSK_HIP(hipStreamSynchronize(st));
+        view->xsi_comm = comm->id;
+        view->xsi_spr = shards_per_rank;
+    }
+    rc = search_padded(view, d_queries, n_queries, k, d_accept, shards_per_rank, st);
+    if (rc) return rc;
+    const uint64_t* image = view->ws_xkeys.as<uint64_t>();
+    if (comm->world > 1) {   // world 1: the local lists are the whole image
+        rc = gather_keys(comm, vs, n_queries, k, shards_per_rank, &st);
+        if (rc) return rc;
+        image = view->ws_xgath.as<uint64_t>();
+    }
+    OSK_HIP(launch_merge_coord(image, nullptr, view->d_xsi.as<int32_t>(), n_queries, comm->world, shards_per_rank, k,
+                               from, size, d_scores, d_docs, d_shard_out, d_count, d_total_hits, d_max_score, st));
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_shards_search_merge(osk_comm* comm, osk_view* const* views, int32_t n_views, const void* queries,
+                                int32_t n_queries, int32_t k, const uint64_t* const* accept, int32_t from, int32_t size,
+                                float* out_scores, int32_t* out_docs, int32_t* out_shard_index, int32_t* out_count,
+                                int64_t* out_total_hits, float* out_max_score) {
+    OSK_GUARD_BEGIN
+    clear_error();
+    OSK_REQUIRE(comm != nullptr && views != nullptr && queries != nullptr, "null argument");
+    OSK_REQUIRE(out_scores && out_docs && out_shard_index && out_count && out_total_hits && out_max_score,
+                "null output");
+    OSK_REQUIRE(n_views == (int32_t)comm->devices.size(), "need one view per local device of the communicator");
+    int spr = 1;
+    for (int i = 0; i < n_views; ++i) {
+        OSK_REQUIRE(views[i] != nullptr, "null view");
+        OSK_REQUIRE(views[i]->device == comm->devices[i], "view i must live on the communicator's local device i");
+        OSK_REQUIRE(views[i]->dim == views[0]->dim && views[i]->enc == views[0]->enc,
+                    "all views must share dim and encoding");
+        spr = std::max(spr, views[i]->n_shards);
+    }
+    // every rank must use the same shards_per_rank: in one-process mode it is the max over the views;
+    // across processes the caller must stage the same number of shards on every rank (or use the
+    // device entry, which takes shards_per_rank explicitly)
+    int32_t rc = check_merge_args(comm, n_queries, k, from, size, spr);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lc(comm->mu);
+    std::vector<std::unique_lock<std::mutex>> locks;
+    std::vector<hipStream_t> sts(n_views);
+    const int64_t elem = views[0]->enc == ENC_FLOAT32 ? 4 : 1;
+    const size_t qbytes = (size_t)n_queries * views[0]->dim * elem;
+    size_t seg_off = 0;
+    for (int i = 0; i < n_views; ++i) {
+        osk_view* v = views[i];
+        rc = check_device(v->device);
+        if (rc) return rc;
+        sts[i] = device_stream(v->device);
+        locks.emplace_back(v->mu);
+        rc = order_after_last(v, sts[i]);
+        if (rc) return rc;
+        // queries and accept bitsets → this device
+        OSK_HIP(v->ws_qin.reserve(std::max<size_t>(16, qbytes)));
+        OSK_HIP(hipMemcpyAsync(v->ws_qin.p, queries, qbytes, hipMemcpyHostToDevice, sts[i]));
+    }
+    rc = exchange_shard_index(comm, views, spr, sts.data());
+    if (rc) return rc;
+    for (int i = 0; i < n_views; ++i) {
+        osk_view* v = views[i];
+        OSK_HIP(hipSetDevice(v->device));
+        const int ns = (int)v->segs.size();
+        const uint64_t* const* d_acc = nullptr;
+        bool any = false;
+        for (int j = 0; accept && j < ns; ++j) any |= accept[seg_off + j] != nullptr;
+        if (any) {
+            size_t words = 0;
+            for (int j = 0; j < ns; ++j)
+                if (accept[seg_off + j]) words += (size_t)(v->segs[j]->max_doc + 63) / 64;
+            OSK_HIP(v->ws_accept.reserve(std::max<size_t>(8, words * 8)));
+            OSK_HIP(v->ws_accept_ptrs.reserve(sizeof(void*) * ns));
+            std::vector<const uint64_t*> ptrs(ns, nullptr);
+            size_t off = 0;
+            for (int j = 0; j < ns; ++j) {
+                if (!accept[seg_off + j]) continue;
+                const size_t w = (size_t)(v->segs[j]->max_doc + 63) / 64;
+                ptrs[j] = v->ws_accept.as<uint64_t>() + off;
+                OSK_HIP(hipMemcpyAsync(const_cast<uint64_t*>(ptrs[j]), accept[seg_off + j], w * 8,
+                                       hipMemcpyHostToDevice, sts[i]));
+                off += w;
+            }
+            OSK_HIP(hipMemcpyAsync(v->ws_accept_ptrs.p, ptrs.data(), sizeof(void*) * ns, hipMemcpyHostToDevice,
+                                   sts[i]));
+            OSK_HIP(hipStreamSynchronize(sts[i]));   // ptrs is a local
+            d_acc = v->ws_accept_ptrs.as<const uint64_t*>();
+        }
+        seg_off += ns;
+        rc = search_padded(v, v->ws_qin.p, n_queries, k, d_acc, spr, sts[i]);
+        if (rc) return rc;
+    }
+    const uint64_t* image = views[0]->ws_xkeys.as<uint64_t>();
+    if (comm->world > 1) {
+        rc = gather_keys(comm, views, n_queries, k, spr, sts.data());
+        if (rc) return rc;
+        image = views[0]->ws_xgath.as<uint64_t>();
+    }
+    // the coordinator reduce on local device 0 (every local device holds the same image)
+    osk_view* v0 = views[0];
+    OSK_HIP(hipSetDevice(v0->device));
+    const size_t n_out = (size_t)n_queries * size;
+    const size_t b_sc = n_out * 4, b_doc = n_out * 4, b_sh = n_out * 4, b_cnt = (size_t)n_queries * 4,
+                 b_tot = (size_t)n_queries * 8, b_max = (size_t)n_queries * 4;
+    const size_t o_sc = 0, o_doc = o_sc + b_sc, o_sh = o_doc + b_doc, o_cnt = o_sh + b_sh,
+                 o_tot = (o_cnt + b_cnt + 7) / 8 * 8, o_max = o_tot + b_tot, total_b = o_max + b_max;
+    OSK_HIP(v0->ws_xout.reserve(total_b));
+    char* ob = v0->ws_xout.as<char>();
+    OSK_HIP(launch_merge_coord(image, nullptr, v0->d_xsi.as<int32_t>(), n_queries, comm->world, spr, k, from, size,
+                               reinterpret_cast<float*>(ob + o_sc), reinterpret_cast<int32_t*>(ob + o_doc),
+                               reinterpret_cast<int32_t*>(ob + o_sh), reinterpret_cast<int32_t*>(ob + o_cnt),
+                               reinterpret_cast<int64_t*>(ob + o_tot), reinterpret_cast<float*>(ob + o_max), sts[0]));
+    OSK_HIP(v0->h_stage.reserve(total_b));
+    OSK_HIP(hipMemcpyAsync(v0->h_stage.p, ob, total_b, hipMemcpyDeviceToHost, sts[0]));
+    for (int i = 0; i < n_views; ++i) {
+        OSK_HIP(hipSetDevice(views[i]->device));
+        OSK_HIP(hipStreamSynchronize(sts[i]));
+    }
+    const char* hb = static_cast<const char*>(v0->h_stage.p);
+    std::memcpy(out_scores, hb + o_sc, b_sc);
+    std::memcpy(out_docs, hb + o_doc, b_doc);
+    std::memcpy(out_shard_index, hb + o_sh, b_sh);
+    std::memcpy(out_count, hb + o_cnt, b_cnt);
+    std::memcpy(out_total_hits, hb + o_tot, b_tot);
+    std::memcpy(out_max_score, hb + o_max, b_max);
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+}  // extern "C"

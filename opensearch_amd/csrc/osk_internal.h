@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <atomic>
 #include "osk_common.h"
 
 namespace osk {
@@ -207,29 +208,32 @@ hipError_t launch_sq8_settle(int cfg, int nq, const SettleParams& p, hipStream_t
 
 int cfg_index(int units);
 
-// Process-wide tuning knobs (osk_tune_set; benchmarks and A/B runs only).
+// Process-wide tuning knobs (osk_tune_set).  Every field is an atomic int: a search reads each knob
+// once where it decides on it, and a concurrent osk_tune_set can only switch between valid settings
+// (every path returns the same exact results).  The fields marked TESTING are settable only in the
+// testing build (libosknn_testing.so, -DOSK_TESTING): they corrupt results or trace internals.
 struct Tuning {
-    int scan_nt = 1;          // non-temporal corpus loads in scan_f32 (+4% HBM rate, profiles/r01_scan_ab.txt)
-    int tiles_target = 0;     // workgroup tiles per view (scan grid size); 0 = whole rounds of the chip's
+    std::atomic<int> scan_nt{1};          // non-temporal corpus loads in scan_f32 (+4% HBM rate, profiles/r01_scan_ab.txt)
+    std::atomic<int> tiles_target{0};     // workgroup tiles per view (scan grid size); 0 = whole rounds of the chip's
                               // resident slots (osk_view_create)
-    int tile_slots_per_cu = 4;    // resident scan workgroups per CU (4 waves/SIMD, 256-thread groups)
-    int tile_large_slots = 24;    // views of ≥ CUs × this × tile_min_rows rows: CUs × this tiles (0 = off)
-    int tile_max_rounds = 4;      // at most this many rounds (10M rows: 4096 tiles, profiles/r01e)
-    int tile_min_rows = 1024; // ...and at least this many rows per tile (1.25M rows: 1024 tiles of 1221
+    std::atomic<int> tile_slots_per_cu{4};    // resident scan workgroups per CU (4 waves/SIMD, 256-thread groups)
+    std::atomic<int> tile_large_slots{24};    // views of ≥ CUs × this × tile_min_rows rows: CUs × this tiles (0 = off)
+    std::atomic<int> tile_max_rounds{4};      // at most this many rounds (10M rows: 4096 tiles, profiles/r01e)
+    std::atomic<int> tile_min_rows{1024}; // ...and at least this many rows per tile (1.25M rows: 1024 tiles of 1221
                               // rows, 4360 QPS vs 3968 for 4096 tiles of 305 rows — profiles/r01e/tiles_ab.txt)
-    int mfma_min_batch = 96;  // batches ≥ this may take the bf16×3 MFMA candidate path (0 = never)...
-    int sq8_cost_pct = 174;   // ...when ⌈nq/256⌉·256 ≤ nq · this / 100 (prefilter cost per 256 queries over a
+    std::atomic<int> mfma_min_batch{96};  // batches ≥ this may take the bf16×3 MFMA candidate path (0 = never)...
+    std::atomic<int> sq8_cost_pct{174};   // ...when ⌈nq/256⌉·256 ≤ nq · this / 100 (prefilter cost per 256 queries over a
                               // bf16×3 block's: C3 20 ms vs 11.5 ms; b128 11.8k vs 6.0k QPS, b256 11.8k vs
                               // 22.1k), else the int8 prefilter
-    int mfma_units = 512;     // workgroup units of the MFMA candidate pass per view
-    int sq8 = 1;              // certified int8 prefilter for float32 batches below mfma_min_batch
-    int sq8_mfma_nt = 1;      // A/B: non-temporal row loads in sq8_mfma
-    int sq8_mfma_queries = 32;    // queries per sq8_mfma launch: 16 or 32 (two MFMA chains per row operand)
-    int sq8_mfma_ablate = 0;  // A/B timing only: 1 skip sq8_mfma's epilogue, 2 its MFMAs (results wrong)
-    int sq8_mfma_min = 2;     // prefilter batches ≥ this scan on int8 MFMA, 16 queries per launch (0 = never)
-    int sq8_force_fallback = 0;   // tests: every list of a prefiltered search is re-scanned exactly
-    int settle_trace = 0;     // A/B only: record settle phase timestamps (debug copy "settle_trace")
-    int mfma_ablate = 0;      // A/B only: 1 skip the epilogue, 2 skip query staging, 4 skip corpus staging,
+    std::atomic<int> mfma_units{512};     // workgroup units of the MFMA candidate pass per view
+    std::atomic<int> sq8{1};              // certified int8 prefilter for float32 batches below mfma_min_batch
+    std::atomic<int> sq8_mfma_nt{1};      // A/B: non-temporal row loads in sq8_mfma
+    std::atomic<int> sq8_mfma_queries{32};    // queries per sq8_mfma launch: 16 or 32 (two MFMA chains per row operand)
+    std::atomic<int> sq8_mfma_ablate{0};  // TESTING. A/B timing only: 1 skip sq8_mfma's epilogue, 2 its MFMAs (results wrong)
+    std::atomic<int> sq8_mfma_min{2};     // prefilter batches ≥ this scan on int8 MFMA, 16 queries per launch (0 = never)
+    std::atomic<int> sq8_force_fallback{0};   // TESTING. tests: every list of a prefiltered search is re-scanned exactly
+    std::atomic<int> settle_trace{0};     // TESTING. A/B only: record settle phase timestamps (debug copy "settle_trace")
+    std::atomic<int> mfma_ablate{0};      // TESTING. A/B only: 1 skip the epilogue, 2 skip query staging, 4 skip corpus staging,
                               // 8 force the full staging epilogue, 16 skip the pilot pass
                               // (results are wrong and the exact fallback is skipped)
 };

@@ -6,10 +6,15 @@ Mapping onto the reference:
     the shard results by score (SearchPhaseController.java:224-246).
   * Here shard s lives on rank `shard_owner(s)` (contiguous blocks, so a GPU owns 8/G shards of an
     8-shard index).  Each rank scans its shards in one launch and produces per-shard top-k lists of
-    8-byte hit keys; one `torch.distributed.all_gather_into_tensor` (backend "nccl" = RCCL over xGMI
-    on the MI355X node, "gloo" in CPU tests) exchanges them; the coordinator reduce then runs on the
-    device straight over the gathered image (`osk_merge_device_ranked`) or, for host tensors, in the
-    library's host reduce.
+    8-byte hit keys; ONE all-gather exchanges them and the coordinator reduce runs on the device
+    straight over the gathered image.
+  * The product path is libosknn's own: `DeviceComm` wraps an `osk_comm` (RCCL inside the library,
+    ncclCommInitRank / ncclCommInitAll) and `ShardSearchMerge` calls `osk_shards_search_merge_device`
+    (scan + ncclAllGather + merge_coord, one C-ABI call per step) — what a Java host would bind.
+    torch.distributed only carries the communicator id at start-up (any backend, gloo included).
+  * `ShardExchange` is the same exchange written over `torch.distributed.all_gather_into_tensor`: the
+    CPU (gloo) tests of the gather/merge logic and the N > 1 rehearsal on one GPU (several ranks per
+    card, which RCCL refuses) use it; for host tensors it reduces in the library's host reduce.
 The exchange is k·B·8 bytes per shard — latency-bound, microseconds next to a millisecond scan.
 """
 from __future__ import annotations
@@ -22,6 +27,111 @@ import torch.distributed as dist
 
 from . import _lib
 from ._lib import check, lib, ptr
+
+
+class DeviceComm:
+    """An RCCL communicator owned by libosknn (`osk_comm`, include/osknn.h)."""
+
+    def __init__(self, handle: int):
+        self._h = C.c_void_p(handle)
+        r, w, n = C.c_int32(), C.c_int32(), C.c_int32()
+        check(lib().osk_comm_info(self._h, C.byref(r), C.byref(w), C.byref(n)))
+        self.rank, self.world, self.n_local = r.value, w.value, n.value
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * _lib.OSK_COMM_ID_BYTES)()
+        check(lib().osk_comm_unique_id(buf))
+        return bytes(buf)
+
+    @classmethod
+    def init_rank(cls, device: int, rank: int, world: int, uid: bytes) -> "DeviceComm":
+        """One process per GPU (ncclCommInitRank; blocks until every rank has joined)."""
+        buf = (C.c_uint8 * _lib.OSK_COMM_ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        check(lib().osk_comm_init_rank(device, rank, world, buf, C.byref(h)))
+        return cls(h.value)
+
+    @classmethod
+    def init_all(cls, devices) -> "DeviceComm":
+        """One process driving several GPUs (ncclCommInitAll): local device i is rank i."""
+        d = np.asarray(devices, np.int32)
+        h = C.c_void_p()
+        check(lib().osk_comm_init_all(ptr(d), len(d), C.byref(h)))
+        return cls(h.value)
+
+    @classmethod
+    def from_process_group(cls, device: int, group=None) -> "DeviceComm":
+        """Rank 0 makes the id; torch.distributed (any backend) hands it to the other ranks."""
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        obj = [cls.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        return cls.init_rank(device, rank, world, obj[0])
+
+    @property
+    def handle(self):
+        return self._h
+
+    def all_gather(self, send: torch.Tensor, recv: torch.Tensor, stream: int | None = None) -> None:
+        check(lib().osk_comm_all_gather(self._h, send.data_ptr(), recv.data_ptr(),
+                                        send.numel() * send.element_size(), stream))
+
+    def close(self):
+        if self._h.value:
+            check(lib().osk_comm_release(self._h))
+            self._h = C.c_void_p()
+
+
+class ShardSearchMerge:
+    """One rank's whole multi-GPU query step through the C-ABI (osk_shards_search_merge_device): scan of
+    the rank's shards, ONE ncclAllGather of the per-shard top-k lists inside libosknn, coordinator
+    TopDocs.merge on the device.  Outputs (scores, docs, shard index, count, total hits, max score)
+    are preallocated and overwritten by the next call."""
+
+    def __init__(self, comm: DeviceComm, view, shards_per_rank: int, nq: int, k: int, from_: int, size: int,
+                 device: int):
+        self.comm, self.view, self.spr = comm, view, shards_per_rank
+        self.nq, self.k, self.from_, self.size = nq, k, from_, size
+        dev = torch.device("cuda", device)
+        self.out = (torch.empty((nq, size), dtype=torch.float32, device=dev),
+                    torch.empty((nq, size), dtype=torch.int32, device=dev),
+                    torch.empty((nq, size), dtype=torch.int32, device=dev),
+                    torch.empty(nq, dtype=torch.int32, device=dev),
+                    torch.empty(nq, dtype=torch.int64, device=dev),
+                    torch.empty(nq, dtype=torch.float32, device=dev))
+
+    def __call__(self, d_queries: int, stream: int, d_accept: int | None = None):
+        sc, dc, sh, cnt, tot, mx = self.out
+        check(lib().osk_shards_search_merge_device(self.comm.handle, self.view, d_queries, self.nq, self.k, d_accept,
+                                                   self.spr, self.from_, self.size, sc.data_ptr(), dc.data_ptr(),
+                                                   sh.data_ptr(), cnt.data_ptr(), tot.data_ptr(), mx.data_ptr(),
+                                                   stream))
+        return self.out
+
+
+def shards_search_merge(comm: DeviceComm, views, queries: np.ndarray, k: int, from_: int, size: int, accept=None):
+    """Host-buffer multi-GPU query (osk_shards_search_merge): views[i] lives on the communicator's local
+    device i; accept = None or one bool mask (or None) per segment of every view, in view order.
+    Returns (scores[nq,size], docs, shard_index, count[nq], total_hits[nq], max_score[nq])."""
+    q = np.ascontiguousarray(queries)
+    nq = q.shape[0]
+    out = (np.empty((nq, size), np.float32), np.empty((nq, size), np.int32), np.empty((nq, size), np.int32),
+           np.empty(nq, np.int32), np.empty(nq, np.int64), np.empty(nq, np.float32))
+    hv = (C.c_void_p * len(views))(*[v.handle if hasattr(v, "handle") else v for v in views])
+    acc_arr, keep = None, []
+    if accept is not None:
+        from .lucene import bits_from_bool
+        ptrs = []
+        for a in accept:
+            if a is None:
+                ptrs.append(None)
+            else:
+                keep.append(bits_from_bool(a))
+                ptrs.append(keep[-1].ctypes.data)
+        acc_arr = (C.c_void_p * len(ptrs))(*ptrs)
+    check(lib().osk_shards_search_merge(comm.handle, hv, len(views), ptr(q), nq, k, acc_arr, from_, size,
+                                        *[ptr(o) for o in out]))
+    return out
 
 
 def shard_owner(shard: int, n_shards: int, world: int) -> int:

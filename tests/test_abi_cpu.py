@@ -36,12 +36,13 @@ def test_library_exports_every_header_symbol():
 
 
 def test_abi_version_and_constants():
-    assert _lib.lib().osk_abi_version() == 1
+    assert _lib.lib().osk_abi_version() == 2
     text = HEADER.read_text()
-    for name in ["OSK_MAX_K", "OSK_EUCLIDEAN", "OSK_DOT_PRODUCT", "OSK_COSINE", "OSK_MAXIMUM_INNER_PRODUCT",
+    for name in ["OSK_COMM_ID_BYTES", "OSK_WARM_PREFILTER", "OSK_WARM_PREFILTER_MFMA", "OSK_WARM_BATCHED",
+                 "OSK_WARM_ALL", "OSK_MAX_K", "OSK_EUCLIDEAN", "OSK_DOT_PRODUCT", "OSK_COSINE", "OSK_MAXIMUM_INNER_PRODUCT",
                  "OSK_FLOAT32", "OSK_BYTE", "OSK_ERR_NO_DEVICE"]:
         val = int(re.search(rf"#define {name}\s+(-?\d+)", text).group(1))
-        py = name if name.startswith(("OSK_ERR", "OSK_MAX_")) else name[4:]
+        py = name if name.startswith(("OSK_ERR", "OSK_MAX_", "OSK_COMM", "OSK_WARM")) else name[4:]
         assert getattr(_lib, py) == val
 
 
@@ -54,6 +55,21 @@ def test_device_entry_points_fail_loudly_without_gpu():
     rc = _lib.lib().osk_seg_synth(0, 10, 8, 0, 0, 1, 0, 0, C.byref(h))
     assert rc == _lib.OSK_ERR_NO_DEVICE and "no HIP device" in _lib.lib().osk_last_error().decode()
     assert _lib.lib().osk_merge_device(0, None, None, None, 1, 1, 10, 0, 10, *([None] * 7)) != 0
+    uid = (C.c_uint8 * _lib.OSK_COMM_ID_BYTES)()
+    assert _lib.lib().osk_comm_unique_id(uid) == _lib.OSK_ERR_NO_DEVICE
+    comm = C.c_void_p()
+    assert _lib.lib().osk_comm_init_rank(0, 0, 1, uid, C.byref(comm)) == _lib.OSK_ERR_NO_DEVICE
+
+
+def test_testing_knobs_only_in_the_testing_build():
+    """The shipped library refuses the result-corrupting A/B and test knobs; the testing build takes them."""
+    for key in ["sq8_force_fallback", "sq8_mfma_ablate", "mfma_ablate", "settle_trace"]:
+        assert _lib.lib().osk_tune_set(key.encode(), 1) == _lib.OSK_ERR_UNSUPPORTED
+        with _lib.testing() as T:
+            assert T.osk_tune_set(key.encode(), 1) == 0 and T.osk_tune_set(key.encode(), 0) == 0
+    assert _lib.lib().osk_view_debug_copy(None, b"qc", None, 0) == _lib.OSK_ERR_UNSUPPORTED
+    for key, bad in [("sq8", 2), ("sq8_mfma_queries", 24), ("tiles_target", -1), ("nope", 0)]:
+        assert _lib.lib().osk_tune_set(key.encode(), bad) == _lib.OSK_ERR_INVALID
 
 
 def test_host_generator_matches_oracle_generator():

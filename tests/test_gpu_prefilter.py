@@ -136,20 +136,22 @@ def test_prefilter_certifies_without_fallback_on_random_data(sim):
 
 
 def test_forced_exact_tiles_is_exact():
+    """Every list re-scanned exactly inside the settle (the testing build's sq8_force_fallback knob)."""
     sim = LU.VectorSimilarityFunction.EUCLIDEAN
     rows = corpus(12000, 128, sim, 9)
     queries = corpus(11, 128, sim, 10)
-    ds, readers = view_of([rows[:5000], rows[5000:]], sim, [0, 1], [1, 0])
-    try:
-        off = with_tune("sq8", 0, lambda: ds.search(queries, 10, 0, 10))
-        forced = with_tune("sq8_force_fallback", 1, lambda: ds.search(queries, 10, 0, 10))
-        assert_same(forced, off)
-        assert ds.counter("sq8_fallback_queries") == len(queries)
-        on = ds.search(queries, 10, 0, 10)
-        assert_same(on, off)
-        assert ds.counter("sq8_fallback_queries") == len(queries)
-    finally:
-        close_all(ds, readers)
+    with _lib.testing():
+        ds, readers = view_of([rows[:5000], rows[5000:]], sim, [0, 1], [1, 0])
+        try:
+            off = with_tune("sq8", 0, lambda: ds.search(queries, 10, 0, 10))
+            forced = with_tune("sq8_force_fallback", 1, lambda: ds.search(queries, 10, 0, 10))
+            assert_same(forced, off)
+            assert ds.counter("sq8_fallback_queries") == len(queries)
+            on = ds.search(queries, 10, 0, 10)
+            assert_same(on, off)
+            assert ds.counter("sq8_fallback_queries") == len(queries)
+        finally:
+            close_all(ds, readers)
 
 
 @pytest.mark.parametrize("sim", SIMS, ids=lambda s: s.name)

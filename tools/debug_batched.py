@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
 """Debug the batched MFMA path on a small case: compare the approx candidates it kept with numpy."""
+import os
+os.environ.setdefault("OSK_TESTING_LIB", "1")   # A/B knobs live in libosknn_testing.so
 import ctypes as C
 import os
 import sys

@@ -8,7 +8,7 @@ timeout -k 10 300 python bench.py --steps 20 --warmup 2 --no-cpu-baseline --dump
 for n in 2 4 8; do
   echo "== N=$n" | tee -a $OUT/steps.log
   timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port 2951$n \
-      bench.py --gpus $n --dist-backend gloo --steps 20 --warmup 2 --no-cpu-baseline --dump $OUT/res_$n.npz > $OUT/rehearse_$n.log 2>&1 || { echo rc=$?; tail -30 $OUT/rehearse_$n.log; exit 1; }
+      bench.py --gpus $n --exchange torch --dist-backend gloo --steps 20 --warmup 2 --no-cpu-baseline --dump $OUT/res_$n.npz > $OUT/rehearse_$n.log 2>&1 || { echo rc=$?; tail -30 $OUT/rehearse_$n.log; exit 1; }
   tail -1 $OUT/rehearse_$n.log | cut -c1-200
 done
 python - <<'PY'

@@ -6,6 +6,8 @@
 ablate bits: 1 = skip the epilogue (scores + selection), 2 = skip query (B) staging, 4 = skip corpus (A) staging.
 Ablated runs produce wrong candidates; only the kernel time (HIP events, osk_view_profile) matters.
 """
+import os
+os.environ.setdefault("OSK_TESTING_LIB", "1")   # A/B knobs live in libosknn_testing.so
 import argparse
 import ctypes as C
 import os

@@ -1,6 +1,8 @@
 """A/B timing of the int8 MFMA prefilter's main pass (C3, 16 queries per search): full kernel vs
 ablations (tune sq8_mfma_ablate: 1 no epilogue, 2 no MFMA, 3 loads only).  Results of ablated runs
 are wrong; only the kernel time (osk_view_scan_time: pilot + merge + main) is reported."""
+import os
+os.environ.setdefault("OSK_TESTING_LIB", "1")   # A/B knobs live in libosknn_testing.so
 import ctypes as C
 import os
 import sys

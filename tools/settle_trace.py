@@ -1,5 +1,7 @@
 """Phase timestamps of the prefilter settle (tune "settle_trace"): where a (slice, query) block spends
 its time.  python tools/settle_trace.py [rows_per_shard] [batch]"""
+import os
+os.environ.setdefault("OSK_TESTING_LIB", "1")   # A/B knobs live in libosknn_testing.so
 import ctypes as C
 import sys
 
