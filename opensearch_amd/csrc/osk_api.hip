@@ -237,6 +237,7 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         {"sq8_cost_pct", &g_tuning.sq8_cost_pct, 0, 100000, false},
         {"mfma_units", &g_tuning.mfma_units, 1, 32768, false},
         {"sq8", &g_tuning.sq8, 0, 1, false},
+        {"filter_gather", &g_tuning.filter_gather, 0, 1, false},
         {"sq8_mfma_nt", &g_tuning.sq8_mfma_nt, 0, 1, false},
         {"sq8_mfma_queries", &g_tuning.sq8_mfma_queries, 16, 32, false},
         {"sq8_mfma_min", &g_tuning.sq8_mfma_min, 0, 1 << 20, false},
@@ -922,6 +923,83 @@ int32_t ensure_sq8t(osk_view* v, hipStream_t st) {
     return OSK_OK;
 }
 
+// Settle slices over the wave lists of a tile table (list = tile·4 + wave): kSliceLists lists each,
+// never spanning shards (an empty shard gets one empty slice so its result is still written); each
+// slice carries its L group (aligned chunks of kLGroupLists lists of the shard).
+void settle_slices(const std::vector<int32_t>& shard_tile_begin, std::vector<int4>& sl, std::vector<int32_t>& ssb) {
+    const int S = (int)shard_tile_begin.size() - 1;
+    sl.clear();
+    ssb.assign(S + 1, 0);
+    for (int sh = 0; sh < S; ++sh) {
+        ssb[sh] = (int32_t)sl.size();
+        const int l0 = 4 * shard_tile_begin[sh], l1 = 4 * shard_tile_begin[sh + 1];
+        if (l0 == l1) sl.push_back(make_int4(l0, l0, l0, l0));
+        for (int l = l0; l < l1; l += kSliceLists) {
+            const int ga = l0 + (l - l0) / kLGroupLists * kLGroupLists;
+            sl.push_back(make_int4(l, std::min(l + kSliceLists, l1), ga, std::min(ga + kLGroupLists, l1)));
+        }
+    }
+    ssb[S] = (int32_t)sl.size();
+}
+
+// Gather tiles for filtered scans over the compacted accepted ordinals (osk_filter.hip): one round of
+// the chip's resident scan workgroups (CUs × 4) split over the segments by rows, at least one per
+// non-empty segment, ordered by shard like the row tiles (so lists never span shards); gather tile
+// j of nj of a segment covers ordinals [cnt·j/nj, cnt·(j+1)/nj) of its cnt accepted ones.  Built once.
+int32_t ensure_gather(osk_view* v, hipStream_t st) {
+    if (v->gather_ready) return OSK_OK;
+    const int ns = (int)v->segs.size();
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, v->device) != hipSuccess || cus <= 0)
+        cus = 256;
+    const int64_t target = std::min<int64_t>((int64_t)cus * 4, std::max(1, v->n_tiles));
+    int64_t total = 0;
+    for (osk_seg* sg : v->segs) total += sg->n_rows;
+    std::vector<int4> gt;
+    std::vector<int32_t> gsb(v->n_shards + 1, 0);
+    for (int sh = 0; sh < v->n_shards; ++sh) {
+        gsb[sh] = (int32_t)gt.size();
+        for (int i = 0; i < ns; ++i) {
+            if (v->seg_shard[i] != sh || v->segs[i]->n_rows == 0) continue;
+            const int64_t nj = std::max<int64_t>(1, (int64_t)((double)v->segs[i]->n_rows * target / std::max<int64_t>(1, total)));
+            for (int64_t j = 0; j < nj; ++j) gt.push_back(make_int4(i, sh, (int)j, (int)nj));
+        }
+    }
+    gsb[v->n_shards] = (int32_t)gt.size();
+    std::vector<int4> sl;
+    std::vector<int32_t> ssb;
+    settle_slices(gsb, sl, ssb);
+    // each segment's tile range in the row-tile table (tiles of a segment are contiguous)
+    std::vector<TileDev> tiles(v->n_tiles);
+    if (v->n_tiles)
+        OSK_HIP(hipMemcpyAsync(tiles.data(), v->d_tiles.p, sizeof(TileDev) * v->n_tiles, hipMemcpyDeviceToHost, st));
+    OSK_HIP(hipStreamSynchronize(st));
+    std::vector<int2> seg_tiles(ns, make_int2(0, 0));
+    for (int t = 0; t < v->n_tiles; ++t) {
+        int2& r = seg_tiles[tiles[t].seg];
+        if (r.x == r.y) r = make_int2(t, t + 1);
+        else r.y = t + 1;
+    }
+    v->n_gtiles = (int)gt.size();
+    v->n_gslices = (int)sl.size();
+    OSK_HIP(v->d_gtiles.reserve(sizeof(int4) * std::max<size_t>(1, gt.size())));
+    OSK_HIP(v->d_gslices.reserve(sizeof(int4) * sl.size()));
+    OSK_HIP(v->d_gshard_slice_begin.reserve(sizeof(int32_t) * ssb.size()));
+    OSK_HIP(v->d_seg_tiles.reserve(sizeof(int2) * ns));
+    OSK_HIP(v->ws_tcnt.reserve(sizeof(int32_t) * std::max(1, v->n_tiles)));
+    OSK_HIP(v->ws_tpre.reserve(sizeof(int32_t) * (v->n_tiles + 1)));
+    OSK_HIP(v->ws_scnt.reserve(sizeof(int32_t) * ns));
+    OSK_HIP(v->ws_comp.reserve(sizeof(uint32_t) * std::max<int64_t>(1, total)));
+    if (!gt.empty())
+        OSK_HIP(hipMemcpyAsync(v->d_gtiles.p, gt.data(), sizeof(int4) * gt.size(), hipMemcpyHostToDevice, st));
+    OSK_HIP(hipMemcpyAsync(v->d_gslices.p, sl.data(), sizeof(int4) * sl.size(), hipMemcpyHostToDevice, st));
+    OSK_HIP(hipMemcpyAsync(v->d_gshard_slice_begin.p, ssb.data(), sizeof(int32_t) * ssb.size(), hipMemcpyHostToDevice, st));
+    OSK_HIP(hipMemcpyAsync(v->d_seg_tiles.p, seg_tiles.data(), sizeof(int2) * ns, hipMemcpyHostToDevice, st));
+    OSK_HIP(hipStreamSynchronize(st));
+    v->gather_ready = true;
+    return OSK_OK;
+}
+
 int32_t ensure_sq8(osk_view* v, hipStream_t st) {
     if (v->sq8_ready) return OSK_OK;
     const int ns = (int)v->segs.size();
@@ -936,17 +1014,8 @@ int32_t ensure_sq8(osk_view* v, hipStream_t st) {
     v->units8 = (v->dim + 15) / 16;
     {
         std::vector<int4> sl;
-        std::vector<int32_t> ssb(v->n_shards + 1, 0);
-        for (int sh = 0; sh < v->n_shards; ++sh) {
-            ssb[sh] = (int32_t)sl.size();
-            const int l0 = 4 * v->shard_tile_begin[sh], l1 = 4 * v->shard_tile_begin[sh + 1];
-            if (l0 == l1) sl.push_back(make_int4(l0, l0, l0, l0));
-            for (int l = l0; l < l1; l += kSliceLists) {   // L groups: aligned chunks of kLGroupLists lists
-                const int ga = l0 + (l - l0) / kLGroupLists * kLGroupLists;
-                sl.push_back(make_int4(l, std::min(l + kSliceLists, l1), ga, std::min(ga + kLGroupLists, l1)));
-            }
-        }
-        ssb[v->n_shards] = (int32_t)sl.size();
+        std::vector<int32_t> ssb;
+        settle_slices(v->shard_tile_begin, sl, ssb);
         v->n_slices = (int)sl.size();
         OSK_HIP(v->d_slices.reserve(sizeof(int4) * sl.size()));
         OSK_HIP(v->d_shard_slice_begin.reserve(sizeof(int32_t) * ssb.size()));
@@ -986,10 +1055,19 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     OSK_HIP(launch_sq8_prep(v->cfg, static_cast<const float*>(d_queries), v->dim, nq, nq_pad, UP, u8,
                             v->ws_q.as<float4>(), v->ws_qnorm.as<float>(), v->ws_q8.p, v->ws_qc.as<float4>(),
                             v->ws_flags.as<int>(), st));
-    const size_t nl = (size_t)nq * 4 * v->n_tiles * kKQ;
+    // batches of ≥ sq8_mfma_min queries: the int8 MFMA scan, 16 queries per launch; else the VALU
+    // scan, ≤ 8 per launch.  Filtered VALU scans run over the compacted accepted ordinals.
+    const bool use_mfma = g_tuning.sq8_mfma_min > 0 && nq >= g_tuning.sq8_mfma_min && sq8_mfma_supported(u8);
+    const bool gather = d_accept && !use_mfma && g_tuning.filter_gather;
+    if (gather) {
+        rc = ensure_gather(v, st);
+        if (rc) return rc;
+    }
+    const int n_scan_tiles = gather ? v->n_gtiles : v->n_tiles;
+    const size_t nl = (size_t)nq * 4 * n_scan_tiles * kKQ;
     OSK_HIP(v->ws_sq8cand.reserve(sizeof(uint64_t) * nl));
     OSK_HIP(v->ws_sq8lb.reserve(sizeof(uint32_t) * nl));
-    OSK_HIP(v->ws_lbmax.reserve(sizeof(uint32_t) * (size_t)nq * 4 * v->n_tiles));
+    OSK_HIP(v->ws_lbmax.reserve(sizeof(uint32_t) * (size_t)nq * 4 * n_scan_tiles));
     Sq8Params p{};
     p.segs = v->d_segs.as<SegDev>();
     p.tiles = v->d_tiles.as<TileDev>();
@@ -1001,16 +1079,31 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     p.cand_lb = v->ws_sq8lb.as<uint32_t>();
     p.list_lbmax = v->ws_lbmax.as<uint32_t>();
     p.visited = reinterpret_cast<unsigned long long*>(d_visited);
-    p.n_tiles = v->n_tiles;
-    p.n_lists = 4 * v->n_tiles;
+    p.n_tiles = n_scan_tiles;
+    p.n_lists = 4 * n_scan_tiles;
     p.units8 = u8;
     p.sim = v->sim;
     p.gam = v->sq8_gam;
     p.g2 = v->sq8_g2;
     p.cos_slack = v->sq8_cos_slack;
-    // batches of ≥ sq8_mfma_min queries: the int8 MFMA scan, 16 queries per launch; else the VALU
-    // scan, ≤ 8 per launch
-    const bool use_mfma = g_tuning.sq8_mfma_min > 0 && nq >= g_tuning.sq8_mfma_min && sq8_mfma_supported(u8);
+    if (gather) {   // accepted ordinals of every segment, compacted (count, prefix, write)
+        FilterParams fp{};
+        fp.segs = v->d_segs.as<SegDev>();
+        fp.tiles = v->d_tiles.as<TileDev>();
+        fp.accept = d_accept;
+        fp.seg_vrow = v->d_seg_vrow.as<int64_t>();
+        fp.seg_tiles = v->d_seg_tiles.as<int2>();
+        fp.tcnt = v->ws_tcnt.as<int32_t>();
+        fp.tpre = v->ws_tpre.as<int32_t>();
+        fp.scnt = v->ws_scnt.as<int32_t>();
+        fp.comp = v->ws_comp.as<uint32_t>();
+        fp.n_tiles = v->n_tiles;
+        fp.n_segs = (int)v->segs.size();
+        OSK_HIP(launch_filter_compact(fp, st));
+        p.gtiles = v->d_gtiles.as<int4>();
+        p.comp = fp.comp;
+        p.scnt = fp.scnt;
+    }
     const int chunk = use_mfma ? (int)g_tuning.sq8_mfma_queries : kMaxNQ;
     if (use_mfma) {
         rc = ensure_sq8t(v, st);
@@ -1051,14 +1144,18 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     }
     rc = profile_end(v, st, false);
     if (rc) return rc;
-    OSK_HIP(v->ws_part.reserve(sizeof(uint64_t) * (size_t)nq * v->n_slices * k));
+    const int n_slices = gather ? v->n_gslices : v->n_slices;
+    OSK_HIP(v->ws_part.reserve(sizeof(uint64_t) * (size_t)nq * n_slices * k));
     SettleParams sp{};
-    sp.slices = v->d_slices.as<int4>();
-    sp.shard_slice_begin = v->d_shard_slice_begin.as<int32_t>();
+    sp.slices = gather ? v->d_gslices.as<int4>() : v->d_slices.as<int4>();
+    sp.shard_slice_begin = gather ? v->d_gshard_slice_begin.as<int32_t>() : v->d_shard_slice_begin.as<int32_t>();
     sp.tiles = v->d_tiles.as<TileDev>();
+    sp.gtiles = p.gtiles;
+    sp.comp = p.comp;
+    sp.scnt = p.scnt;
     sp.accept = d_accept;
     sp.part = v->ws_part.as<uint64_t>();
-    sp.n_slices = v->n_slices;
+    sp.n_slices = n_slices;
     sp.segs = v->d_segs.as<SegDev>();
     sp.seg_vrow = v->d_seg_vrow.as<int64_t>();
     sp.cand = p.cand;
@@ -1070,7 +1167,7 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     sp.shard_counts = d_shard_counts;
     sp.flags = v->ws_flags.as<int>();
     sp.counters = v->d_counters.as<unsigned long long>();
-    sp.n_lists = 4 * v->n_tiles;
+    sp.n_lists = 4 * n_scan_tiles;
     sp.scan_R = use_mfma ? kMfmaScanR : 64 / sq8_lanes(u8);
     sp.n_shards = S;
     sp.n_segs = (int)v->segs.size();
@@ -1079,7 +1176,7 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     sp.sim = v->sim;
     sp.force_fail = g_tuning.sq8_force_fallback;
     if (g_tuning.settle_trace) {
-        OSK_HIP(v->ws_trace.reserve(sizeof(unsigned long long) * 8 * (size_t)nq * v->n_slices));
+        OSK_HIP(v->ws_trace.reserve(sizeof(unsigned long long) * 8 * (size_t)nq * n_slices));
         sp.trace = v->ws_trace.as<unsigned long long>();
     }
     OSK_HIP(launch_sq8_settle(v->cfg, nq, sp, st));

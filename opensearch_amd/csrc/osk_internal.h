@@ -153,6 +153,12 @@ struct Sq8Params {
     uint64_t* pilot_keys;
     const uint64_t* thr_keys;
     const int32_t* thr_counts;
+    // gather mode (filtered sq8_scan, osk_filter.hip compaction): the grid runs over gather tiles
+    // {seg, shard, j, nj} — tile j of nj over segment seg's scnt[seg] accepted ordinals at
+    // comp[seg_vrow[seg] …] — instead of `tiles`; null = the row-range tiles
+    const int4* gtiles;
+    const uint32_t* comp;
+    const int32_t* scnt;
 };
 
 struct SettleParams {
@@ -182,8 +188,28 @@ struct SettleParams {
     int k;
     int sim;
     int force_fail;                  // tests: re-scan every list exactly
+    const int4* gtiles;              // gather mode (see Sq8Params): lists are gather tile·4 + wave
+    const uint32_t* comp;
+    const int32_t* scnt;
     unsigned long long* trace;       // A/B only: per (query, slice) 8 slots of phase timestamps, or null
 };
+
+// Filter pushdown by compaction (osk_filter.hip): per segment, the accepted ordinals in ascending order
+// at comp[seg_vrow[seg] …], scnt[seg] of them.
+struct FilterParams {
+    const SegDev* segs;
+    const TileDev* tiles;               // the view's scan tiles (row ranges of one segment each)
+    const uint64_t* const* accept;      // per segment: accept bitset or null (= every row accepted)
+    const int64_t* seg_vrow;            // view row of each segment's ord 0
+    const int2* seg_tiles;              // per segment: [first tile, end tile) in the tile table
+    int32_t* tcnt;                      // [n_tiles] accepted rows per tile
+    int32_t* tpre;                      // [n_tiles + 1] exclusive prefix of tcnt
+    int32_t* scnt;                      // [n_segs] accepted rows per segment
+    uint32_t* comp;                     // [view rows] compacted ordinals
+    int n_tiles;
+    int n_segs;
+};
+hipError_t launch_filter_compact(const FilterParams& p, hipStream_t s);
 
 hipError_t launch_sq8_quantize(const float4* x, int64_t n, int units, int pitch, int units8, void* out8,
                                float4* aux, int mode, hipStream_t s);
@@ -227,6 +253,8 @@ struct Tuning {
                               // 22.1k), else the int8 prefilter
     std::atomic<int> mfma_units{512};     // workgroup units of the MFMA candidate pass per view
     std::atomic<int> sq8{1};              // certified int8 prefilter for float32 batches below mfma_min_batch
+    std::atomic<int> filter_gather{1};    // filtered prefilter scans (VALU sq8_scan) compact the accepted ordinals
+                                          // first and scan them (osk_filter.hip); 0 = walk the bitset windows
     std::atomic<int> sq8_mfma_nt{1};      // A/B: non-temporal row loads in sq8_mfma
     std::atomic<int> sq8_mfma_queries{32};    // queries per sq8_mfma launch: 16 or 32 (two MFMA chains per row operand)
     std::atomic<int> sq8_mfma_ablate{0};  // TESTING. A/B timing only: 1 skip sq8_mfma's epilogue, 2 its MFMAs (results wrong)

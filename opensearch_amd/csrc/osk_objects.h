@@ -180,6 +180,12 @@ struct osk_view {
     osk::DevBuf d_slices, d_shard_slice_begin, ws_part;
     osk::DevBuf ws_pilot, ws_thr, ws_thr_counts;   // int8 MFMA prefilter: pilot keys, per-(query, shard) floors
     int64_t sq8_calls = 0;
+    // filter pushdown by compaction (osk_filter.hip): gather tiles over the compacted accepted ordinals
+    // (one round of the chip, split over segments by rows), their settle slices, per-segment tile ranges
+    bool gather_ready = false;
+    int n_gtiles = 0, n_gslices = 0;
+    osk::DevBuf d_gtiles, d_gslices, d_gshard_slice_begin, d_seg_tiles;
+    osk::DevBuf ws_tcnt, ws_tpre, ws_scnt, ws_comp;
     // multi-GPU exchange (osk_comm.hip): this rank's lists padded to the comm's shards per rank, the
     // gathered image of every rank, and the shardIndex of every gathered slot (exchanged once per comm)
     osk::DevBuf ws_xkeys, ws_xgath, d_xsi, ws_xout;

@@ -339,12 +339,34 @@ __device__ __forceinline__ int rs_base(int t) {
 // dots are reduce-scattered (rs_reduce) so each lane finishes the bound and quick test of P
 // (row, query) pairs instead of all NQ.
 // ------------------------------------------------------------------------------------------------
-template <int L, int V, int NQ, int U, bool FQ = false>
-__global__ __launch_bounds__(kBlock, FQ ? 4 : 1) void sq8_scan(Sq8Params p) {
+// MODE: kScanRows (row-range tiles; a filter is walked 64-row window by window), kScanQueue (single
+// query, filtered: accepted rows of sparse windows queued across windows), kScanGather (filtered: the
+// grid runs over gather tiles of the compacted accepted ordinals, osk_filter.hip).
+constexpr int kScanRows = 0, kScanQueue = 1, kScanGather = 2;
+
+// A gather tile's entry range and its scan wave's share: tile j of nj over cnt accepted ordinals, split
+// in 4 contiguous quarters.  The settle re-derives the same ranges for an overflowed list.
+__device__ __forceinline__ void gather_wave_range(int64_t cnt, int j, int nj, int wave, int64_t& b, int64_t& e) {
+    const int64_t e0 = cnt * j / nj, e1 = cnt * (j + 1) / nj;
+    const int64_t pw = (e1 - e0 + 3) / 4;
+    b = min(e0 + wave * pw, e1);
+    e = min(b + pw, e1);
+}
+
+template <int L, int V, int NQ, int U, int MODE = kScanRows>
+__global__ __launch_bounds__(kBlock, MODE == kScanQueue ? 4 : 1) void sq8_scan(Sq8Params p) {
     constexpr int R = 64 / L;
+    constexpr bool FQ = MODE == kScanQueue;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int t = lane & (L - 1), g = lane / L;
-    const TileDev tile = p.tiles[blockIdx.x];
+    TileDev tile;
+    int4 gt = make_int4(0, 0, 0, 1);
+    if constexpr (MODE == kScanGather) {
+        gt = p.gtiles[blockIdx.x];
+        tile = TileDev{gt.x, gt.y, 0, 0};
+    } else {
+        tile = p.tiles[blockIdx.x];
+    }
     const SegDev seg = p.segs[tile.seg];
     const int4* __restrict__ X = p.rows8[tile.seg];
     const float4* __restrict__ AX = p.aux[tile.seg];
@@ -542,7 +564,19 @@ __global__ __launch_bounds__(kBlock, FQ ? 4 : 1) void sq8_scan(Sq8Params p) {
         }
     };
 
-    if (FQ && abits && !seg.ord_to_doc) {
+    if constexpr (MODE == kScanGather) {
+        // filter pushdown by compaction: this wave's quarter of the gather tile's accepted ordinals,
+        // 64 at a time (one coalesced index load, then the rows), any segment layout (dense or sparse)
+        // (counts and ordinals are clamped to the segment: a corrupt list can never address outside it)
+        int64_t eb, ee;
+        gather_wave_range(min<int64_t>(p.scnt[tile.seg], seg.n_rows), gt.z, gt.w, wave, eb, ee);
+        const uint32_t* __restrict__ C = p.comp + vbase;
+        for (int64_t e0 = eb; e0 < ee; e0 += 64) {
+            const int n = (int)min<int64_t>(64, ee - e0);
+            const int pos = lane < n ? (int)min<int64_t>(C[e0 + lane], seg.n_rows - 1) : 0;
+            for (int i0 = 0; i0 < n; i0 += R * U) process(0, true, i0, n, pos);
+        }
+    } else if (FQ && abits && !seg.ord_to_doc) {
         // filter pushdown, FQ instance: the accepted rows of successive sparse 64-row windows are
         // queued across windows (lane l holds entry l: the row's offset from wb) and scanned 64 at a
         // time, so a sparse filter does not pay one load round trip per window.  Its own instance:
@@ -634,17 +668,25 @@ using Sq8Fn = void (*)(Sq8Params);
 #define OSK_SQ8_ROW(L, V) {sq8_scan<L, V, 1, 4>, sq8_scan<L, V, 2, 4>, sq8_scan<L, V, 4, 4>, sq8_scan<L, V, 8, 2>}
 static const Sq8Fn kSq8[8][4] = {OSK_SQ8_ROW(4, 1),  OSK_SQ8_ROW(8, 1),  OSK_SQ8_ROW(16, 1), OSK_SQ8_ROW(16, 2),
                                  OSK_SQ8_ROW(16, 3), OSK_SQ8_ROW(16, 4), OSK_SQ8_ROW(32, 4), OSK_SQ8_ROW(64, 4)};
-// single-query filtered scans: the FQ instance (cross-window queue of accepted rows)
-static const Sq8Fn kSq8Filtered[8] = {sq8_scan<4, 1, 1, 4, true>,  sq8_scan<8, 1, 1, 4, true>,
-                                      sq8_scan<16, 1, 1, 4, true>, sq8_scan<16, 2, 1, 4, true>,
-                                      sq8_scan<16, 3, 1, 4, true>, sq8_scan<16, 4, 1, 4, true>,
-                                      sq8_scan<32, 4, 1, 4, true>, sq8_scan<64, 4, 1, 4, true>};
+// single-query filtered scans without compaction: the queue instance (cross-window queue of accepted rows)
+static const Sq8Fn kSq8Filtered[8] = {sq8_scan<4, 1, 1, 4, kScanQueue>,  sq8_scan<8, 1, 1, 4, kScanQueue>,
+                                      sq8_scan<16, 1, 1, 4, kScanQueue>, sq8_scan<16, 2, 1, 4, kScanQueue>,
+                                      sq8_scan<16, 3, 1, 4, kScanQueue>, sq8_scan<16, 4, 1, 4, kScanQueue>,
+                                      sq8_scan<32, 4, 1, 4, kScanQueue>, sq8_scan<64, 4, 1, 4, kScanQueue>};
+// filtered scans over the compacted accepted ordinals (gather tiles)
+#define OSK_SQ8_GROW(L, V)                                                                          \
+    {sq8_scan<L, V, 1, 4, kScanGather>, sq8_scan<L, V, 2, 4, kScanGather>, sq8_scan<L, V, 4, 4, kScanGather>, \
+     sq8_scan<L, V, 8, 2, kScanGather>}
+static const Sq8Fn kSq8Gather[8][4] = {OSK_SQ8_GROW(4, 1),  OSK_SQ8_GROW(8, 1),  OSK_SQ8_GROW(16, 1),
+                                       OSK_SQ8_GROW(16, 2), OSK_SQ8_GROW(16, 3), OSK_SQ8_GROW(16, 4),
+                                       OSK_SQ8_GROW(32, 4), OSK_SQ8_GROW(64, 4)};
 
 hipError_t launch_sq8_scan(int nq, const Sq8Params& p, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
     const int slot = nq <= 1 ? 0 : nq <= 2 ? 1 : nq <= 4 ? 2 : 3;
     // NQ > 1: the queries and the 4 waves' per-query lists in LDS
     const size_t lds = slot == 0 ? 0 : (size_t)(1 << slot) * (p.units8 * 16 + 4 * kKQ * 12);
-    const auto fn = (slot == 0 && p.accept) ? kSq8Filtered[sq8_cfg(p.units8)] : kSq8[sq8_cfg(p.units8)][slot];
+    const int c = sq8_cfg(p.units8);
+    const auto fn = p.gtiles ? kSq8Gather[c][slot] : (slot == 0 && p.accept) ? kSq8Filtered[c] : kSq8[c][slot];
     if (ev_start || ev_stop)
         hipExtLaunchKernelGGL(fn, dim3(p.n_tiles), dim3(kBlock), lds, s, ev_start, ev_stop, 0, p);
     else
@@ -1152,7 +1194,28 @@ __global__ __launch_bounds__(kSettleThreads) void sq8_settle(SettleParams p) {
     if (p.trace && tid == 0) p.trace[((size_t)q * p.n_slices + g) * 8 + 3] = wall_clock64();
     // (c') overflowed lists: every accepted row of the scan wave's range (the scan's split of its
     // tile: per_wave = ⌈rows / 4R_s⌉·R_s), walked by this block's 4 waves (filter pushdown included)
-    for (uint32_t bits = exact; bits; bits &= bits - 1u) {
+    for (uint32_t bits = exact; bits && p.gtiles; bits &= bits - 1u) {
+        // gather mode: the scan wave's quarter of its gather tile's compacted ordinals (all accepted)
+        const int list = sl.x + __builtin_ctz(bits);
+        const int4 gt = p.gtiles[list >> 2];
+        const SegDev seg = p.segs[gt.x];
+        int64_t lb0, lb1;
+        gather_wave_range(min<int64_t>(p.scnt[gt.x], seg.n_rows), gt.z, gt.w, list & 3, lb0, lb1);
+        const uint32_t* __restrict__ C = p.comp + p.seg_vrow[gt.x];
+        const int64_t per_wave = ((lb1 - lb0 + kSettleWaves * R - 1) / (kSettleWaves * R)) * R;
+        const int64_t wb = lb0 + wave * per_wave;
+        const int64_t we = min(wb + per_wave, lb1);
+        const float4* X = static_cast<const float4*>(seg.rows);
+        for (int64_t e0 = wb; e0 < we; e0 += R) {
+            const bool valid = e0 + gr < we;
+            const int64_t row = valid ? min<int64_t>(C[e0 + gr], seg.n_rows - 1) : 0;
+            const int32_t doc = valid ? (seg.ord_to_doc ? seg.ord_to_doc[row] : (int32_t)row) : 0;
+            const float xn = (!L2K && sim == SIM_COSINE && valid) ? seg.xnorm_f[row] : 0.0f;
+            const float sc = settle_exact<L, V, L2K>(X + row * p.units, valid, p.units, t, qf, sim, qn, xn);
+            wave_offer(valid ? make_key(sc, (uint32_t)(seg.doc_base + doc)) : 0ull, t == 0, lk, thr, lane, k);
+        }
+    }
+    for (uint32_t bits = p.gtiles ? 0u : exact; bits; bits &= bits - 1u) {
         const int list = sl.x + __builtin_ctz(bits);
         const TileDev td = p.tiles[list >> 2];
         const SegDev seg = p.segs[td.seg];

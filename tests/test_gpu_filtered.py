@@ -1,10 +1,14 @@
 """GPU parity of single-query filtered searches (the C5 configuration as benchmarked).
 
-A single float32 query with an accept bitset over a dense segment takes its own scan instance:
-`sq8_scan<…, FQ = true>` (osk_sq8.hip), which queues the accepted rows of sparse 64-row windows
-across windows (one `ds_permute` append each) and scans the queue 64 rows at a time, flushing when
-the next window would overflow it.  These tests drive exactly that call (`search_batch(q[i:i+1])`,
-`DeviceShardSet.search` with one query) and compare docs and score bits against
+A float32 query with an accept bitset takes one of two scans (both run by every test here):
+  * gather (default, tune filter_gather 1): the accepted ordinals of every segment are compacted first
+    (osk_filter.hip: count per tile, prefix, write) and `sq8_scan<…, kScanGather>` runs over gather
+    tiles of that list; an overflowed list is re-scanned exactly over the same compacted range;
+  * window walk (filter_gather 0): `sq8_scan<…, kScanQueue>` queues the accepted rows of sparse
+    64-row windows across windows (one `ds_permute` append each) and scans the queue 64 rows at a
+    time, flushing when the next window would overflow it.
+These tests drive exactly that call (`search_batch(q[i:i+1])`, `DeviceShardSet.search` with one query)
+and compare docs and score bits against
 
   * the fp32 streaming scan of the same call (tune "sq8" 0), and
   * the oracle's [L] exactSearch restatement (`O.exact_search(..., accept_bits=...)`, ORDER_DEVICE),
@@ -84,6 +88,16 @@ def check_single(reader, rows, queries, k, sim, mask, ord_to_doc=None):
         assert np.array_equal(d[0, : c[0]], od), (i, d[0, : c[0]], od)
         assert np.array_equal(bits(s[0, : c[0]]), bits(os_))
         assert v[0] == ov
+
+
+@pytest.fixture(autouse=True, params=[1, 0], ids=["gather", "window_walk"])
+def filter_mode(request):
+    """Filtered single-query scans compact the accepted ordinals and scan them (tune filter_gather 1,
+    the default, osk_filter.hip), or walk the bitset's 64-row windows with the cross-window queue
+    instance (filter_gather 0)."""
+    _lib.tune("filter_gather", request.param)
+    yield request.param
+    _lib.tune("filter_gather", 1)
 
 
 @pytest.fixture(params=[0, 8], ids=["tiles_default", "tiles_8"])
@@ -195,4 +209,48 @@ def test_single_query_filtered_sparse_field():
     try:
         check_single(r, rows, queries, 10, COS, rng.random(max_doc) < 0.05, ord_to_doc=docs)
     finally:
+        r.close()
+
+
+@pytest.mark.parametrize("nq", [1, 5])
+def test_filtered_forced_exact_rescan_of_every_list(nq):
+    """The settle's exact re-scan of an overflowed list, forced for every list (the testing build's
+    sq8_force_fallback): in gather mode it walks the list's share of the compacted ordinals, in window
+    mode its row range; both must equal the fp32 scan."""
+    rows = corpus(40000, 128, COS, 140)
+    queries = corpus(nq, 128, COS, 141)
+    mask = np.random.default_rng(nq).random(40000) < 0.07
+    ab = O.bits_from_bool(mask)
+    with _lib.testing():
+        _lib.tune("sq8_mfma_min", 0)   # batches on the VALU scan (the gather path's)
+        r = LU.GpuFlatVectorsReader("v", rows, COS)
+        try:
+            off = sq8_off(lambda: r.search_batch(queries, 10, ab))
+            _lib.tune("sq8_force_fallback", 1)
+            forced = r.search_batch(queries, 10, ab)
+            _lib.tune("sq8_force_fallback", 0)
+            assert_same(forced, off)
+            assert_same(r.search_batch(queries, 10, ab), off)
+        finally:
+            r.close()
+            _lib.tune("sq8_mfma_min", 2)
+
+
+def test_filtered_batches_on_the_valu_scan():
+    """Filtered batches of 2…8 queries on the VALU scan (sq8_mfma_min 0) also take the gather path."""
+    rows = corpus(50000, 384, COS, 150)
+    queries = corpus(8, 384, COS, 151)
+    mask = np.random.default_rng(4).random(50000) < 0.03
+    ab = O.bits_from_bool(mask)
+    r = LU.GpuFlatVectorsReader("v", rows, COS)
+    _lib.tune("sq8_mfma_min", 0)
+    try:
+        for b in (2, 3, 8):
+            on = r.search_batch(queries[:b], 10, ab)
+            assert_same(on, sq8_off(lambda: r.search_batch(queries[:b], 10, ab)))
+            for i in range(b):
+                os_, od, _ = O.exact_search(rows, queries[i], 10, int(COS), accept_bits=ab)
+                assert np.array_equal(on[1][i], od)
+    finally:
+        _lib.tune("sq8_mfma_min", 2)
         r.close()

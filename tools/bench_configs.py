@@ -139,9 +139,15 @@ def main():
                 bits = [torch.from_numpy(bits_from_bool(rng.random(1_250_000) < sel).view(np.int64)).cuda()
                         for _ in range(8)]
                 ptrs = torch.tensor([b.data_ptr() for b in bits], dtype=torch.int64, device="cuda")
-                ms, km = run(v, q, 1, st, wu, accept_ptrs=ptrs)
-                emit(f"C5f-{int(sel * 100)}%", v, 1, ms, km, int(10_000_000 * sel) * 768 * 4 + 10_000_000 // 8,
-                     {"selectivity": sel})
+                for gmode in (1, 0):   # compacted gather scan (default) vs the bitset window walk
+                    _lib.tune("filter_gather", gmode)
+                    ms, km = run(v, q, 1, st, wu, accept_ptrs=ptrs)
+                    # the prefilter's own bytes: accepted int8 rows + 16-B bound terms + the bitset
+                    b8 = int(10_000_000 * sel) * (768 + 16) + 10_000_000 // 8
+                    emit(f"C5f-{int(sel * 100)}%", v, 1, ms, km, int(10_000_000 * sel) * 768 * 4 + 10_000_000 // 8,
+                         {"selectivity": sel, "filter_gather": gmode,
+                          "int8_prefilter_GBps": b8 / (km * 1e-3) / 1e9})
+                _lib.tune("filter_gather", 1)
         v.close()
     if "C4" in only:
         v = View(8, 12_500_000, 96, _lib.DOT_PRODUCT, _lib.FLOAT32, _lib.DIST_NORMALISH_UNIT)

@@ -6,7 +6,7 @@
 #   tools/gpu_run.sh test                 pytest -m gpu (all GPU parity tests)
 #   tools/gpu_run.sh test:K_EXPR          pytest -m gpu -k K_EXPR
 #   tools/gpu_run.sh smoke                __graft_entry__.smoke()
-#   tools/gpu_run.sh bench[:ARGS]         python bench.py ARGS   (ARGS comma-separated, e.g. bench:--batch,32)
+#   tools/gpu_run.sh bench[:ARGS]         python bench.py ARGS   (ARGS "+"-separated, e.g. bench:--batch+32)
 #   tools/gpu_run.sh prof[:ARGS]          rocprofv3 --kernel-trace --stats of a short bench.py ARGS run
 #   tools/gpu_run.sh pmc[:ARGS]           FETCH_SIZE and WRITE_SIZE passes (separate runs) + tools/pmc_traffic.py
 #   tools/gpu_run.sh mfmapmc[:ARGS]       SQ_INSTS_VALU_MFMA_MOPS_* / SQ_VALU_MFMA_BUSY_CYCLES pass of bench.py ARGS
@@ -27,7 +27,7 @@ run() {  # run <seconds> <logfile> cmd...
   echo "   rc=$rc ($(tail -c 300 "$log" | tr '\n' ' ' | cut -c1-300))" | tee -a "$OUT/steps.log"
   if [[ $rc != 0 ]]; then echo "step failed rc=$rc, stopping"; exit $rc; fi
 }
-args() { echo "${1//,/ }"; }
+args() { echo "${1//+/ }"; }   # step args are "+"-separated (bench:--batch+32)
 
 for step in "$@"; do
   name=${step%%:*}
