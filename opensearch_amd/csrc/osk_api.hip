@@ -238,6 +238,7 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         {"mfma_units", &g_tuning.mfma_units, 1, 32768, false},
         {"sq8", &g_tuning.sq8, 0, 1, false},
         {"filter_gather", &g_tuning.filter_gather, 0, 1, false},
+        {"gather_min", &g_tuning.gather_min, 0, 1 << 20, false},
         {"sq8_mfma_nt", &g_tuning.sq8_mfma_nt, 0, 1, false},
         {"sq8_mfma_queries", &g_tuning.sq8_mfma_queries, 16, 32, false},
         {"sq8_mfma_min", &g_tuning.sq8_mfma_min, 0, 1 << 20, false},
@@ -1103,6 +1104,7 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
         p.gtiles = v->d_gtiles.as<int4>();
         p.comp = fp.comp;
         p.scnt = fp.scnt;
+        p.gather_min = g_tuning.gather_min;
     }
     const int chunk = use_mfma ? (int)g_tuning.sq8_mfma_queries : kMaxNQ;
     if (use_mfma) {
@@ -1153,6 +1155,7 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     sp.gtiles = p.gtiles;
     sp.comp = p.comp;
     sp.scnt = p.scnt;
+    sp.gather_min = p.gather_min;   // the scan's split, exactly
     sp.accept = d_accept;
     sp.part = v->ws_part.as<uint64_t>();
     sp.n_slices = n_slices;

@@ -159,6 +159,7 @@ struct Sq8Params {
     const int4* gtiles;
     const uint32_t* comp;
     const int32_t* scnt;
+    int gather_min;                  // at most one gather tile per this many accepted rows of a segment
 };
 
 struct SettleParams {
@@ -191,6 +192,7 @@ struct SettleParams {
     const int4* gtiles;              // gather mode (see Sq8Params): lists are gather tile·4 + wave
     const uint32_t* comp;
     const int32_t* scnt;
+    int gather_min;
     unsigned long long* trace;       // A/B only: per (query, slice) 8 slots of phase timestamps, or null
 };
 
@@ -253,6 +255,8 @@ struct Tuning {
                               // 22.1k), else the int8 prefilter
     std::atomic<int> mfma_units{512};     // workgroup units of the MFMA candidate pass per view
     std::atomic<int> sq8{1};              // certified int8 prefilter for float32 batches below mfma_min_batch
+    std::atomic<int> gather_min{0};       // ...at most one gather tile per this many accepted rows (0 = every gather
+                                          // tile; fewer, longer tiles were slower: profiles/r02c/gather_min_ab.jsonl)
     std::atomic<int> filter_gather{1};    // filtered prefilter scans (VALU sq8_scan) compact the accepted ordinals
                                           // first and scan them (osk_filter.hip); 0 = walk the bitset windows
     std::atomic<int> sq8_mfma_nt{1};      // A/B: non-temporal row loads in sq8_mfma

@@ -339,14 +339,24 @@ __device__ __forceinline__ int rs_base(int t) {
 // dots are reduce-scattered (rs_reduce) so each lane finishes the bound and quick test of P
 // (row, query) pairs instead of all NQ.
 // ------------------------------------------------------------------------------------------------
-// MODE: kScanRows (row-range tiles; a filter is walked 64-row window by window), kScanQueue (single
-// query, filtered: accepted rows of sparse windows queued across windows), kScanGather (filtered: the
-// grid runs over gather tiles of the compacted accepted ordinals, osk_filter.hip).
-constexpr int kScanRows = 0, kScanQueue = 1, kScanGather = 2;
+// MODE: kScanRows (row-range tiles; a filter is walked 64-row window by window: its accepted rows
+// compacted to the front of the wave, one load round trip per non-empty window), kScanGather (filtered:
+// the grid runs over gather tiles of the compacted accepted ordinals, osk_filter.hip — measured faster
+// at every selectivity: C5 1 % 70 → 30 µs, 10 % 227 → 155 µs, 50 % 700 → 663 µs per scan,
+// profiles/r02c/c5f_gather_ab.jsonl; a cross-window queue instance of the window walk was retired).
+constexpr int kScanRows = 0, kScanGather = 2;
 
 // A gather tile's entry range and its scan wave's share: tile j of nj over cnt accepted ordinals, split
-// in 4 contiguous quarters.  The settle re-derives the same ranges for an overflowed list.
-__device__ __forceinline__ void gather_wave_range(int64_t cnt, int j, int nj, int wave, int64_t& b, int64_t& e) {
+// in 4 contiguous quarters.  A sparse filter uses fewer tiles of the segment — at most one per
+// min_entries accepted rows (short wave lists fill with most of their rows, so the settle would
+// re-score most rows) — and the others stay empty.  The settle re-derives the same ranges.
+__device__ __forceinline__ void gather_wave_range(int64_t cnt, int j, int nj, int min_entries, int wave, int64_t& b,
+                                                  int64_t& e) {
+    if (min_entries > 0) nj = (int)max<int64_t>(1, min<int64_t>(nj, (cnt + min_entries - 1) / min_entries));
+    if (j >= nj) {
+        b = e = 0;
+        return;
+    }
     const int64_t e0 = cnt * j / nj, e1 = cnt * (j + 1) / nj;
     const int64_t pw = (e1 - e0 + 3) / 4;
     b = min(e0 + wave * pw, e1);
@@ -354,9 +364,8 @@ __device__ __forceinline__ void gather_wave_range(int64_t cnt, int j, int nj, in
 }
 
 template <int L, int V, int NQ, int U, int MODE = kScanRows>
-__global__ __launch_bounds__(kBlock, MODE == kScanQueue ? 4 : 1) void sq8_scan(Sq8Params p) {
+__global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
     constexpr int R = 64 / L;
-    constexpr bool FQ = MODE == kScanQueue;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int t = lane & (L - 1), g = lane / L;
     TileDev tile;
@@ -569,47 +578,13 @@ __global__ __launch_bounds__(kBlock, MODE == kScanQueue ? 4 : 1) void sq8_scan(S
         // 64 at a time (one coalesced index load, then the rows), any segment layout (dense or sparse)
         // (counts and ordinals are clamped to the segment: a corrupt list can never address outside it)
         int64_t eb, ee;
-        gather_wave_range(min<int64_t>(p.scnt[tile.seg], seg.n_rows), gt.z, gt.w, wave, eb, ee);
+        gather_wave_range(min<int64_t>(p.scnt[tile.seg], seg.n_rows), gt.z, gt.w, p.gather_min, wave, eb, ee);
         const uint32_t* __restrict__ C = p.comp + vbase;
         for (int64_t e0 = eb; e0 < ee; e0 += 64) {
             const int n = (int)min<int64_t>(64, ee - e0);
             const int pos = lane < n ? (int)min<int64_t>(C[e0 + lane], seg.n_rows - 1) : 0;
             for (int i0 = 0; i0 < n; i0 += R * U) process(0, true, i0, n, pos);
         }
-    } else if (FQ && abits && !seg.ord_to_doc) {
-        // filter pushdown, FQ instance: the accepted rows of successive sparse 64-row windows are
-        // queued across windows (lane l holds entry l: the row's offset from wb) and scanned 64 at a
-        // time, so a sparse filter does not pay one load round trip per window.  Its own instance:
-        // the queue costs 4 VGPRs, which would take the unfiltered kernel below 4 waves/SIMD.
-        int qpos = 0, qn = 0;
-        for (int64_t w0 = wb; w0 < we; w0 += 64) {
-            const int64_t word = w0 >> 6;
-            const int sh = (int)(w0 & 63);
-            uint64_t m = abits[word] >> sh;
-            if (sh && (word + 1) * 64 < we) m |= abits[word + 1] << (64 - sh);
-            if (we - w0 < 64) m &= (1ull << (we - w0)) - 1ull;
-            const int n = __popcll(m);
-            if (n == 0) continue;
-            const bool bit = (m >> lane) & 1ull;
-            const int below = __popcll(m & ((1ull << lane) - 1ull));
-            if (qn == 0 && n >= R * U) {   // a dense window with nothing queued: scan it in place
-                const int dst = bit ? below : n + (lane - below);
-                const int pos = __builtin_amdgcn_ds_permute(dst << 2, lane);
-                for (int i0 = 0; i0 < n; i0 += R * U) process(w0, true, i0, n, pos);
-                continue;
-            }
-            if (qn + n > 64) {
-                for (int i0 = 0; i0 < qn; i0 += R * U) process(wb, true, i0, qn, qpos);
-                qn = 0;
-            }
-            // append: set lanes to entries qn + below, the others to the remaining entries (a
-            // bijection mod 64); only entries [qn, qn + n) take the permuted value
-            const int dst = (bit ? qn + below : qn + n + (lane - below)) & 63;
-            const int v = __builtin_amdgcn_ds_permute(dst << 2, (int)(w0 - wb) + lane);
-            if (lane >= qn && lane < qn + n) qpos = v;
-            qn += n;
-        }
-        for (int i0 = 0; i0 < qn; i0 += R * U) process(wb, true, i0, qn, qpos);
     } else if (abits && !seg.ord_to_doc) {
         // filter pushdown: accepted rows of 64 compacted to the front of the wave (see walk_rows)
         for (int64_t w0 = wb; w0 < we; w0 += 64) {
@@ -668,11 +643,6 @@ using Sq8Fn = void (*)(Sq8Params);
 #define OSK_SQ8_ROW(L, V) {sq8_scan<L, V, 1, 4>, sq8_scan<L, V, 2, 4>, sq8_scan<L, V, 4, 4>, sq8_scan<L, V, 8, 2>}
 static const Sq8Fn kSq8[8][4] = {OSK_SQ8_ROW(4, 1),  OSK_SQ8_ROW(8, 1),  OSK_SQ8_ROW(16, 1), OSK_SQ8_ROW(16, 2),
                                  OSK_SQ8_ROW(16, 3), OSK_SQ8_ROW(16, 4), OSK_SQ8_ROW(32, 4), OSK_SQ8_ROW(64, 4)};
-// single-query filtered scans without compaction: the queue instance (cross-window queue of accepted rows)
-static const Sq8Fn kSq8Filtered[8] = {sq8_scan<4, 1, 1, 4, kScanQueue>,  sq8_scan<8, 1, 1, 4, kScanQueue>,
-                                      sq8_scan<16, 1, 1, 4, kScanQueue>, sq8_scan<16, 2, 1, 4, kScanQueue>,
-                                      sq8_scan<16, 3, 1, 4, kScanQueue>, sq8_scan<16, 4, 1, 4, kScanQueue>,
-                                      sq8_scan<32, 4, 1, 4, kScanQueue>, sq8_scan<64, 4, 1, 4, kScanQueue>};
 // filtered scans over the compacted accepted ordinals (gather tiles)
 #define OSK_SQ8_GROW(L, V)                                                                          \
     {sq8_scan<L, V, 1, 4, kScanGather>, sq8_scan<L, V, 2, 4, kScanGather>, sq8_scan<L, V, 4, 4, kScanGather>, \
@@ -686,7 +656,7 @@ hipError_t launch_sq8_scan(int nq, const Sq8Params& p, hipStream_t s, hipEvent_t
     // NQ > 1: the queries and the 4 waves' per-query lists in LDS
     const size_t lds = slot == 0 ? 0 : (size_t)(1 << slot) * (p.units8 * 16 + 4 * kKQ * 12);
     const int c = sq8_cfg(p.units8);
-    const auto fn = p.gtiles ? kSq8Gather[c][slot] : (slot == 0 && p.accept) ? kSq8Filtered[c] : kSq8[c][slot];
+    const auto fn = p.gtiles ? kSq8Gather[c][slot] : kSq8[c][slot];
     if (ev_start || ev_stop)
         hipExtLaunchKernelGGL(fn, dim3(p.n_tiles), dim3(kBlock), lds, s, ev_start, ev_stop, 0, p);
     else
@@ -1200,7 +1170,7 @@ __global__ __launch_bounds__(kSettleThreads) void sq8_settle(SettleParams p) {
         const int4 gt = p.gtiles[list >> 2];
         const SegDev seg = p.segs[gt.x];
         int64_t lb0, lb1;
-        gather_wave_range(min<int64_t>(p.scnt[gt.x], seg.n_rows), gt.z, gt.w, list & 3, lb0, lb1);
+        gather_wave_range(min<int64_t>(p.scnt[gt.x], seg.n_rows), gt.z, gt.w, p.gather_min, list & 3, lb0, lb1);
         const uint32_t* __restrict__ C = p.comp + p.seg_vrow[gt.x];
         const int64_t per_wave = ((lb1 - lb0 + kSettleWaves * R - 1) / (kSettleWaves * R)) * R;
         const int64_t wb = lb0 + wave * per_wave;

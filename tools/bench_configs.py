@@ -79,6 +79,12 @@ def run(view, queries, batch, steps, warmup, accept_ptrs=None, k=10):
     return dt / steps * 1e3, ms.value / max(1, calls.value)
 
 
+def counter(view, name):
+    v = C.c_int64()
+    _lib.check(L.osk_view_counter(view.v, name.encode(), C.byref(v)))
+    return v.value
+
+
 def emit(name, view, batch, ms_step, kernel_ms, bytes_per_launch, extra=None):
     rec = {"config": name, "batch": batch, "qps": batch / (ms_step * 1e-3), "ms_per_batch": ms_step,
            "kernel_ms": kernel_ms, "fp32_equiv_GBps": bytes_per_launch / (kernel_ms * 1e-3) / 1e9,
@@ -101,7 +107,12 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--c4-batches", default="1,1024")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE")
+    ap.add_argument("--c5f-sel", default="0.01,0.1,0.5", help="C5f selectivities")
+    ap.add_argument("--c5f-modes", default="1:0,0:0",
+                    help="C5f filter modes filter_gather:gather_min, comma-separated (1:0 = compacted gather, 0:0 = "
+                         "bitset window walk)")
     a = ap.parse_args()
+    a.c5f_modes = [tuple(int(x) for x in m.split(":")) for m in a.c5f_modes.split(",")]
     for kv in a.tune:
         key, val = kv.split("=")
         _lib.tune(key, int(val))
@@ -126,28 +137,34 @@ def main():
         ms, km = run(v, q, 256, st, wu)
         emit("C2", v, 256, ms, km, 1_000_000 * 128 * 4)
         v.close()
-    if "C3" in only:
+    if "C3" in only or "C5f" in only:
         v = View(8, 1_250_000, 768, _lib.COSINE, _lib.FLOAT32, _lib.DIST_NORMALISH_UNIT)
         q = qpool(512, 768, _lib.DIST_NORMALISH_UNIT)
-        ms, km = run(v, q, 1, st, wu)
-        emit("C3", v, 1, ms, km, 10_000_000 * 768 * 4)
-        ms, km = run(v, q, 256, st, wu)
-        emit("C3", v, 256, ms, km, 10_000_000 * 768 * 4)
+        if "C3" in only:
+            ms, km = run(v, q, 1, st, wu)
+            emit("C3", v, 1, ms, km, 10_000_000 * 768 * 4)
+            ms, km = run(v, q, 256, st, wu)
+            emit("C3", v, 256, ms, km, 10_000_000 * 768 * 4)
         if "C5f" in only:
             rng = np.random.default_rng(44)
-            for sel in [0.01, 0.10, 0.50]:
+            for sel in [float(x) for x in a.c5f_sel.split(",")]:
                 bits = [torch.from_numpy(bits_from_bool(rng.random(1_250_000) < sel).view(np.int64)).cuda()
                         for _ in range(8)]
                 ptrs = torch.tensor([b.data_ptr() for b in bits], dtype=torch.int64, device="cuda")
-                for gmode in (1, 0):   # compacted gather scan (default) vs the bitset window walk
+                for gmode, gmin in a.c5f_modes:   # compacted gather scan vs the bitset window walk
                     _lib.tune("filter_gather", gmode)
+                    _lib.tune("gather_min", gmin)
+                    r0, x0 = counter(v, "sq8_rescored_rows"), counter(v, "sq8_exact_tiles")
                     ms, km = run(v, q, 1, st, wu, accept_ptrs=ptrs)
                     # the prefilter's own bytes: accepted int8 rows + 16-B bound terms + the bitset
                     b8 = int(10_000_000 * sel) * (768 + 16) + 10_000_000 // 8
                     emit(f"C5f-{int(sel * 100)}%", v, 1, ms, km, int(10_000_000 * sel) * 768 * 4 + 10_000_000 // 8,
-                         {"selectivity": sel, "filter_gather": gmode,
+                         {"selectivity": sel, "filter_gather": gmode, "gather_min": gmin,
+                          "rescored_rows_per_query": (counter(v, "sq8_rescored_rows") - r0) / (st + wu),
+                          "exact_lists_per_query": (counter(v, "sq8_exact_tiles") - x0) / (st + wu),
                           "int8_prefilter_GBps": b8 / (km * 1e-3) / 1e9})
                 _lib.tune("filter_gather", 1)
+                _lib.tune("gather_min", 0)
         v.close()
     if "C4" in only:
         v = View(8, 12_500_000, 96, _lib.DOT_PRODUCT, _lib.FLOAT32, _lib.DIST_NORMALISH_UNIT)
