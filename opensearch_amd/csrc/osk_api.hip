@@ -988,7 +988,6 @@ int32_t ensure_gather(osk_view* v, hipStream_t st) {
     OSK_HIP(v->d_gshard_slice_begin.reserve(sizeof(int32_t) * ssb.size()));
     OSK_HIP(v->d_seg_tiles.reserve(sizeof(int2) * ns));
     OSK_HIP(v->ws_tcnt.reserve(sizeof(int32_t) * std::max(1, v->n_tiles)));
-    OSK_HIP(v->ws_tpre.reserve(sizeof(int32_t) * (v->n_tiles + 1)));
     OSK_HIP(v->ws_scnt.reserve(sizeof(int32_t) * ns));
     OSK_HIP(v->ws_comp.reserve(sizeof(uint32_t) * std::max<int64_t>(1, total)));
     if (!gt.empty())
@@ -1087,7 +1086,7 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     p.gam = v->sq8_gam;
     p.g2 = v->sq8_g2;
     p.cos_slack = v->sq8_cos_slack;
-    if (gather) {   // accepted ordinals of every segment, compacted (count, prefix, write)
+    if (gather) {   // accepted ordinals of every segment, compacted (count, then prefix + write)
         FilterParams fp{};
         fp.segs = v->d_segs.as<SegDev>();
         fp.tiles = v->d_tiles.as<TileDev>();
@@ -1095,7 +1094,6 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
         fp.seg_vrow = v->d_seg_vrow.as<int64_t>();
         fp.seg_tiles = v->d_seg_tiles.as<int2>();
         fp.tcnt = v->ws_tcnt.as<int32_t>();
-        fp.tpre = v->ws_tpre.as<int32_t>();
         fp.scnt = v->ws_scnt.as<int32_t>();
         fp.comp = v->ws_comp.as<uint32_t>();
         fp.n_tiles = v->n_tiles;

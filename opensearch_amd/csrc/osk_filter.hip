@@ -10,11 +10,10 @@
 // every row of that segment is accepted.
 //
 //   filt_count   one wave per scan tile: accepted rows of the tile's row range  → tcnt[tile]
-//   filt_scan    one workgroup: exclusive prefix of tcnt over the tile table → tpre[tile], and per
-//                segment the accepted count scnt[seg] (a segment's tiles are contiguous in the table:
-//                seg_tiles[seg] = [first, end))
-//   filt_write   one wave per scan tile: its accepted ordinals, ascending, at
-//                comp[seg_vrow[seg] + tpre[tile] − tpre[first tile of seg] + i]
+//   filt_write   one wave per scan tile: its offset in the segment's list (Σ tcnt of the segment's
+//                earlier tiles; a segment's tiles are contiguous in the table, seg_tiles[seg] =
+//                [first, end)), then its accepted ordinals, ascending, at comp[seg_vrow[seg] + offset + i];
+//                the segment's last tile writes the segment's count scnt[seg]
 // comp therefore holds, for segment g, scnt[g] ascending ordinals starting at its view row seg_vrow[g].
 #include "osk_internal.h"
 #include "osk_wave.h"
@@ -38,9 +37,12 @@ __device__ __forceinline__ uint64_t window_mask(const uint64_t* abits, int64_t w
     return m;
 }
 
-__global__ __launch_bounds__(64) void filt_count(FilterParams p) {
-    const int lane = threadIdx.x;
-    const TileDev t = p.tiles[blockIdx.x];
+// one wave per tile, 4 tiles per workgroup (6k one-wave workgroups dispatch slower than 1.5k of four)
+__global__ __launch_bounds__(256) void filt_count(FilterParams p) {
+    const int lane = threadIdx.x & 63;
+    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile >= p.n_tiles) return;
+    const TileDev t = p.tiles[tile];
     const SegDev seg = p.segs[t.seg];
     const uint64_t* abits = p.accept[t.seg];
     int64_t n = 0;
@@ -54,65 +56,68 @@ __global__ __launch_bounds__(64) void filt_count(FilterParams p) {
         for (int64_t r = t.row_begin + lane; r < t.row_end; r += 64) n += accepted(abits, seg.ord_to_doc, r);
     }
     for (int o = 32; o >= 1; o >>= 1) n += __shfl_xor(n, o);
-    if (lane == 0) p.tcnt[blockIdx.x] = (int32_t)n;
+    if (lane == 0) p.tcnt[tile] = (int32_t)n;
 }
 
-// exclusive prefix of tcnt[0, n_tiles] (tpre[n_tiles] = total) in chunks of 1024 with a carry
-__global__ __launch_bounds__(1024) void filt_scan(FilterParams p) {
-    __shared__ int32_t s_w[16];
-    __shared__ int32_t s_carry;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid == 0) s_carry = 0;
-    __syncthreads();
-    for (int base = 0; base <= p.n_tiles; base += 1024) {
-        const int i = base + tid;
-        const int32_t v = i < p.n_tiles ? p.tcnt[i] : 0;
-        int32_t x = v;   // inclusive wave scan
-        for (int o = 1; o < 64; o <<= 1) {
-            const int32_t y = __shfl_up(x, o);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) s_w[wave] = x;
-        __syncthreads();
-        if (wave == 0) {
-            int32_t w = lane < 16 ? s_w[lane] : 0;
-            for (int o = 1; o < 16; o <<= 1) {
-                const int32_t y = __shfl_up(w, o);
-                if (lane >= o) w += y;
-            }
-            if (lane < 16) s_w[lane] = w;   // inclusive over waves
-        }
-        __syncthreads();
-        const int32_t carry = s_carry;
-        const int32_t excl = carry + (wave ? s_w[wave - 1] : 0) + x - v;
-        if (i <= p.n_tiles) p.tpre[i] = excl;
-        __syncthreads();
-        if (tid == 1023) s_carry = excl + v;
-        __syncthreads();
-    }
-    // per segment: accepted count = prefix at its tile end − prefix at its tile begin
-    for (int g = tid; g < p.n_segs; g += 1024)
-        p.scnt[g] = p.tpre[p.seg_tiles[g].y] - p.tpre[p.seg_tiles[g].x];
-}
-
-__global__ __launch_bounds__(64) void filt_write(FilterParams p) {
-    const int lane = threadIdx.x;
-    const TileDev t = p.tiles[blockIdx.x];
+__global__ __launch_bounds__(256) void filt_write(FilterParams p) {
+    const int lane = threadIdx.x & 63;
+    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile >= p.n_tiles) return;
+    const TileDev t = p.tiles[tile];
     const SegDev seg = p.segs[t.seg];
     const uint64_t* abits = p.accept[t.seg];
-    uint32_t* out = p.comp + p.seg_vrow[t.seg] + (p.tpre[blockIdx.x] - p.tpre[p.seg_tiles[t.seg].x]);
-    int64_t o = 0;
-    for (int64_t w0 = t.row_begin; w0 < t.row_end; w0 += 64) {
-        uint64_t m;
-        if (!abits) {
-            m = t.row_end - w0 >= 64 ? ~0ull : (1ull << (t.row_end - w0)) - 1ull;
-        } else if (!seg.ord_to_doc) {
-            m = window_mask(abits, w0, t.row_end);
-        } else {
-            m = __ballot(w0 + lane < t.row_end && accepted(abits, seg.ord_to_doc, w0 + lane));
+    // this tile's offset inside its segment's list = Σ counts of the segment's earlier tiles (≤ a few
+    // hundred L2-resident ints: cheaper than a separate prefix launch); the segment's last tile
+    // publishes the segment's total
+    const int2 st = p.seg_tiles[t.seg];
+    int64_t off = 0;
+    const int n_before = tile - st.x;
+    for (int b = 0; b < n_before; b += 64 * 8) {   // 8 independent loads in flight per lane
+        int v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int u = b + j * 64 + lane;
+            v[j] = u < n_before ? p.tcnt[st.x + u] : 0;
         }
-        if ((m >> lane) & 1ull) out[o + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)(w0 + lane);
-        o += __popcll(m);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) off += v[j];
+    }
+    for (int o = 32; o >= 1; o >>= 1) off += __shfl_xor(off, o);
+    if (lane == 0 && tile == st.y - 1) p.scnt[t.seg] = (int32_t)(off + p.tcnt[tile]);
+    uint32_t* out = p.comp + p.seg_vrow[t.seg];
+    if (abits && seg.ord_to_doc) {   // sparse field: accept by doc, one 64-row window per step
+        for (int64_t w0 = t.row_begin; w0 < t.row_end; w0 += 64) {
+            const uint64_t m = __ballot(w0 + lane < t.row_end && accepted(abits, seg.ord_to_doc, w0 + lane));
+            if ((m >> lane) & 1ull) out[off + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)(w0 + lane);
+            off += __popcll(m);
+        }
+        return;
+    }
+    // dense field: lane w loads the mask of window w of this pass of 64 windows (one load round trip),
+    // a wave scan of their popcounts gives every window's output position, then the windows are
+    // written one after the other from registers (no load in the loop)
+    for (int64_t pb = t.row_begin; pb < t.row_end; pb += 64 * 64) {
+        const int64_t w0 = pb + (int64_t)lane * 64;
+        uint64_t m = 0ull;
+        if (w0 < t.row_end) {
+            const int64_t left = t.row_end - w0;
+            m = abits ? window_mask(abits, w0, t.row_end) : (left >= 64 ? ~0ull : (1ull << left) - 1ull);
+        }
+        const int c = __popcll(m);
+        int incl = c;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        const int excl = incl - c;
+        const int nw = (int)min<int64_t>(64, (t.row_end - pb + 63) / 64);
+        for (int w = 0; w < nw; ++w) {
+            const uint64_t mw = readlane64(m, w);
+            const int base = __builtin_amdgcn_readlane(excl, w);
+            if ((mw >> lane) & 1ull)
+                out[off + base + __popcll(mw & ((1ull << lane) - 1ull))] = (uint32_t)(pb + (int64_t)w * 64 + lane);
+        }
+        off += __builtin_amdgcn_readlane(incl, 63);
     }
 }
 
@@ -120,9 +125,9 @@ __global__ __launch_bounds__(64) void filt_write(FilterParams p) {
 
 hipError_t launch_filter_compact(const FilterParams& p, hipStream_t s) {
     if (p.n_tiles <= 0) return hipSuccess;
-    hipLaunchKernelGGL(filt_count, dim3(p.n_tiles), dim3(64), 0, s, p);
-    hipLaunchKernelGGL(filt_scan, dim3(1), dim3(1024), 0, s, p);
-    hipLaunchKernelGGL(filt_write, dim3(p.n_tiles), dim3(64), 0, s, p);
+    const unsigned grid = (unsigned)((p.n_tiles + 3) / 4);
+    hipLaunchKernelGGL(filt_count, dim3(grid), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(filt_write, dim3(grid), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 

@@ -205,7 +205,6 @@ struct FilterParams {
     const int64_t* seg_vrow;            // view row of each segment's ord 0
     const int2* seg_tiles;              // per segment: [first tile, end tile) in the tile table
     int32_t* tcnt;                      // [n_tiles] accepted rows per tile
-    int32_t* tpre;                      // [n_tiles + 1] exclusive prefix of tcnt
     int32_t* scnt;                      // [n_segs] accepted rows per segment
     uint32_t* comp;                     // [view rows] compacted ordinals
     int n_tiles;

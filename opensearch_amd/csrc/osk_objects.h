@@ -185,7 +185,7 @@ struct osk_view {
     bool gather_ready = false;
     int n_gtiles = 0, n_gslices = 0;
     osk::DevBuf d_gtiles, d_gslices, d_gshard_slice_begin, d_seg_tiles;
-    osk::DevBuf ws_tcnt, ws_tpre, ws_scnt, ws_comp;
+    osk::DevBuf ws_tcnt, ws_scnt, ws_comp;
     // multi-GPU exchange (osk_comm.hip): this rank's lists padded to the comm's shards per rank, the
     // gathered image of every rank, and the shardIndex of every gathered slot (exchanged once per comm)
     osk::DevBuf ws_xkeys, ws_xgath, d_xsi, ws_xout;
