@@ -54,7 +54,7 @@ extern "C" {
 #endif
 
 #define OSK_ABI_VERSION 2
-#define OSK_MAX_K       64   /* largest k (and from+size) the device path serves in this build */
+#define OSK_MAX_K       10000 /* largest k: index.max_result_window (S/index/IndexSettings.java:223-226) */
 #define OSK_MAX_DIM     4096
 
 /* ---- return codes ---- */

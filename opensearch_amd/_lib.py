@@ -22,7 +22,7 @@ OSK_ERR_DEVICE = -2
 OSK_ERR_OOM = -3
 OSK_ERR_UNSUPPORTED = -4
 OSK_ERR_NO_DEVICE = -5
-OSK_MAX_K = 64
+OSK_MAX_K = 10000
 OSK_MAX_DIM = 4096
 OSK_COMM_ID_BYTES = 128
 

@@ -27,8 +27,8 @@ LIB_TESTING = PKG / "libosknn_testing.so"
 TESTING_VARIANT = "osk_api.hip"   # the only source whose object differs in the testing build
 OBJDIR = ROOT / "build" / "osknn"
 
-SOURCES = ["osk_kernels.hip", "osk_mfma.hip", "osk_sq8.hip", "osk_filter.hip", "osk_api.hip", "osk_comm.hip", "osk_host.cpp"]
-HEADERS = ["osk_common.h", "osk_internal.h", "osk_wave.h", "osk_objects.h"]
+SOURCES = ["osk_kernels.hip", "osk_mfma.hip", "osk_sq8.hip", "osk_filter.hip", "osk_select.hip", "osk_api.hip", "osk_comm.hip", "osk_host.cpp"]
+HEADERS = ["osk_common.h", "osk_internal.h", "osk_wave.h", "osk_objects.h", "osk_device.h"]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"

@@ -238,6 +238,7 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         {"mfma_units", &g_tuning.mfma_units, 1, 32768, false},
         {"sq8", &g_tuning.sq8, 0, 1, false},
         {"filter_gather", &g_tuning.filter_gather, 0, 1, false},
+        {"select_mid_k", &g_tuning.select_mid_k, 0, 1, false},
         {"gather_min", &g_tuning.gather_min, 0, 1 << 20, false},
         {"sq8_mfma_nt", &g_tuning.sq8_mfma_nt, 0, 1, false},
         {"sq8_mfma_queries", &g_tuning.sq8_mfma_queries, 16, 32, false},
@@ -1185,6 +1186,108 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     return OSK_OK;
 }
 
+// The select path (osk_select.hip): exact top-k for any k ≤ OSK_MAX_K, one query at a time.
+//   bounds = true: float32 fields through the int8 prefilter copy (bounds → threshold → candidates →
+//   exact re-score); a query with a shard whose candidates overflow kSelCap is answered again in exact
+//   mode (exact fp32 keys → threshold → the top k).  bounds = false: exact mode (float32 with the
+//   prefilter off, byte vectors).  ws_q / ws_qnorm hold the padded queries (exact mode: the caller's
+//   launch_prep_queries; bounds mode: sq8_prep here).
+int32_t select_search(osk_view* v, const void* d_queries, int nq, int k, int UP, const uint64_t* const* d_accept,
+                      uint64_t* d_shard_keys, int32_t* d_shard_counts, int64_t* d_visited, hipStream_t st,
+                      bool bounds) {
+    const int S = v->n_shards;
+    int64_t total = 0;
+    for (osk_seg* sg : v->segs) total += sg->n_rows;
+    const int nq_pad = (nq + kMaxNQ - 1) / kMaxNQ * kMaxNQ;
+    int u8 = 0;
+    if (bounds) {
+        int32_t rc = ensure_sq8(v, st);
+        if (rc) return rc;
+        u8 = v->units8;
+        OSK_HIP(v->ws_q8.reserve((size_t)nq_pad * u8 * 16));
+        OSK_HIP(v->ws_qc.reserve(sizeof(float4) * nq_pad));
+        OSK_HIP(v->ws_flags.reserve(sizeof(int) * nq));
+        OSK_HIP(launch_sq8_prep(v->cfg, static_cast<const float*>(d_queries), v->dim, nq, nq_pad, UP, u8,
+                                v->ws_q.as<float4>(), v->ws_qnorm.as<float>(), v->ws_q8.p, v->ws_qc.as<float4>(),
+                                v->ws_flags.as<int>(), st));
+        OSK_HIP(v->ws_sel_lb.reserve(sizeof(uint32_t) * std::max<int64_t>(1, total)));
+        OSK_HIP(v->ws_sel_ub.reserve(sizeof(uint32_t) * std::max<int64_t>(1, total)));
+    } else {
+        if (v->enc == ENC_FLOAT32 && v->sim == SIM_COSINE)
+            OSK_HIP(launch_row_norms_f32(v->ws_q.as<float4>(), nq, UP, v->cfg, v->ws_qnorm.as<float>(), st));
+        OSK_HIP(v->ws_flags.reserve(sizeof(int) * nq));
+        OSK_HIP(hipMemsetAsync(v->ws_flags.p, 0, sizeof(int) * nq, st));
+        OSK_HIP(v->ws_sel_keys.reserve(sizeof(uint64_t) * std::max<int64_t>(1, total)));
+    }
+    OSK_HIP(v->ws_sel_state.reserve(sizeof(RadixState) * S));
+    OSK_HIP(v->ws_sel_hist.reserve(sizeof(uint32_t) * 256 * S));
+    OSK_HIP(v->ws_sel_cand.reserve(sizeof(uint64_t) * (size_t)kSelCap * S));
+    OSK_HIP(v->ws_sel_cnt.reserve(sizeof(int32_t) * S));
+    SelParams p{};
+    p.segs = v->d_segs.as<SegDev>();
+    p.tiles = v->d_tiles.as<TileDev>();
+    p.seg_vrow = v->d_seg_vrow.as<int64_t>();
+    p.accept = d_accept;
+    p.n_tiles = v->n_tiles;
+    p.n_shards = S;
+    p.n_segs = (int)v->segs.size();
+    p.k = k;
+    p.sim = v->sim;
+    p.dim = v->dim;
+    p.units = v->units;
+    p.units8 = u8;
+    p.enc = v->enc;
+    p.rows8 = v->d_sq8_rows.as<const int4*>();
+    p.aux = v->d_sq8_aux.as<const float4*>();
+    p.gam = v->sq8_gam;
+    p.g2 = v->sq8_g2;
+    p.lb = v->ws_sel_lb.as<uint32_t>();
+    p.ub = v->ws_sel_ub.as<uint32_t>();
+    p.keys = v->ws_sel_keys.as<uint64_t>();
+    p.state = v->ws_sel_state.as<RadixState>();
+    p.hist = v->ws_sel_hist.as<uint32_t>();
+    p.cand = v->ws_sel_cand.as<uint64_t>();
+    p.cand_count = v->ws_sel_cnt.as<int32_t>();
+    p.cap = kSelCap;
+    auto one = [&](int q, bool exact) -> int32_t {
+        p.exact = exact ? 1 : 0;
+        p.q = v->ws_q.as<char>() + (size_t)q * UP * 16;
+        p.qnorm = v->ws_qnorm.as<float>() + q;
+        p.q8 = v->ws_q8.as<int4>() + (size_t)q * u8;
+        p.qc = v->ws_qc.as<float4>() + q;
+        p.out_keys = d_shard_keys + (size_t)q * S * k;
+        p.out_counts = d_shard_counts + (size_t)q * S;
+        p.flag = v->ws_flags.as<int>() + q;
+        p.visited = q == 0 ? reinterpret_cast<unsigned long long*>(d_visited) : nullptr;
+        OSK_HIP(launch_select_one(p, v->cfg, st, v->profile && q == 0 ? v->ev0 : nullptr,
+                                  v->profile && q == nq - 1 ? v->ev1 : nullptr));
+        return OSK_OK;
+    };
+    for (int q = 0; q < nq; ++q) {
+        int32_t rc = one(q, !bounds);
+        if (rc) return rc;
+    }
+    v->sel_calls += 1;
+    if (!bounds) return OSK_OK;
+    // a shard whose candidates overflowed kSelCap flagged its query: answer it in exact mode
+    OSK_HIP(v->h_sel_flags.reserve(sizeof(int) * nq));
+    OSK_HIP(hipMemcpyAsync(v->h_sel_flags.p, v->ws_flags.p, sizeof(int) * nq, hipMemcpyDeviceToHost, st));
+    OSK_HIP(hipStreamSynchronize(st));
+    const int* fl = static_cast<const int*>(v->h_sel_flags.p);
+    for (int q = 0; q < nq; ++q) {
+        if (!fl[q]) continue;
+        OSK_HIP(v->ws_sel_keys.reserve(sizeof(uint64_t) * std::max<int64_t>(1, total)));
+        p.keys = v->ws_sel_keys.as<uint64_t>();
+        const bool prof = v->profile;
+        v->profile = false;
+        int32_t rc = one(q, true);
+        v->profile = prof;
+        if (rc) return rc;
+        v->sel_exact_queries += 1;
+    }
+    return OSK_OK;
+}
+
 }  // namespace
 
 namespace osk {
@@ -1230,23 +1333,30 @@ int32_t view_search_device(osk_view* v, const void* d_queries, int nq, int k,
     OSK_HIP(v->ws_qnorm.reserve(sizeof(float) * nq_pad));
     // bf16×3 works in blocks of 256 queries; the int8 prefilter (k ≤ kKQ − 4) costs ≈ sq8_cost_pct % of a
     // bf16×3 block per 256 queries (C3: 32 queries per 2.5 ms launch vs 11.5 ms per 256-query block)
-    const bool sq8_ok = v->enc == ENC_FLOAT32 && g_tuning.sq8 && k <= kKQ - 4;
+    const bool sq8_on = v->enc == ENC_FLOAT32 && g_tuning.sq8;
+    const bool sq8_ok = sq8_on && k <= kKQ - 4;
     const bool blocks_cheaper = (int64_t)((nq + 255) / 256) * 256 * 100 <= (int64_t)nq * g_tuning.sq8_cost_pct;
     const bool batched = v->enc == ENC_FLOAT32 && g_tuning.mfma_min_batch > 0 &&
                          nq >= g_tuning.mfma_min_batch && k <= kKC - 4 && (!sq8_ok || blocks_cheaper);
     // k ≤ kKQ − 4: a tile list holds 4 more rows than k, so it rarely overflows past the certificate
-    const bool prefilter = !batched && v->enc == ENC_FLOAT32 && g_tuning.sq8 && k <= kKQ - 4;
+    const bool prefilter = !batched && sq8_ok;
+    // the select path: k beyond the streaming scans' 64-lane lists, or float32 k beyond the prefilter's
+    // lists (its int8 bounds pass reads ¼ of the fp32 scan's bytes)
+    const bool select = !batched && !prefilter && (k > kScanMaxK || (sq8_on && k > kKQ - 4 && g_tuning.select_mid_k));
     // queries → padded unit layout (zeros past dim and for the dummy queries of the last launch); the
-    // prefilter path does this inside its own fused prep launch
-    if (!prefilter)
+    // prefilter path does this inside its own fused prep launch (so does the select path's bounds mode)
+    if (!prefilter && !(select && sq8_on))
         OSK_HIP(launch_prep_queries(d_queries, (int64_t)v->dim * elem, nq, v->ws_q.p, UP, nq_pad, st));
 
     if (d_visited) OSK_HIP(hipMemsetAsync(d_visited, 0, sizeof(int64_t) * v->segs.size(), st));
 
     int32_t rc;
-    if (prefilter && (rc = ensure_sq8(v, st)) != OSK_OK) return rc;   // one-time build, outside the timing
+    if ((prefilter || (select && sq8_on)) && (rc = ensure_sq8(v, st)) != OSK_OK) return rc;   // one-time build
     if (v->profile && (rc = profile_begin(v, st, batched)) != OSK_OK) return rc;
-    if (prefilter) {
+    if (select) {
+        rc = select_search(v, d_queries, nq, k, UP, d_accept, d_shard_keys, d_shard_counts, d_visited, st, sq8_on);
+        if (rc == OSK_OK) rc = profile_end(v, st, false);
+    } else if (prefilter) {
         rc = sq8_search(v, d_queries, nq, k, UP, d_accept, d_shard_keys, d_shard_counts, d_visited, st);
     } else if (batched) {
         // |q|² in the device lane layout: approx transforms, the re-score (COSINE) and the bound
@@ -1289,15 +1399,13 @@ int32_t osk_merge_device(int32_t device, const uint64_t* d_shard_keys, const int
     OSK_REQUIRE(n_queries >= 1 && n_shards >= 1, "n_queries and n_shards must be >= 1");
     OSK_REQUIRE(k >= 1 && k <= OSK_MAX_K, "k must be in [1, OSK_MAX_K]");
     OSK_REQUIRE(from >= 0 && size >= 1 && (int64_t)from + size <= 100000, "bad from/size");
-    OSK_REQUIRE((int64_t)n_shards * std::min(k, from + size) <= 4096,
-                "n_shards * min(k, from+size) exceeds 4096 hits per query");
     OSK_REQUIRE(d_shard_keys && d_shard_counts && d_shard_index && d_scores && d_docs && d_shard_out &&
                     d_count && d_total_hits && d_max_score,
                 "null device buffer");
     int32_t rc = check_device(device);
     if (rc) return rc;
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : device_stream(device);
-    OSK_HIP(launch_merge_coord(d_shard_keys, d_shard_counts, d_shard_index, n_queries, 1, n_shards, k,
+    OSK_HIP(launch_coord_reduce(d_shard_keys, d_shard_counts, d_shard_index, n_queries, 1, n_shards, k,
                                from, size, d_scores, d_docs, d_shard_out, d_count, d_total_hits,
                                d_max_score, st));
     return OSK_OK;
@@ -1315,15 +1423,13 @@ int32_t osk_merge_device_ranked(int32_t device, const uint64_t* d_keys, int32_t 
                 "n_queries, n_ranks and shards_per_rank must be >= 1");
     OSK_REQUIRE(k >= 1 && k <= OSK_MAX_K, "k must be in [1, OSK_MAX_K]");
     OSK_REQUIRE(from >= 0 && size >= 1 && (int64_t)from + size <= 100000, "bad from/size");
-    OSK_REQUIRE((int64_t)n_ranks * shards_per_rank * std::min(k, from + size) <= 4096,
-                "n_shards * min(k, from+size) exceeds 4096 hits per query");
     OSK_REQUIRE(d_keys && d_shard_index && d_scores && d_docs && d_shard_out && d_count && d_total_hits &&
                     d_max_score,
                 "null device buffer");
     int32_t rc = check_device(device);
     if (rc) return rc;
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : device_stream(device);
-    OSK_HIP(launch_merge_coord(d_keys, nullptr, d_shard_index, n_queries, n_ranks, shards_per_rank, k, from,
+    OSK_HIP(launch_coord_reduce(d_keys, nullptr, d_shard_index, n_queries, n_ranks, shards_per_rank, k, from,
                                size, d_scores, d_docs, d_shard_out, d_count, d_total_hits, d_max_score, st));
     return OSK_OK;
     OSK_GUARD_END
@@ -1399,6 +1505,8 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
     if (n == "mfma_calls") *value = v->mfma_calls;
     else if (n == "mfma_fallback_queries") *value = v->mfma_fallback_queries;
     else if (n == "sq8_calls") *value = v->sq8_calls;
+    else if (n == "select_calls") *value = v->sel_calls;
+    else if (n == "select_exact_queries") *value = v->sel_exact_queries;
     else if (n == "sq8_slices")
         *value = v->n_slices;
     else if (n == "sq8_fallback_queries" || n == "sq8_rescored_rows" || n == "sq8_exact_tiles") {
@@ -1441,8 +1549,6 @@ int32_t osk_view_search(osk_view* v, const void* queries, int32_t n_queries, int
                 "null output");
     OSK_REQUIRE(n_queries >= 1, "n_queries must be >= 1");
     OSK_REQUIRE(from >= 0 && size >= 1, "bad from/size");
-    OSK_REQUIRE((int64_t)v->n_shards * std::min(k, from + size) <= 4096,
-                "n_shards * min(k, from+size) exceeds 4096 hits per query");
     int32_t rc = check_device(v->device);
     if (rc) return rc;
     hipStream_t st = device_stream(v->device);
@@ -1493,7 +1599,7 @@ int32_t osk_view_search(osk_view* v, const void* queries, int32_t n_queries, int
                  total_b = o_max + b_max;
     OSK_HIP(v->ws_out.reserve(total_b));
     char* ob = v->ws_out.as<char>();
-    OSK_HIP(launch_merge_coord(v->ws_keys.as<uint64_t>(), v->ws_counts.as<int32_t>(),
+    OSK_HIP(launch_coord_reduce(v->ws_keys.as<uint64_t>(), v->ws_counts.as<int32_t>(),
                                v->d_shard_index.as<int32_t>(), nq, 1, S, k, from, size,
                                reinterpret_cast<float*>(ob + o_sc), reinterpret_cast<int32_t*>(ob + o_doc),
                                reinterpret_cast<int32_t*>(ob + o_sh), reinterpret_cast<int32_t*>(ob + o_cnt),

@@ -183,8 +183,6 @@ int32_t check_merge_args(const osk_comm* c, int nq, int k, int from, int size, i
     OSK_REQUIRE(k >= 1 && k <= OSK_MAX_K, "k must be in [1, OSK_MAX_K]");
     OSK_REQUIRE(from >= 0 && size >= 1 && (int64_t)from + size <= 100000, "bad from/size");
     OSK_REQUIRE(spr >= 1, "shards_per_rank must be >= 1");
-    OSK_REQUIRE((int64_t)c->world * spr * std::min(k, from + size) <= 4096,
-                "world * shards_per_rank * min(k, from+size) exceeds 4096 hits per query");
     return OSK_OK;
 }
 
@@ -335,7 +333,7 @@ int32_t osk_shards_search_merge_device(osk_comm* comm, osk_view* view, const voi
         if (rc) return rc;
         image = view->ws_xgath.as<uint64_t>();
     }
-    OSK_HIP(launch_merge_coord(image, nullptr, view->d_xsi.as<int32_t>(), n_queries, comm->world, shards_per_rank, k,
+    OSK_HIP(launch_coord_reduce(image, nullptr, view->d_xsi.as<int32_t>(), n_queries, comm->world, shards_per_rank, k,
                                from, size, d_scores, d_docs, d_shard_out, d_count, d_total_hits, d_max_score, st));
     return OSK_OK;
     OSK_GUARD_END
@@ -432,7 +430,7 @@ int32_t osk_shards_search_merge(osk_comm* comm, osk_view* const* views, int32_t 
                  o_tot = (o_cnt + b_cnt + 7) / 8 * 8, o_max = o_tot + b_tot, total_b = o_max + b_max;
     OSK_HIP(v0->ws_xout.reserve(total_b));
     char* ob = v0->ws_xout.as<char>();
-    OSK_HIP(launch_merge_coord(image, nullptr, v0->d_xsi.as<int32_t>(), n_queries, comm->world, spr, k, from, size,
+    OSK_HIP(launch_coord_reduce(image, nullptr, v0->d_xsi.as<int32_t>(), n_queries, comm->world, spr, k, from, size,
                                reinterpret_cast<float*>(ob + o_sc), reinterpret_cast<int32_t*>(ob + o_doc),
                                reinterpret_cast<int32_t*>(ob + o_sh), reinterpret_cast<int32_t*>(ob + o_cnt),
                                reinterpret_cast<int64_t*>(ob + o_tot), reinterpret_cast<float*>(ob + o_max), sts[0]));

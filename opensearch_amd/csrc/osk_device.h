@@ -1,0 +1,94 @@
+// osk_device.h — device helpers shared by the prefilter (osk_sq8.hip) and the large-k select path
+// (osk_select.hip): the certified bound of an int8 dot, the exact fp32 score in the streaming scan's
+// lane order, and global-address-space loads.
+#pragma once
+#include "osk_internal.h"
+
+namespace osk {
+
+__device__ __forceinline__ float f32_round_up(double d) {   // d ≥ 0: smallest float ≥ d
+    float f = (float)d;
+    if ((double)f < d) f = __uint_as_float(__float_as_uint(f) + 1u);
+    return f;
+}
+
+// ------------------------------------------------------------------------------------------------
+// bounds
+// ------------------------------------------------------------------------------------------------
+// [lo, hi] ∋ the raw value the fp32 streaming scan computes for (row, query): its dot product
+// (DOT_PRODUCT / COSINE / MAXIMUM_INNER_PRODUCT) or its squared distance (EUCLIDEAN).
+//   x·b = s_x·s_b·I + e,  |e| ≤ s_x|q_x|·|δ_b| + |δ_x|·(s_b|q_b| + |δ_b|) = ax.y·qc.y + ax.z·qc.z
+//   dot:  |dot_dev − x·b| ≤ γ_n·|x||b| ≤ gam·(|x|² + |b|²)
+//   d²:   d² = |x|² + |b|² − 2x·b,  |d²_dev − d²| ≤ g2·d²
+// Every float operation below rounds by ≤ 2^-24 relative; the 2^-20 slack covers all of them.
+__device__ __forceinline__ void sq8_bounds(int sim, float I, float4 ax, float4 qc, float gam, float g2,
+                                           float& lo, float& hi) {
+    const float approx = I * (ax.x * qc.x);
+    const float eq = fmaf(ax.y, qc.y, ax.z * qc.z);
+    if (sim == SIM_EUCLIDEAN) {
+        const float base = ax.w + qc.w;
+        const float sl = 0x1p-20f * (base + 2.0f * (fabsf(approx) + eq));
+        const float d2lo = base - 2.0f * (approx + eq) - sl;
+        const float d2hi = base - 2.0f * (approx - eq) + sl;
+        lo = fmaxf(d2lo, 0.0f) * (1.0f - g2);
+        hi = d2hi * (1.0f + g2);
+    } else {
+        const float e = eq + gam * (ax.w + qc.w);
+        const float sl = 0x1p-20f * (fabsf(approx) + e);
+        hi = approx + e + sl;
+        lo = approx - e - sl;
+    }
+}
+
+// Global-address-space loads (global_load, not flat_load): a flat load also counts in lgkmcnt, so
+// the first LDS read after it would wait for every row load in flight, prefetched ones included.
+__device__ __forceinline__ int4 load_i4_g(const int4* p, bool nt) {
+    typedef int i4v __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) const i4v gi4v;
+    const gi4v* g = (const gi4v*)p;
+    const i4v v = nt ? __builtin_nontemporal_load(g) : *g;
+    return make_int4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float4 load_f4_g(const float4* p) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) const f4v gf4v;
+    const f4v v = *(const gf4v*)p;
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ int4 load_i4_nt(const int4* p) {
+    typedef int i4v __attribute__((ext_vector_type(4)));
+    const i4v v = __builtin_nontemporal_load(reinterpret_cast<const i4v*>(p));
+    return make_int4(v.x, v.y, v.z, v.w);
+}
+
+// (kept in the scan's lane layout: L lanes per row, V float4 per lane, 4 fma chains, pairwise tree)
+// exact score of one row (the streaming scan's arithmetic: same lane layout and fma order)
+template <int L, int V, bool L2K>
+__device__ __forceinline__ float settle_exact(const float4* xr, bool valid, int units, int t,
+                                              const float4 (&qf)[V], int sim, float qn, float xn) {
+    float4 xv[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+        const int f = t + j * L;
+        xv[j] = (valid && f < units) ? xr[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float ax = 0.f, ay = 0.f, az = 0.f, aw = 0.f;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+        const float4 x = xv[j];
+        if constexpr (L2K) {
+            const float dx = x.x - qf[j].x, dy = x.y - qf[j].y, dz = x.z - qf[j].z, dw = x.w - qf[j].w;
+            ax = fmaf(dx, dx, ax); ay = fmaf(dy, dy, ay); az = fmaf(dz, dz, az); aw = fmaf(dw, dw, aw);
+        } else {
+            ax = fmaf(x.x, qf[j].x, ax); ay = fmaf(x.y, qf[j].y, ay);
+            az = fmaf(x.z, qf[j].z, az); aw = fmaf(x.w, qf[j].w, aw);
+        }
+    }
+    float sum = (ax + ay) + (az + aw);
+#pragma unroll
+    for (int m = 1; m < L; m <<= 1) sum += __shfl_xor(sum, m);
+    if constexpr (L2K) return score_f32_l2(sum);
+    else return score_f32(sim, sum, qn, xn);
+}
+
+}  // namespace osk

@@ -47,6 +47,7 @@ struct ScanParams {
 
 constexpr int kBlock = 256;          // 4 wavefronts per workgroup
 constexpr int kMaxNQ = 8;            // queries per streaming-scan launch
+constexpr int kScanMaxK = 64;        // k the streaming scans' wave lists hold (beyond: the select path)
 constexpr int kKsAlign = 4;        // MFMA K-steps (32 dims) per segment split copy: a multiple of this
 constexpr int kKC = 16;              // candidates per (query, shard) of the batched MFMA path (k ≤ kKC − 4)
 
@@ -212,6 +213,57 @@ struct FilterParams {
 };
 hipError_t launch_filter_compact(const FilterParams& p, hipStream_t s);
 
+// ---- the select path: exact top-k for any k ≤ OSK_MAX_K (osk_select.hip) ----
+constexpr int kSelCap = 16384;       // candidates per (query, shard) the select path sorts in LDS
+struct RadixState {
+    uint64_t prefix;                 // the digits of the k-th largest value decided so far
+    int32_t krem;                    // its rank among the values that share them
+    int32_t all;                     // ≤ k accepted rows: take every one
+    int32_t pad;
+};
+struct SelParams {
+    const SegDev* segs;
+    const TileDev* tiles;
+    const int64_t* seg_vrow;
+    const uint64_t* const* accept;
+    unsigned long long* visited;     // [n_segs] or null
+    int n_tiles, n_shards, n_segs;
+    int k, sim, dim, units, units8, enc;
+    int exact;                       // 1: 64-bit keys of exact scores; 0: int8 bounds LB/UB + exact re-score
+    const void* q;                   // this query, padded (fp32 UP float4 / int8 16-B units)
+    const float* qnorm;              // its |q|² in the device lane order (COSINE)
+    const int4* q8;                  // bounds mode: its int8 copy and bound terms
+    const float4* qc;
+    const int4* const* rows8;
+    const float4* const* aux;
+    float gam, g2;
+    uint32_t* lb;                    // bounds mode, [view rows]
+    uint32_t* ub;
+    uint64_t* keys;                  // exact mode, [view rows]
+    RadixState* state;               // [n_shards]
+    uint32_t* hist;                  // [n_shards][256]
+    uint64_t* cand;                  // [n_shards][cap]
+    int32_t* cand_count;             // [n_shards]
+    int cap;
+    uint64_t* out_keys;              // this query's [n_shards][k]
+    int32_t* out_counts;             // [n_shards]
+    int* flag;                       // this query's flag: set on a bounds-mode overflow
+};
+// one query: writer → radix select → collect → (re-score) → sort; cfg = the view's fp32/byte lane cfg
+hipError_t launch_select_one(const SelParams& p, int cfg, hipStream_t s, hipEvent_t ev_start = nullptr,
+                             hipEvent_t ev_stop = nullptr);
+// The coordinator reduce: merge_coord (one workgroup per query, ≤ kCoordMax = 4096 hits ranked in LDS)
+// or, for more hits per query, merge_rank (launch_merge_rank); same layout, same outputs.
+hipError_t launch_coord_reduce(const uint64_t* shard_keys, const int32_t* shard_counts, const int32_t* shard_index,
+                               int nq, int n_ranks, int sl, int k, int from, int size, float* scores, int32_t* docs,
+                               int32_t* shard_out, int32_t* count, int64_t* total_hits, float* max_score,
+                               hipStream_t s);
+// coordinator reduce for lists of any length (merge_coord's layout and outputs; no 4096-hit limit)
+hipError_t launch_merge_rank(const uint64_t* keys, const int32_t* counts, const int32_t* shard_index, int nq,
+                             int n_ranks, int sl, int k, int from, int size, float* scores, int32_t* docs,
+                             int32_t* shard_out, int32_t* count, int64_t* total_hits, float* max_score,
+                             hipStream_t s);
+
 hipError_t launch_sq8_quantize(const float4* x, int64_t n, int units, int pitch, int units8, void* out8,
                                float4* aux, int mode, hipStream_t s);
 // ev_start / ev_stop (optional): stamped by the kernel's own dispatch packet (hipExtLaunchKernelGGL),
@@ -256,6 +308,8 @@ struct Tuning {
     std::atomic<int> sq8{1};              // certified int8 prefilter for float32 batches below mfma_min_batch
     std::atomic<int> gather_min{0};       // ...at most one gather tile per this many accepted rows (0 = every gather
                                           // tile; fewer, longer tiles were slower: profiles/r02c/gather_min_ab.jsonl)
+    std::atomic<int> select_mid_k{1};     // float32 12 < k ≤ 64 with the prefilter on: the select path's int8
+                                          // bounds pass instead of the fp32 streaming scan (0 = the scan)
     std::atomic<int> filter_gather{1};    // filtered prefilter scans (VALU sq8_scan) compact the accepted ordinals
                                           // first and scan them (osk_filter.hip); 0 = walk the bitset windows
     std::atomic<int> sq8_mfma_nt{1};      // A/B: non-temporal row loads in sq8_mfma
