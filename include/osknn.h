@@ -102,6 +102,14 @@ int32_t osk_seg_stage(int32_t device, const void* rows, int64_t n_rows, int32_t 
 int32_t osk_seg_stage_device(int32_t device, const void* d_rows, int64_t src_pitch_bytes,
                              int64_t n_rows, int32_t dim, int32_t encoding, int32_t similarity,
                              const int32_t* ord_to_doc, int32_t max_doc, osk_seg** out);
+/* Same, from a Lucene99 flat vectors data file (.vec): the field's rows are the n_rows × dim
+ * little-endian elements at byte data_offset (its FieldEntry in .vemf: vectorDataOffset), memory-mapped
+ * and staged through pinned buffers into HBM (S/index/store/FsDirectoryFactory.java:98-110 maps .vec;
+ * S/index/IndexModule.java:215-233).  ord_to_doc as osk_seg_stage (the docsWithField IndexedDISI's
+ * order for a sparse field).  A missing or short file is OSK_ERR_INVALID with the OS message. */
+int32_t osk_seg_stage_file(int32_t device, const char* path, int64_t data_offset, int64_t n_rows, int32_t dim,
+                           int32_t encoding, int32_t similarity, const int32_t* ord_to_doc, int32_t max_doc,
+                           osk_seg** out);
 /* A synthetic dense segment generated on the device: row r of the segment is global row
  * row0 + r of the counter-based generator (seed, dist). osk_synth_host() yields identical values. */
 int32_t osk_seg_synth(int32_t device, int64_t n_rows, int32_t dim, int32_t encoding,

@@ -59,6 +59,7 @@ SIGNATURES = {
     "osk_last_error": (C.c_char_p, []),
     "osk_device_count": (_I32, [_PI32]),
     "osk_seg_stage": (_I32, [_I32, _P, _I64, _I32, _I32, _I32, _P, _I32, C.POINTER(_P)]),
+    "osk_seg_stage_file": (_I32, [_I32, C.c_char_p, _I64, _I64, _I32, _I32, _I32, _P, _I32, C.POINTER(_P)]),
     "osk_seg_stage_device": (_I32, [_I32, _P, _I64, _I64, _I32, _I32, _I32, _P, _I32, C.POINTER(_P)]),
     "osk_seg_synth": (_I32, [_I32, _I64, _I32, _I32, _I32, _U64, _I32, _I64, C.POINTER(_P)]),
     "osk_seg_release": (_I32, [_P]),

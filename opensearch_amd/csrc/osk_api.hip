@@ -2,10 +2,16 @@
 // single-device search paths and the coordinator merge.  The object model (osk_seg, osk_view) is in
 // osk_objects.h; the multi-GPU exchange (osk_comm, RCCL) in osk_comm.hip.
 // Every entry point catches all C++ exceptions and returns an error code (see osknn.h).
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cerrno>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -292,6 +298,86 @@ int32_t osk_seg_stage(int32_t device, const void* rows, int64_t n_rows, int32_t 
         OSK_HIP(hipMemset2DAsync(s->d_rows, dst_pitch, 0, dst_pitch, n_rows, st));
         OSK_HIP(hipMemcpy2DAsync(s->d_rows, dst_pitch, rows, src_pitch, src_pitch, n_rows,
                                  hipMemcpyHostToDevice, st));
+    }
+    rc = seg_finish(s.get(), ord_to_doc, st);
+    if (rc) return rc;
+    *out = s.release();
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_seg_stage_file(int32_t device, const char* path, int64_t data_offset, int64_t n_rows, int32_t dim,
+                           int32_t encoding, int32_t similarity, const int32_t* ord_to_doc, int32_t max_doc,
+                           osk_seg** out) {
+    OSK_GUARD_BEGIN
+    clear_error();
+    OSK_REQUIRE(out != nullptr && path != nullptr, "null argument");
+    OSK_REQUIRE(data_offset >= 0, "negative data offset");
+    std::unique_ptr<osk_seg> s;
+    int32_t rc = seg_alloc(device, n_rows, dim, encoding, similarity, max_doc, ord_to_doc, s);
+    if (rc) return rc;
+    hipStream_t st = device_stream(device);
+    const int64_t row_bytes = (int64_t)dim * (encoding == ENC_FLOAT32 ? 4 : 1);
+    const int64_t bytes = n_rows * row_bytes;
+    const int64_t dst_pitch = (int64_t)s->units * 16;
+    if (n_rows > 0) {
+        // the .vec slice: memory-mapped (as FsDirectoryFactory maps .vec under hybridfs), copied chunk by
+        // chunk into one of two pinned buffers while the other one's H2D copy runs, then into the
+        // segment's padded rows (zeros past dim)
+        const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+        if (fd < 0) {
+            set_error(std::string("cannot open ") + path + ": " + std::strerror(errno));
+            return OSK_ERR_INVALID;
+        }
+        struct stat sb;
+        if (::fstat(fd, &sb) != 0 || sb.st_size < data_offset + bytes) {
+            ::close(fd);
+            set_error(std::string(path) + " is shorter than the field's vector data");
+            return OSK_ERR_INVALID;
+        }
+        const int64_t page = ::sysconf(_SC_PAGESIZE);
+        const int64_t map_off = data_offset / page * page;
+        const size_t map_len = (size_t)(data_offset + bytes - map_off);
+        void* map = ::mmap(nullptr, map_len, PROT_READ, MAP_PRIVATE, fd, map_off);
+        ::close(fd);
+        if (map == MAP_FAILED) {
+            set_error(std::string("mmap of ") + path + " failed: " + std::strerror(errno));
+            return OSK_ERR_INVALID;
+        }
+        (void)::madvise(map, map_len, MADV_SEQUENTIAL);
+        const char* src = static_cast<const char*>(map) + (data_offset - map_off);
+        constexpr int64_t kChunk = 32ll << 20;
+        const int64_t rows_per = std::max<int64_t>(1, kChunk / row_bytes);
+        HostPinned ring[2];
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        bool used[2] = {false, false};
+        int32_t err = OSK_OK;
+        auto fail = [&](hipError_t e, const char* what) {
+            set_error(std::string(what) + ": " + hipGetErrorString(e));
+            err = OSK_ERR_DEVICE;
+        };
+        hipError_t e;
+        for (int i = 0; i < 2 && !err; ++i) {
+            if ((e = ring[i].reserve((size_t)std::min(n_rows, rows_per) * row_bytes)) != hipSuccess) fail(e, "pinned staging buffer");
+            else if ((e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming)) != hipSuccess) fail(e, "staging event");
+        }
+        if (!err && (e = hipMemset2DAsync(s->d_rows, dst_pitch, 0, dst_pitch, n_rows, st)) != hipSuccess)
+            fail(e, "hipMemset2DAsync");
+        int slot = 0;
+        for (int64_t r0 = 0; r0 < n_rows && !err; r0 += rows_per, slot ^= 1) {
+            const int64_t cnt = std::min(rows_per, n_rows - r0);
+            if (used[slot] && (e = hipEventSynchronize(ev[slot])) != hipSuccess) { fail(e, "hipEventSynchronize"); break; }
+            std::memcpy(ring[slot].p, src + r0 * row_bytes, (size_t)(cnt * row_bytes));
+            if ((e = hipMemcpy2DAsync(static_cast<char*>(s->d_rows) + r0 * dst_pitch, dst_pitch, ring[slot].p, row_bytes,
+                                      row_bytes, cnt, hipMemcpyHostToDevice, st)) != hipSuccess) { fail(e, "hipMemcpy2DAsync"); break; }
+            if ((e = hipEventRecord(ev[slot], st)) != hipSuccess) { fail(e, "hipEventRecord"); break; }
+            used[slot] = true;
+        }
+        if ((e = hipStreamSynchronize(st)) != hipSuccess && !err) fail(e, "hipStreamSynchronize");
+        for (int i = 0; i < 2; ++i)
+            if (ev[i]) (void)hipEventDestroy(ev[i]);
+        ::munmap(map, map_len);
+        if (err) return err;
     }
     rc = seg_finish(s.get(), ord_to_doc, st);
     if (rc) return rc;
@@ -1249,7 +1335,7 @@ int32_t select_search(osk_view* v, const void* d_queries, int nq, int k, int UP,
     p.cand = v->ws_sel_cand.as<uint64_t>();
     p.cand_count = v->ws_sel_cnt.as<int32_t>();
     p.cap = kSelCap;
-    auto one = [&](int q, bool exact) -> int32_t {
+    auto one = [&](int q, bool exact, bool count_visited) -> int32_t {
         p.exact = exact ? 1 : 0;
         p.q = v->ws_q.as<char>() + (size_t)q * UP * 16;
         p.qnorm = v->ws_qnorm.as<float>() + q;
@@ -1258,13 +1344,13 @@ int32_t select_search(osk_view* v, const void* d_queries, int nq, int k, int UP,
         p.out_keys = d_shard_keys + (size_t)q * S * k;
         p.out_counts = d_shard_counts + (size_t)q * S;
         p.flag = v->ws_flags.as<int>() + q;
-        p.visited = q == 0 ? reinterpret_cast<unsigned long long*>(d_visited) : nullptr;
+        p.visited = q == 0 && count_visited ? reinterpret_cast<unsigned long long*>(d_visited) : nullptr;
         OSK_HIP(launch_select_one(p, v->cfg, st, v->profile && q == 0 ? v->ev0 : nullptr,
                                   v->profile && q == nq - 1 ? v->ev1 : nullptr));
         return OSK_OK;
     };
     for (int q = 0; q < nq; ++q) {
-        int32_t rc = one(q, !bounds);
+        int32_t rc = one(q, !bounds, true);
         if (rc) return rc;
     }
     v->sel_calls += 1;
@@ -1280,7 +1366,7 @@ int32_t select_search(osk_view* v, const void* d_queries, int nq, int k, int UP,
         p.keys = v->ws_sel_keys.as<uint64_t>();
         const bool prof = v->profile;
         v->profile = false;
-        int32_t rc = one(q, true);
+        int32_t rc = one(q, true, false);   // (its rows were already counted as visited)
         v->profile = prof;
         if (rc) return rc;
         v->sel_exact_queries += 1;

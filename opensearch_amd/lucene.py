@@ -176,6 +176,26 @@ class GpuFlatVectorsReader:
                                   C.byref(h)))
         return cls(field, None, similarity, encoding, device=device, _handle=h.value, _dim=dim, _n=n)
 
+    @classmethod
+    def from_files(cls, field: str, directory: str, segment: str, segment_id: bytes, max_doc: int,
+                   field_number: int, suffix: str = "", device: int = 0):
+        """The reader a `KnnVectorsFormat.fieldsReader(SegmentReadState)` builds when the segment opens:
+        the field's entry parsed from `segment.vemf`, its `.vec` slice staged into HBM
+        (flatfiles.stage_field → osk_seg_stage_file)."""
+        import os
+        from . import flatfiles as FF
+        base = segment + (f"_{suffix}" if suffix else "")
+        vec, vemf = os.path.join(directory, base + ".vec"), os.path.join(directory, base + ".vemf")
+        FF.check_data_file(vec, segment_id, suffix)
+        entries = {e.number: e for e in FF.read_meta(vemf, segment_id, suffix)}
+        if field_number not in entries:
+            raise ValueError(f"field {field_number} has no vectors in {vemf}")
+        e = entries[field_number]
+        h = FF.stage_field(vec, e, max_doc, device)
+        r = cls(field, None, VectorSimilarityFunction(e.similarity), VectorEncoding(e.encoding), max_doc=max_doc,
+                device=device, _handle=h, _dim=e.dim, _n=e.size)
+        return r
+
     @property
     def handle(self) -> int:
         if not self._h.value:
