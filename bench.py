@@ -135,11 +135,14 @@ def cpu_baseline(sample_rows: int, n_queries: int, threads: int, passes: int = 5
 
 
 def main():
+    global K, SIZE
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--k", type=int, default=K, help="k (and size); the headline is k = 10. k > 12 takes the "
+                    "select path (osk_select.hip), k ≤ 12 the prefilter's wave lists")
     ap.add_argument("--rows-per-shard", type=int, default=ROWS_PER_SHARD)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sq8", action="store_true", help="measure the fp32 streaming scan as the main path")
@@ -164,6 +167,7 @@ def main():
     ap.add_argument("--cpu-queries", type=int, default=256)
     a = ap.parse_args()
 
+    K = SIZE = a.k
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -260,17 +264,25 @@ def main():
 
     _lib.tune("sq8", 0 if a.no_sq8 else 1)
     fb0, rs0, calls0 = counter("sq8_fallback_queries"), counter("sq8_rescored_rows"), counter("sq8_calls")
+    sel0 = counter("select_calls")
     elapsed_max, scan_avg_ms, ev_ms, out = timed(a.steps, a.warmup)
-    # the path the library chose (prefilter searches count sq8_calls; else bf16×3 from batch 16, else fp32)
+    # the path the library chose (prefilter searches count sq8_calls, select-path searches select_calls;
+    # else bf16×3 from batch 96, else fp32)
     prefilter = counter("sq8_calls") > calls0
-    batched = not prefilter and B >= 16 and K <= 12
+    select = counter("select_calls") > sel0
+    batched = not prefilter and not select and B >= 96 and K <= 12
     sq8_mfma = prefilter and sq8_mfma_min > 0 and B >= sq8_mfma_min
     # sanity on the last step: every query got `SIZE` hits from the 10M corpus
     cnt = out[3].cpu().numpy()
     assert np.all(cnt == SIZE), cnt
 
     u8 = (DIM + 15) // 16
-    if sq8_mfma:
+    if select:
+        passes = B
+        bytes_per_launch = rows_local * (u8 * 16 + 16 + 8) * passes
+        kernel_name = ("sel_bounds<16,3> select path writer (k > 12): int8 rows + 16-B bound terms read, 8-B LB/UB "
+                       "written per row, one query per launch; then radix select, collect, exact re-score, sort")
+    elif sq8_mfma:
         passes = (B + 31) // 32
         bytes_per_launch = rows_local * (u8 * 16 + 16) * passes
         kernel_name = ("sq8_mfma<KS=12,QB=2> certified int8 prefilter on v_mfma_i32_16x16x64_i8 (bytes = int8 rows "
@@ -351,9 +363,11 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (device counter generator: Irwin-Hall(4)≈N(0,1), rows L2-normalised; seed 42/43)",
-            "config": {"workload": "C3 Cohere-shaped exact k-NN: 10M×768 fp32 COSINE, 8 shards, k=10, from=0, size=10",
+            "config": {"workload": f"C3 Cohere-shaped exact k-NN: 10M×768 fp32 COSINE, 8 shards, k={K}, from=0, size={SIZE}",
                        "batch": B, "rows": N_SHARDS * a.rows_per_shard, "dim": DIM, "shards": N_SHARDS,
-                       "path": "prefilter" if prefilter else "mfma" if batched else "fp32_stream",
+                       "k": K,
+                       "path": ("prefilter" if prefilter else "select" if select else "mfma" if batched
+                                else "fp32_stream"),
                        "parallelism": (f"8 shards over {world} GPU(s); " + (
                            ("one C-ABI step per rank: scan + libosknn RCCL all-gather + device merge" if world > 1
                             else "one GPU: scan + device merge, no collective")

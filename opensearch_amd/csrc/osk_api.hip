@@ -1274,16 +1274,22 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
 
 // The select path (osk_select.hip): exact top-k for any k ≤ OSK_MAX_K, one query at a time.
 //   bounds = true: float32 fields through the int8 prefilter copy (bounds → threshold → candidates →
-//   exact re-score); a query with a shard whose candidates overflow kSelCap is answered again in exact
-//   mode (exact fp32 keys → threshold → the top k).  bounds = false: exact mode (float32 with the
-//   prefilter off, byte vectors).  ws_q / ws_qnorm hold the padded queries (exact mode: the caller's
+//   exact re-score → top k); bounds = false: exact mode (exact keys → threshold → top k; float32 with the
+//   prefilter off, byte vectors).  The candidate buffer holds a whole shard, so nothing overflows and
+//   nothing waits on the host.  ws_q / ws_qnorm hold the padded queries (exact mode: the caller's
 //   launch_prep_queries; bounds mode: sq8_prep here).
 int32_t select_search(osk_view* v, const void* d_queries, int nq, int k, int UP, const uint64_t* const* d_accept,
                       uint64_t* d_shard_keys, int32_t* d_shard_counts, int64_t* d_visited, hipStream_t st,
                       bool bounds) {
     const int S = v->n_shards;
     int64_t total = 0;
-    for (osk_seg* sg : v->segs) total += sg->n_rows;
+    std::vector<int64_t> shard_rows(S, 0);
+    for (size_t i = 0; i < v->segs.size(); ++i) {
+        total += v->segs[i]->n_rows;
+        shard_rows[v->seg_shard[i]] += v->segs[i]->n_rows;
+    }
+    const int64_t cap = std::max<int64_t>(1, *std::max_element(shard_rows.begin(), shard_rows.end()));
+    OSK_REQUIRE(cap < (1ll << 31), "a shard holds < 2^31 rows");
     const int nq_pad = (nq + kMaxNQ - 1) / kMaxNQ * kMaxNQ;
     int u8 = 0;
     if (bounds) {
@@ -1301,13 +1307,11 @@ int32_t select_search(osk_view* v, const void* d_queries, int nq, int k, int UP,
     } else {
         if (v->enc == ENC_FLOAT32 && v->sim == SIM_COSINE)
             OSK_HIP(launch_row_norms_f32(v->ws_q.as<float4>(), nq, UP, v->cfg, v->ws_qnorm.as<float>(), st));
-        OSK_HIP(v->ws_flags.reserve(sizeof(int) * nq));
-        OSK_HIP(hipMemsetAsync(v->ws_flags.p, 0, sizeof(int) * nq, st));
         OSK_HIP(v->ws_sel_keys.reserve(sizeof(uint64_t) * std::max<int64_t>(1, total)));
     }
     OSK_HIP(v->ws_sel_state.reserve(sizeof(RadixState) * S));
-    OSK_HIP(v->ws_sel_hist.reserve(sizeof(uint32_t) * 256 * S));
-    OSK_HIP(v->ws_sel_cand.reserve(sizeof(uint64_t) * (size_t)kSelCap * S));
+    OSK_HIP(v->ws_sel_hist.reserve(sizeof(uint32_t) * kSelBins * S));
+    OSK_HIP(v->ws_sel_cand.reserve(sizeof(uint64_t) * (size_t)cap * S));
     OSK_HIP(v->ws_sel_cnt.reserve(sizeof(int32_t) * S));
     SelParams p{};
     p.segs = v->d_segs.as<SegDev>();
@@ -1323,6 +1327,7 @@ int32_t select_search(osk_view* v, const void* d_queries, int nq, int k, int UP,
     p.units = v->units;
     p.units8 = u8;
     p.enc = v->enc;
+    p.exact = bounds ? 0 : 1;
     p.rows8 = v->d_sq8_rows.as<const int4*>();
     p.aux = v->d_sq8_aux.as<const float4*>();
     p.gam = v->sq8_gam;
@@ -1334,43 +1339,19 @@ int32_t select_search(osk_view* v, const void* d_queries, int nq, int k, int UP,
     p.hist = v->ws_sel_hist.as<uint32_t>();
     p.cand = v->ws_sel_cand.as<uint64_t>();
     p.cand_count = v->ws_sel_cnt.as<int32_t>();
-    p.cap = kSelCap;
-    auto one = [&](int q, bool exact, bool count_visited) -> int32_t {
-        p.exact = exact ? 1 : 0;
+    p.cap = (int)cap;
+    for (int q = 0; q < nq; ++q) {
         p.q = v->ws_q.as<char>() + (size_t)q * UP * 16;
         p.qnorm = v->ws_qnorm.as<float>() + q;
         p.q8 = v->ws_q8.as<int4>() + (size_t)q * u8;
         p.qc = v->ws_qc.as<float4>() + q;
         p.out_keys = d_shard_keys + (size_t)q * S * k;
         p.out_counts = d_shard_counts + (size_t)q * S;
-        p.flag = v->ws_flags.as<int>() + q;
-        p.visited = q == 0 && count_visited ? reinterpret_cast<unsigned long long*>(d_visited) : nullptr;
+        p.visited = q == 0 ? reinterpret_cast<unsigned long long*>(d_visited) : nullptr;
         OSK_HIP(launch_select_one(p, v->cfg, st, v->profile && q == 0 ? v->ev0 : nullptr,
                                   v->profile && q == nq - 1 ? v->ev1 : nullptr));
-        return OSK_OK;
-    };
-    for (int q = 0; q < nq; ++q) {
-        int32_t rc = one(q, !bounds, true);
-        if (rc) return rc;
     }
     v->sel_calls += 1;
-    if (!bounds) return OSK_OK;
-    // a shard whose candidates overflowed kSelCap flagged its query: answer it in exact mode
-    OSK_HIP(v->h_sel_flags.reserve(sizeof(int) * nq));
-    OSK_HIP(hipMemcpyAsync(v->h_sel_flags.p, v->ws_flags.p, sizeof(int) * nq, hipMemcpyDeviceToHost, st));
-    OSK_HIP(hipStreamSynchronize(st));
-    const int* fl = static_cast<const int*>(v->h_sel_flags.p);
-    for (int q = 0; q < nq; ++q) {
-        if (!fl[q]) continue;
-        OSK_HIP(v->ws_sel_keys.reserve(sizeof(uint64_t) * std::max<int64_t>(1, total)));
-        p.keys = v->ws_sel_keys.as<uint64_t>();
-        const bool prof = v->profile;
-        v->profile = false;
-        int32_t rc = one(q, true, false);   // (its rows were already counted as visited)
-        v->profile = prof;
-        if (rc) return rc;
-        v->sel_exact_queries += 1;
-    }
     return OSK_OK;
 }
 
@@ -1592,7 +1573,6 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
     else if (n == "mfma_fallback_queries") *value = v->mfma_fallback_queries;
     else if (n == "sq8_calls") *value = v->sq8_calls;
     else if (n == "select_calls") *value = v->sel_calls;
-    else if (n == "select_exact_queries") *value = v->sel_exact_queries;
     else if (n == "sq8_slices")
         *value = v->n_slices;
     else if (n == "sq8_fallback_queries" || n == "sq8_rescored_rows" || n == "sq8_exact_tiles") {

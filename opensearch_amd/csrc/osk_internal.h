@@ -215,6 +215,9 @@ hipError_t launch_filter_compact(const FilterParams& p, hipStream_t s);
 
 // ---- the select path: exact top-k for any k ≤ OSK_MAX_K (osk_select.hip) ----
 constexpr int kSelCap = 16384;       // candidates per (query, shard) the select path sorts in LDS
+constexpr int kSelDigit = 11;        // radix select digit width (2048-bin histograms)
+constexpr int kSelBins = 1 << kSelDigit;
+constexpr int kSelShift0 = 32 - kSelDigit;   // the first digit of a 32-bit LB
 struct RadixState {
     uint64_t prefix;                 // the digits of the k-th largest value decided so far
     int32_t krem;                    // its rank among the values that share them
@@ -241,13 +244,12 @@ struct SelParams {
     uint32_t* ub;
     uint64_t* keys;                  // exact mode, [view rows]
     RadixState* state;               // [n_shards]
-    uint32_t* hist;                  // [n_shards][256]
+    uint32_t* hist;                  // [n_shards][kSelBins]
     uint64_t* cand;                  // [n_shards][cap]
     int32_t* cand_count;             // [n_shards]
-    int cap;
+    int cap;                         // the largest shard's rows: a shard's candidates always fit
     uint64_t* out_keys;              // this query's [n_shards][k]
     int32_t* out_counts;             // [n_shards]
-    int* flag;                       // this query's flag: set on a bounds-mode overflow
 };
 // one query: writer → radix select → collect → (re-score) → sort; cfg = the view's fp32/byte lane cfg
 hipError_t launch_select_one(const SelParams& p, int cfg, hipStream_t s, hipEvent_t ev_start = nullptr,

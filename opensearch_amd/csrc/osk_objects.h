@@ -184,8 +184,7 @@ struct osk_view {
     // (one round of the chip, split over segments by rows), their settle slices, per-segment tile ranges
     // the select path (osk_select.hip, any k): per-row records of one query, radix state, candidates
     osk::DevBuf ws_sel_lb, ws_sel_ub, ws_sel_keys, ws_sel_state, ws_sel_hist, ws_sel_cand, ws_sel_cnt;
-    osk::HostPinned h_sel_flags;
-    int64_t sel_calls = 0, sel_exact_queries = 0;
+    int64_t sel_calls = 0;
     bool gather_ready = false;
     int n_gtiles = 0, n_gslices = 0;
     osk::DevBuf d_gtiles, d_gslices, d_gshard_slice_begin, d_seg_tiles;

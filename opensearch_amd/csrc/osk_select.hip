@@ -11,16 +11,18 @@
 //                 scores LB/UB (u32 each) of the certified int8 bound (osk_sq8.hip);
 //                 exact mode: the 64-bit hit key (sortable score << 32 | ~doc), the score computed
 //                 with the streaming scan's exact arithmetic (fp32 lane order / exact int32 bytes).
-//   radix       per shard, T = the k-th largest LB (4 passes of 8 bits) or the k-th largest key
-//               (8 passes): LDS histograms per tile, global per-shard histograms, one wave picks the
-//               digit (RadixState).  A shard with fewer than k accepted rows takes all of them.
+//   radix       per shard, T = the k-th largest LB (3 passes of 11-bit digits) or the k-th largest
+//               key (6 passes): LDS histograms
+//               per tile, global per-shard histograms, one wave picks the digit (RadixState).  A shard
+//               with fewer than k accepted rows takes all of them.
 //   collect     bounds: rows with UB ≥ T → candidate rows (every row that can reach the shard's top k:
 //               k rows have exact ≥ LB ≥ T, so the k-th exact score ≥ T, and a row with UB < T scores
 //               below it); exact: keys ≥ T → exactly min(k, accepted) keys.  Wave-aggregated appends.
 //   rescore     bounds: each candidate re-scored exactly (the streaming scan's arithmetic) → its key.
-//   sort_topk   per shard, the candidates' keys bitonic-sorted in LDS (≤ kSelCap = 16384), first k out.
-//               A bounds-mode shard with more than kSelCap candidates flags the query, which the host
-//               then answers in exact mode.
+//   sort        per shard, the top k of the candidates sorted best first: few candidates → one LDS
+//               bitonic sort; many → a radix select of the k-th candidate key (LDS, or global memory past
+//               kSelCap = 16384), the k keys ≥ it sorted.  The candidate buffer holds every row of the
+//               shard, so nothing can overflow and no host round trip is needed.
 // The coordinator merge of large lists (merge_rank): every hit's global rank by binary search in the
 // other (sorted) shard lists — (score desc, shardIndex asc, doc asc), [L] TopDocs.merge's order
 // (S/action/search/SearchPhaseController.java:224-246) — so S × min(k, from+size) is unbounded.
@@ -138,10 +140,11 @@ __global__ __launch_bounds__(kSelThreads) void sel_keys_i8(SelParams p) {
     if (p.visited && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
 }
 
-// bounds mode: the int8 prefilter copy's certified [lb, ub] score interval per row (sq8_scan's bound)
+// bounds mode: the int8 prefilter copy's certified [lb, ub] score interval per row (sq8_scan's bound),
+// U row groups loaded before any is reduced (≈ U·V KiB in flight per wave, as sq8_scan)
 template <int L, int V>
 __global__ __launch_bounds__(kSelThreads) void sel_bounds(SelParams p) {
-    constexpr int R = 64 / L;
+    constexpr int R = 64 / L, U = 4;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int t = lane & (L - 1), g = lane / L;
     const TileDev tile = p.tiles[blockIdx.x];
@@ -164,34 +167,47 @@ __global__ __launch_bounds__(kSelThreads) void sel_bounds(SelParams p) {
     int64_t wb, we;
     wave_rows<R>(tile, wave, wb, we);
     uint32_t nvis = 0;
-    for (int64_t r0 = wb; r0 < we; r0 += R) {
-        const int64_t row = r0 + g;
-        const bool in = row < we;
-        int32_t doc = 0;
-        const bool valid = in && row_accepted(abits, seg, row, doc);
-        const int4* xr = X + (in ? row : 0) * u8;
-        int acc = 0;
+    for (int64_t r0 = wb; r0 < we; r0 += R * U) {
+        int64_t row[U];
+        bool in[U], valid[U];
+        int4 xv[U][V];
+        float4 ax[U];
 #pragma unroll
-        for (int j = 0; j < V; ++j) {
-            const int f = t + j * L;
-            const int4 x = (valid && f < u8) ? load_i4_nt(xr + f) : make_int4(0, 0, 0, 0);
-            acc = __builtin_amdgcn_sdot4(x.x, qf[j].x, acc, false);
-            acc = __builtin_amdgcn_sdot4(x.y, qf[j].y, acc, false);
-            acc = __builtin_amdgcn_sdot4(x.z, qf[j].z, acc, false);
-            acc = __builtin_amdgcn_sdot4(x.w, qf[j].w, acc, false);
+        for (int u = 0; u < U; ++u) {
+            row[u] = r0 + u * R + g;
+            in[u] = row[u] < we;
+            int32_t doc = 0;
+            valid[u] = in[u] && row_accepted(abits, seg, row[u], doc);
+            const int4* xr = X + (in[u] ? row[u] : 0) * u8;
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                const int f = t + j * L;
+                xv[u][j] = (valid[u] && f < u8) ? load_i4_nt(xr + f) : make_int4(0, 0, 0, 0);
+            }
+            ax[u] = valid[u] ? AX[row[u]] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
-        for (int m = 1; m < L; m <<= 1) acc += __shfl_xor(acc, m);
-        const float4 ax = valid ? AX[row] : make_float4(0.f, 0.f, 0.f, 0.f);
-        float lo, hi;
-        sq8_bounds(sim, (float)acc, ax, qc, p.gam, p.g2, lo, hi);
-        const float xnd = (sim == SIM_COSINE && valid) ? seg.xnorm_f[row] : 0.0f;
-        const float ub = sim == SIM_EUCLIDEAN ? score_f32_l2(lo) : score_f32(sim, hi, qnd, xnd);
-        const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qnd, xnd);
-        nvis += __popcll(__ballot(t == 0 && valid));
-        if (in && t == 0) {   // every real score is ≥ 0, whose sortable form is ≥ 2^31: 0 = no row
-            p.lb[vbase + row] = valid ? float_to_sortable(lb) : 0u;
-            p.ub[vbase + row] = valid ? float_to_sortable(ub) : 0u;
+        for (int u = 0; u < U; ++u) {
+            int acc = 0;
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                acc = __builtin_amdgcn_sdot4(xv[u][j].x, qf[j].x, acc, false);
+                acc = __builtin_amdgcn_sdot4(xv[u][j].y, qf[j].y, acc, false);
+                acc = __builtin_amdgcn_sdot4(xv[u][j].z, qf[j].z, acc, false);
+                acc = __builtin_amdgcn_sdot4(xv[u][j].w, qf[j].w, acc, false);
+            }
+#pragma unroll
+            for (int m = 1; m < L; m <<= 1) acc += __shfl_xor(acc, m);
+            float lo, hi;
+            sq8_bounds(sim, (float)acc, ax[u], qc, p.gam, p.g2, lo, hi);
+            const float xnd = (sim == SIM_COSINE && valid[u]) ? seg.xnorm_f[row[u]] : 0.0f;
+            const float ub = sim == SIM_EUCLIDEAN ? score_f32_l2(lo) : score_f32(sim, hi, qnd, xnd);
+            const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qnd, xnd);
+            nvis += __popcll(__ballot(t == 0 && valid[u]));
+            if (in[u] && t == 0) {   // every real score is ≥ 0, whose sortable form is ≥ 2^31: 0 = no row
+                p.lb[vbase + row[u]] = valid[u] ? float_to_sortable(lb) : 0u;
+                p.ub[vbase + row[u]] = valid[u] ? float_to_sortable(ub) : 0u;
+            }
         }
     }
     if (p.visited && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
@@ -199,59 +215,110 @@ __global__ __launch_bounds__(kSelThreads) void sel_bounds(SelParams p) {
 
 // ---- radix select of the k-th largest LB (u32) / key (u64) per shard ---------------------------
 
-__global__ __launch_bounds__(64) void sel_init(SelParams p) {
-    for (int s = threadIdx.x; s < p.n_shards; s += 64) {
+__global__ __launch_bounds__(256) void sel_init(SelParams p) {
+    for (int s = threadIdx.x; s < p.n_shards; s += 256) {
         p.state[s] = RadixState{0ull, p.k, 0, 0};
         p.cand_count[s] = 0;
     }
-    for (int i = threadIdx.x; i < p.n_shards * 256; i += 64) p.hist[i] = 0u;
+    for (int i = threadIdx.x; i < p.n_shards * kSelBins; i += 256) p.hist[i] = 0u;
 }
 
-__global__ __launch_bounds__(kSelThreads) void sel_hist(SelParams p, int shift) {
-    __shared__ uint32_t h[256];
+// digit `pass` of a 32-bit (bounds: LB) or 64-bit (exact: key) value: 11-bit digits from the top
+__device__ __host__ __forceinline__ void sel_digit(int exact, int pass, int& shift, int& width) {
+    const int bits = exact ? 64 : 32;
+    const int hi = bits - kSelDigit * pass;   // bits above the digit's top are decided
+    width = hi >= kSelDigit ? kSelDigit : hi;
+    shift = hi - width;
+}
+
+// EXACT is a template parameter: a runtime choice between the two arrays inside the unrolled loop made
+// the compiler wait for every load before issuing the next (collect: 145 µs instead of ≈15 at C3)
+template <bool EXACT>
+__global__ __launch_bounds__(kSelThreads) void sel_hist(SelParams p, int pass) {
+    __shared__ uint32_t h[kSelBins];
     const int tid = threadIdx.x;
     const TileDev tile = p.tiles[blockIdx.x];
     const RadixState st = p.state[tile.shard];
     if (st.all) return;   // (block-uniform)
-    h[tid] = 0u;
+    int shift, width;
+    sel_digit(EXACT, pass, shift, width);
+    for (int i = tid; i < kSelBins; i += kSelThreads) h[i] = 0u;
     __syncthreads();
-    const uint64_t mask = shift + 8 >= 64 ? 0ull : (~0ull << (shift + 8));
+    const uint64_t mask = shift + width >= 64 ? 0ull : (~0ull << (shift + width));
     const uint64_t want = st.prefix & mask;
+    const uint32_t dmask = (1u << width) - 1u;
     const int64_t vbase = p.seg_vrow[tile.seg];
-    for (int64_t r = tile.row_begin + tid; r < tile.row_end; r += kSelThreads) {
-        const uint64_t key = p.exact ? p.keys[vbase + r] : (uint64_t)p.lb[vbase + r];
-        if (key && (key & mask) == want) atomicAdd(&h[(key >> shift) & 255u], 1u);
+    for (int64_t r0 = tile.row_begin; r0 < tile.row_end; r0 += 4 * kSelThreads) {
+        uint64_t key[4];   // four independent loads in flight per thread
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t r = r0 + u * kSelThreads + tid;
+            key[u] = r < tile.row_end ? (EXACT ? p.keys[vbase + r] : (uint64_t)p.lb[vbase + r]) : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            // scores cluster, so a wave's keys often share one bin: one LDS atomic for the wave then
+            // (a per-lane atomic on one address serialises 64-fold)
+            const bool hit = key[u] && (key[u] & mask) == want;
+            const uint32_t bin = (uint32_t)(key[u] >> shift) & dmask;
+            const uint64_t act = __ballot(hit);
+            if (!act) continue;
+            const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)bin, __builtin_ctzll(act));
+            const uint64_t same = __ballot(hit && bin == b0);
+            if (same == act) {
+                if ((threadIdx.x & 63) == __builtin_ctzll(act)) atomicAdd(&h[b0], (uint32_t)__popcll(act));
+            } else if (hit) {
+                atomicAdd(&h[bin], 1u);
+            }
+        }
     }
     __syncthreads();
-    if (h[tid]) atomicAdd(&p.hist[tile.shard * 256 + tid], h[tid]);
+    for (int i = tid; i < kSelBins; i += kSelThreads)
+        if (h[i]) atomicAdd(&p.hist[(size_t)tile.shard * kSelBins + i], h[i]);
 }
 
-__global__ __launch_bounds__(64) void sel_pick(SelParams p, int shift, int first) {
-    __shared__ uint32_t h[256];
+// one wave per shard: the digit holding the krem-th largest value; lanes own 32 bins each, a suffix
+// scan over lanes finds the lane, that lane walks its bins
+__global__ __launch_bounds__(64) void sel_pick(SelParams p, int pass) {
     const int s = blockIdx.x, lane = threadIdx.x;
     RadixState st = p.state[s];
     if (st.all) return;
-    for (int i = lane; i < 256; i += 64) {
-        h[i] = p.hist[s * 256 + i];
-        p.hist[s * 256 + i] = 0u;   // ready for the next pass
+    int shift, width;
+    sel_digit(p.exact, pass, shift, width);
+    constexpr int kPer = kSelBins / 64;
+    uint32_t* hs = p.hist + (size_t)s * kSelBins;
+    uint32_t h[kPer];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+        h[i] = hs[lane * kPer + i];
+        hs[lane * kPer + i] = 0u;   // ready for the next pass
+        sum += h[i];
     }
-    __syncthreads();
-    if (lane == 0) {
-        uint32_t total = 0;
-        if (first) {
-            for (int b = 0; b < 256; ++b) total += h[b];
-            if ((int64_t)total <= (int64_t)st.krem) st.all = 1;   // ≤ k rows: take every one
+    uint32_t incl = sum;   // Σ over lanes ≥ this one
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_down(incl, o);
+        if (lane + o < 64) incl += y;
+    }
+    const uint32_t total = __shfl(incl, 0);
+    const uint32_t above = incl - sum;
+    if (pass == 0 && (int64_t)total <= (int64_t)st.krem) {   // ≤ k rows: take every one
+        if (lane == 0) {
+            st.all = 1;
+            p.state[s] = st;
         }
-        if (!st.all) {
-            uint32_t cum = 0;
-            for (int b = 255; b >= 0; --b) {
-                if ((int64_t)cum + h[b] >= (int64_t)st.krem) {
-                    st.prefix |= (uint64_t)b << shift;
-                    st.krem -= (int32_t)cum;
-                    break;
-                }
-                cum += h[b];
+        return;
+    }
+    const bool mine = (int64_t)above < (int64_t)st.krem && (int64_t)st.krem <= (int64_t)incl;
+    if (mine) {
+        uint32_t cum = above;
+        for (int i = kPer - 1; i >= 0; --i) {
+            if ((int64_t)cum + h[i] >= (int64_t)st.krem) {
+                st.prefix |= (uint64_t)(lane * kPer + i) << shift;
+                st.krem -= (int32_t)cum;
+                break;
             }
+            cum += h[i];
         }
         p.state[s] = st;
     }
@@ -259,6 +326,7 @@ __global__ __launch_bounds__(64) void sel_pick(SelParams p, int shift, int first
 
 // ---- collect / rescore / sort -----------------------------------------------------------------
 
+template <bool EXACT>
 __global__ __launch_bounds__(kSelThreads) void sel_collect(SelParams p) {
     const int tid = threadIdx.x, lane = tid & 63;
     const TileDev tile = p.tiles[blockIdx.x];
@@ -267,27 +335,43 @@ __global__ __launch_bounds__(kSelThreads) void sel_collect(SelParams p) {
     const uint64_t thr = st.all ? 1ull : st.prefix;
     const int64_t vbase = p.seg_vrow[tile.seg];
     uint64_t* out = p.cand + (size_t)s * p.cap;
-    for (int64_t r0 = tile.row_begin; r0 < tile.row_end; r0 += kSelThreads) {
-        const int64_t r = r0 + tid;
-        uint64_t val = 0ull;
-        bool take = false;
-        if (r < tile.row_end) {
-            if (p.exact) {
-                val = p.keys[vbase + r];
-                take = val && val >= thr;
+    for (int64_t r0 = tile.row_begin; r0 < tile.row_end; r0 += 4 * kSelThreads) {
+        uint64_t val[4];
+        bool take[4];
+        int c = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t r = r0 + u * kSelThreads + tid;
+            take[u] = false;
+            val[u] = 0ull;
+            if (EXACT) {
+                val[u] = r < tile.row_end ? p.keys[vbase + r] : 0ull;
             } else {
-                const uint32_t u = p.ub[vbase + r];
-                take = u && (uint64_t)u >= thr;
-                val = (uint64_t)(vbase + r);
+                val[u] = r < tile.row_end ? (uint64_t)p.ub[vbase + r] : 0ull;   // the UB, then the row
             }
         }
-        const uint64_t m = __ballot(take);
-        if (!m) continue;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            take[u] = val[u] && val[u] >= thr;
+            if (!EXACT) val[u] = (uint64_t)(vbase + r0 + u * kSelThreads + tid);
+            c += take[u];
+        }
+        int incl = c;   // wave prefix of the takes
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        const int tot = __shfl(incl, 63);
+        if (!tot) continue;
         int base = 0;
-        if (lane == 0) base = atomicAdd(&p.cand_count[s], __popcll(m));
-        base = __shfl(base, 0);
-        const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
-        if (take && pos < p.cap) out[pos] = val;
+        if (lane == 63) base = atomicAdd(&p.cand_count[s], tot);
+        base = __shfl(base, 63) + incl - c;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (take[u]) {
+                if (base < p.cap) out[base] = val[u];   // (cap = the shard's rows: never exceeded)
+                ++base;
+            }
     }
 }
 
@@ -297,8 +381,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_rescore(SelParams p) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int t = lane & (L - 1), gr = lane / L;
     const int s = blockIdx.x;
-    const int n = p.cand_count[s];
-    if (n > p.cap) return;   // overflow: the query is answered in exact mode
+    const int n = min(p.cand_count[s], p.cap);
     const float4* __restrict__ Q = static_cast<const float4*>(p.q);
     float4 qf[V];
 #pragma unroll
@@ -327,25 +410,8 @@ __global__ __launch_bounds__(kSelThreads) void sel_rescore(SelParams p) {
     }
 }
 
-// per shard: bitonic sort (descending) of its ≤ cap candidate keys in LDS, first k out
-__global__ __launch_bounds__(1024) void sel_sort(SelParams p) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t sk[];
-    const int s = blockIdx.x, tid = threadIdx.x;
-    const int n_raw = p.cand_count[s];
-    uint64_t* ok = p.out_keys + (size_t)s * p.k;
-    if (n_raw > p.cap) {   // bounds mode overflow: flag the query, write an empty list
-        if (tid == 0) {
-            p.flag[0] = 1;
-            p.out_counts[s] = 0;
-        }
-        for (int i = tid; i < p.k; i += 1024) ok[i] = 0ull;
-        return;
-    }
-    const int n = n_raw;
-    int np = 2;
-    while (np < n) np <<= 1;
-    const uint64_t* c = p.cand + (size_t)s * p.cap;
-    for (int i = tid; i < np; i += 1024) sk[i] = i < n ? c[i] : 0ull;
+// bitonic sort (descending) of np (a power of two) keys in LDS by 1024 threads
+__device__ __forceinline__ void bitonic_desc(uint64_t* sk, int np, int tid) {
     for (int size = 2; size <= np; size <<= 1) {
         for (int j = size >> 1; j > 0; j >>= 1) {
             __syncthreads();
@@ -362,7 +428,85 @@ __global__ __launch_bounds__(1024) void sel_sort(SelParams p) {
         }
     }
     __syncthreads();
+}
+
+// per shard: the top k of its n candidate keys (distinct), sorted best first.  Few candidates
+// (n ≤ 2k + 256, in LDS): one bitonic sort.  Otherwise: a radix select (8-bit digits, LDS histogram)
+// of the kk-th largest key over the candidates (in LDS when n ≤ kSelCap, else in global memory), the
+// kk keys ≥ it gathered into the output slots, then sorted in LDS.
+__global__ __launch_bounds__(1024) void sel_sort(SelParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t sk[];
+    __shared__ uint32_t h[256];
+    __shared__ uint64_t s_prefix;
+    __shared__ int s_krem, s_ctr;
+    const int s = blockIdx.x, tid = threadIdx.x;
+    const int n = min(p.cand_count[s], p.cap);
     const int kk = min(p.k, n);
+    uint64_t* ok = p.out_keys + (size_t)s * p.k;
+    const uint64_t* c = p.cand + (size_t)s * p.cap;
+    const bool in_lds = n <= kSelCap;
+    if (in_lds)
+        for (int i = tid; i < n; i += 1024) sk[i] = c[i];
+    if (in_lds && n <= 2 * kk + 256) {
+        int np = 2;
+        while (np < n) np <<= 1;
+        for (int i = n + tid; i < np; i += 1024) sk[i] = 0ull;
+        bitonic_desc(sk, np, tid);
+        for (int i = tid; i < p.k; i += 1024) ok[i] = i < kk ? sk[i] : 0ull;
+        if (tid == 0) p.out_counts[s] = kk;
+        return;
+    }
+    const uint64_t* src = in_lds ? sk : c;
+    if (tid == 0) {
+        s_prefix = 0ull;
+        s_krem = kk;
+        s_ctr = 0;
+    }
+    for (int shift = 56; shift >= 0; shift -= 8) {
+        if (tid < 256) h[tid] = 0u;
+        __syncthreads();
+        const uint64_t mask = shift == 56 ? 0ull : (~0ull << (shift + 8));
+        const uint64_t want = s_prefix & mask;
+        for (int i = tid; i < n; i += 1024) {
+            const uint64_t key = src[i];
+            if ((key & mask) == want) atomicAdd(&h[(key >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (tid < 64) {   // one wave: 4 bins per lane, suffix scan, the owning lane walks its bins
+            uint32_t hb[4], sum = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) sum += (hb[i] = h[tid * 4 + i]);
+            uint32_t incl = sum;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_down(incl, o);
+                if (tid + o < 64) incl += y;
+            }
+            const int krem = s_krem;
+            const uint32_t above = incl - sum;
+            if ((int64_t)above < krem && krem <= (int64_t)incl) {
+                uint32_t cum = above;
+                for (int i = 3; i >= 0; --i) {
+                    if ((int64_t)cum + hb[i] >= krem) {
+                        s_prefix |= (uint64_t)(tid * 4 + i) << shift;
+                        s_krem = krem - (int)cum;
+                        break;
+                    }
+                    cum += hb[i];
+                }
+            }
+        }
+        __syncthreads();
+    }
+    const uint64_t kth = s_prefix;   // the kk-th largest key: exactly kk keys are ≥ it
+    for (int i = tid; i < n; i += 1024) {
+        const uint64_t key = src[i];
+        if (key >= kth) ok[atomicAdd(&s_ctr, 1)] = key;
+    }
+    __syncthreads();
+    int np = 2;
+    while (np < kk) np <<= 1;
+    for (int i = tid; i < np; i += 1024) sk[i] = i < kk ? ok[i] : 0ull;
+    bitonic_desc(sk, np, tid);
     for (int i = tid; i < p.k; i += 1024) ok[i] = i < kk ? sk[i] : 0ull;
     if (tid == 0) p.out_counts[s] = kk;
 }
@@ -512,7 +656,7 @@ static int sel_bounds_cfg(int u8) {
 hipError_t launch_select_one(const SelParams& p, int cfg, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
     if (p.n_tiles <= 0) return hipSuccess;
     const dim3 tg(p.n_tiles), tb(kSelThreads);
-    hipLaunchKernelGGL(sel_init, dim3(1), dim3(64), 0, s, p);
+    hipLaunchKernelGGL(sel_init, dim3(1), dim3(256), 0, s, p);
     // the writer (stamped by the profile events when given)
     SelFn writer = p.exact ? (p.enc == ENC_BYTE ? kSelKeysI8[cfg] : kSelKeysF32[cfg][p.sim == SIM_EUCLIDEAN ? 1 : 0])
                            : kSelBounds[sel_bounds_cfg(p.units8)];
@@ -520,16 +664,15 @@ hipError_t launch_select_one(const SelParams& p, int cfg, hipStream_t s, hipEven
         hipExtLaunchKernelGGL(writer, tg, tb, 0, s, ev_start, ev_stop, 0, p);
     else
         hipLaunchKernelGGL(writer, tg, tb, 0, s, p);
-    const int passes = p.exact ? 8 : 4;
+    const int passes = ((p.exact ? 64 : 32) + kSelDigit - 1) / kSelDigit;   // 6 (u64) or 3 (u32)
     for (int i = 0; i < passes; ++i) {
-        const int shift = 8 * (passes - 1 - i);
-        hipLaunchKernelGGL(sel_hist, tg, tb, 0, s, p, shift);
-        hipLaunchKernelGGL(sel_pick, dim3(p.n_shards), dim3(64), 0, s, p, shift, i == 0 ? 1 : 0);
+        hipLaunchKernelGGL(p.exact ? sel_hist<true> : sel_hist<false>, tg, tb, 0, s, p, i);
+        hipLaunchKernelGGL(sel_pick, dim3(p.n_shards), dim3(64), 0, s, p, i);
     }
-    hipLaunchKernelGGL(sel_collect, tg, tb, 0, s, p);
+    hipLaunchKernelGGL(p.exact ? sel_collect<true> : sel_collect<false>, tg, tb, 0, s, p);
     if (!p.exact)
         hipLaunchKernelGGL(kSelRescore[cfg][p.sim == SIM_EUCLIDEAN ? 1 : 0], dim3(p.n_shards, 64), tb, 0, s, p);
-    hipLaunchKernelGGL(sel_sort, dim3(p.n_shards), dim3(1024), (size_t)p.cap * 8, s, p);
+    hipLaunchKernelGGL(sel_sort, dim3(p.n_shards), dim3(1024), (size_t)kSelCap * 8, s, p);
     return hipGetLastError();
 }
 
@@ -552,7 +695,10 @@ hipError_t launch_coord_reduce(const uint64_t* shard_keys, const int32_t* shard_
                                int nq, int n_ranks, int sl, int k, int from, int size, float* scores, int32_t* docs,
                                int32_t* shard_out, int32_t* count, int64_t* total_hits, float* max_score,
                                hipStream_t s) {
-    if ((int64_t)n_ranks * sl * std::min(k, from + size) <= 4096)
+    // merge_coord ranks every hit against every other in one workgroup: best for few hits (k = 10:
+    // 80 per query); beyond a few hundred the parallel binary-search ranking wins (k = 100, 8 shards:
+    // 105 µs → ≈10 µs)
+    if ((int64_t)n_ranks * sl * std::min(k, from + size) <= 256)
         return launch_merge_coord(shard_keys, shard_counts, shard_index, nq, n_ranks, sl, k, from, size, scores, docs,
                                   shard_out, count, total_hits, max_score, s);
     return launch_merge_rank(shard_keys, shard_counts, shard_index, nq, n_ranks, sl, k, from, size, scores, docs,

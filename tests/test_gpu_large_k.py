@@ -145,21 +145,22 @@ def test_select_ties_lower_doc_wins():
         r.close()
 
 
-def test_select_bounds_overflow_takes_exact_mode():
-    """Rows so alike that the int8 bounds cannot tell them apart: a shard's candidates overflow the
-    sort capacity (16384), the query is flagged and answered in exact mode — same result."""
+def test_select_many_candidates_beyond_lds():
+    """Rows so alike that the int8 bounds cannot tell them apart: every row of the shard is a candidate
+    (40000 > the 16384 keys an LDS sort holds), so the top k is radix-selected in global memory — the
+    result must equal the exact mode's."""
     rng = np.random.default_rng(360)
     rows = (np.ones((40000, 32), np.float32) + rng.standard_normal((40000, 32)).astype(np.float32) * 1e-4)
     queries = np.ones((2, 32), np.float32)
     r = LU.GpuFlatVectorsReader("v", rows, LU.VectorSimilarityFunction.DOT_PRODUCT)
     ds = LU.DeviceShardSet([[LU.LeafReaderContext(0, 0, r)]], [0])
     try:
-        got = ds.search(queries, 100, 0, 100)
-        assert ds.counter("select_exact_queries") >= 1
-        want = with_sq8(0, lambda: ds.search(queries, 100, 0, 100))
-        for a, b in zip(got, want):
-            assert np.array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8))
-        check_reader(r, rows, queries, 100, LU.VectorSimilarityFunction.DOT_PRODUCT)
+        for k in (100, 5000):
+            got = ds.search(queries, k, 0, k)
+            want = with_sq8(0, lambda: ds.search(queries, k, 0, k))
+            for a, b in zip(got, want):
+                assert np.array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8))
+            check_reader(r, rows, queries, k, LU.VectorSimilarityFunction.DOT_PRODUCT)
     finally:
         ds.close()
         r.close()
