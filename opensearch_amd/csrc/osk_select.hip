@@ -142,7 +142,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_keys_i8(SelParams p) {
 
 // bounds mode: the int8 prefilter copy's certified [lb, ub] score interval per row (sq8_scan's bound),
 // U row groups loaded before any is reduced (≈ U·V KiB in flight per wave, as sq8_scan)
-template <int L, int V>
+template <int L, int V, bool FILT>
 __global__ __launch_bounds__(kSelThreads) void sel_bounds(SelParams p) {
     constexpr int R = 64 / L, U = 4;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -177,14 +177,21 @@ __global__ __launch_bounds__(kSelThreads) void sel_bounds(SelParams p) {
             row[u] = r0 + u * R + g;
             in[u] = row[u] < we;
             int32_t doc = 0;
-            valid[u] = in[u] && row_accepted(abits, seg, row[u], doc);
-            const int4* xr = X + (in[u] ? row[u] : 0) * u8;
+            // (FILT is compile-time: a runtime accept test put a branch with a full load wait between
+            // the row groups, so their loads no longer overlapped)
+            valid[u] = in[u];
+            if constexpr (FILT) valid[u] = valid[u] && (!abits || row_accepted(abits, seg, row[u], doc));
+            // loads on a clamped row, results masked (no load under a branch: those serialise)
+            const int64_t rc = in[u] ? row[u] : wb;
+            const int4* xr = X + rc * u8;
 #pragma unroll
             for (int j = 0; j < V; ++j) {
                 const int f = t + j * L;
-                xv[u][j] = (valid[u] && f < u8) ? load_i4_nt(xr + f) : make_int4(0, 0, 0, 0);
+                const int4 x = load_i4_nt(xr + (f < u8 ? f : 0));
+                const int m = (valid[u] && f < u8) ? -1 : 0;
+                xv[u][j] = make_int4(x.x & m, x.y & m, x.z & m, x.w & m);
             }
-            ax[u] = valid[u] ? AX[row[u]] : make_float4(0.f, 0.f, 0.f, 0.f);
+            ax[u] = AX[rc];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -252,8 +259,12 @@ __global__ __launch_bounds__(kSelThreads) void sel_hist(SelParams p, int pass) {
         uint64_t key[4];   // four independent loads in flight per thread
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
+            // clamped index, unconditional load, masked value: a conditional load made the compiler wait
+            // for each load before the next
             const int64_t r = r0 + u * kSelThreads + tid;
-            key[u] = r < tile.row_end ? (EXACT ? p.keys[vbase + r] : (uint64_t)p.lb[vbase + r]) : 0ull;
+            const int64_t rc = min(r, tile.row_end - 1);
+            const uint64_t v = EXACT ? p.keys[vbase + rc] : (uint64_t)p.lb[vbase + rc];
+            key[u] = r < tile.row_end ? v : 0ull;
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -344,11 +355,9 @@ __global__ __launch_bounds__(kSelThreads) void sel_collect(SelParams p) {
             const int64_t r = r0 + u * kSelThreads + tid;
             take[u] = false;
             val[u] = 0ull;
-            if (EXACT) {
-                val[u] = r < tile.row_end ? p.keys[vbase + r] : 0ull;
-            } else {
-                val[u] = r < tile.row_end ? (uint64_t)p.ub[vbase + r] : 0ull;   // the UB, then the row
-            }
+            const int64_t rc = min(r, tile.row_end - 1);   // unconditional loads (see sel_hist)
+            const uint64_t v = EXACT ? p.keys[vbase + rc] : (uint64_t)p.ub[vbase + rc];   // the UB, then the row
+            val[u] = r < tile.row_end ? v : 0ull;
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -645,8 +654,9 @@ static const SelFn kSelRescore[9][2] = {OSK_SEL_RS(4, 2),  OSK_SEL_RS(8, 2),  OS
                                         OSK_SEL_RS(16, 4), OSK_SEL_RS(16, 8), OSK_SEL_RS(16, 12),
                                         OSK_SEL_RS(32, 8), OSK_SEL_RS(64, 8), OSK_SEL_RS(64, 16)};
 // int8 prefilter lane configs by 16-byte units (sq8_cfg's)
-static const SelFn kSelBounds[8] = {sel_bounds<4, 1>,  sel_bounds<8, 1>,  sel_bounds<16, 1>, sel_bounds<16, 2>,
-                                    sel_bounds<16, 3>, sel_bounds<16, 4>, sel_bounds<32, 4>, sel_bounds<64, 4>};
+#define OSK_SEL_B(L, V) {sel_bounds<L, V, false>, sel_bounds<L, V, true>}
+static const SelFn kSelBounds[8][2] = {OSK_SEL_B(4, 1),  OSK_SEL_B(8, 1),  OSK_SEL_B(16, 1), OSK_SEL_B(16, 2),
+                                       OSK_SEL_B(16, 3), OSK_SEL_B(16, 4), OSK_SEL_B(32, 4), OSK_SEL_B(64, 4)};
 static int sel_bounds_cfg(int u8) {
     return u8 <= 4 ? 0 : u8 <= 8 ? 1 : u8 <= 16 ? 2 : u8 <= 32 ? 3 : u8 <= 48 ? 4 : u8 <= 64 ? 5 : u8 <= 128 ? 6 : 7;
 }
@@ -659,7 +669,7 @@ hipError_t launch_select_one(const SelParams& p, int cfg, hipStream_t s, hipEven
     hipLaunchKernelGGL(sel_init, dim3(1), dim3(256), 0, s, p);
     // the writer (stamped by the profile events when given)
     SelFn writer = p.exact ? (p.enc == ENC_BYTE ? kSelKeysI8[cfg] : kSelKeysF32[cfg][p.sim == SIM_EUCLIDEAN ? 1 : 0])
-                           : kSelBounds[sel_bounds_cfg(p.units8)];
+                           : kSelBounds[sel_bounds_cfg(p.units8)][p.accept ? 1 : 0];
     if (ev_start || ev_stop)
         hipExtLaunchKernelGGL(writer, tg, tb, 0, s, ev_start, ev_stop, 0, p);
     else
