@@ -98,7 +98,9 @@ int32_t     osk_device_count(int32_t* n);
 int32_t osk_seg_stage(int32_t device, const void* rows, int64_t n_rows, int32_t dim,
                       int32_t encoding, int32_t similarity, const int32_t* ord_to_doc,
                       int32_t max_doc, osk_seg** out);
-/* Same, from rows already on `device` (row pitch `src_pitch_bytes`); ord_to_doc is host memory. */
+/* Same, from rows already on `device` (row pitch `src_pitch_bytes`); ord_to_doc is host memory.
+ * The copy is issued on the library's own stream for `device`, which does not wait on the caller's
+ * streams: whatever writes d_rows must have completed (e.g. its stream synchronised) before the call. */
 int32_t osk_seg_stage_device(int32_t device, const void* d_rows, int64_t src_pitch_bytes,
                              int64_t n_rows, int32_t dim, int32_t encoding, int32_t similarity,
                              const int32_t* ord_to_doc, int32_t max_doc, osk_seg** out);
@@ -227,6 +229,13 @@ int32_t osk_view_scan_time(osk_view* view, double* total_ms, int64_t* calls);
  *                     default 2; 0 = always the VALU sq8_scan)
  *   "sq8_mfma_queries"  16 | 32 queries per sq8_mfma launch (default 32)
  *   "sq8_mfma_nt"     0|1 non-temporal row loads in sq8_mfma (default 1)
+ *   "filter_gather"   0|1 filtered prefilter scans over the device-compacted accepted ordinals
+ *                     (osk_filter.hip; default 1) instead of a walk over 64-row bitset windows
+ *   "gather_min"      accepted rows per gather tile at least (default 0 = every tile of the segment)
+ *   "select_mid_k"    0|1 float32 searches with 12 < k ≤ 64 take the select path over int8 bounds
+ *                     (default 1) instead of the fp32 streaming scan; k > 64 always takes it
+ *   "sel_writer"      select path bounds writer: 0 = 4 row groups in flight + Java's transform,
+ *                     1 = 4 groups + fp32 COSINE bounds (default), 2 = 2 groups, 3 = 1 group (fast bounds)
  * The testing build (libosknn_testing.so) also accepts "sq8_mfma_ablate", "mfma_ablate" (A/B timing,
  * results wrong), "sq8_force_fallback" (every prefilter list re-scanned exactly) and "settle_trace";
  * the shipped library returns OSK_ERR_UNSUPPORTED for them. */
@@ -238,7 +247,8 @@ int32_t osk_view_stats(osk_view* view, int64_t* batched_calls, int64_t* fallback
 /* Named counters of a view: "mfma_calls", "mfma_fallback_queries" (as osk_view_stats),
  * "sq8_calls" (prefiltered searches), "sq8_fallback_queries" (queries where some tile's candidate
  * list overflowed past the certificate and the tile was re-scanned exactly), "sq8_exact_tiles"
- * (such tiles), "sq8_rescored_rows" (rows re-scored exactly, all calls). */
+ * (such tiles), "sq8_rescored_rows" (rows re-scored exactly, all calls), "select_calls" (searches
+ * on the select path, k > 12). */
 int32_t osk_view_counter(osk_view* view, const char* name, int64_t* value);
 /* Testing build only (the shipped library returns OSK_ERR_UNSUPPORTED): copy `bytes` of an internal
  * buffer of the view's last search ("akeys", "cand_a", "flags", "qsplit", "qnorm", "sq8cand", "sq8lb",

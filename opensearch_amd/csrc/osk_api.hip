@@ -245,6 +245,7 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         {"sq8", &g_tuning.sq8, 0, 1, false},
         {"filter_gather", &g_tuning.filter_gather, 0, 1, false},
         {"select_mid_k", &g_tuning.select_mid_k, 0, 1, false},
+        {"sel_writer", &g_tuning.sel_writer, 0, 3, false},
         {"gather_min", &g_tuning.gather_min, 0, 1 << 20, false},
         {"sq8_mfma_nt", &g_tuning.sq8_mfma_nt, 0, 1, false},
         {"sq8_mfma_queries", &g_tuning.sq8_mfma_queries, 16, 32, false},
@@ -593,6 +594,15 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
     }
     v->shard_tile_begin[n_shards] = (int32_t)tiles.size();
     v->n_tiles = (int)tiles.size();
+    // each tile's first row's slot in its shard's candidate region (the select path's collect)
+    std::vector<int32_t> tile_coff(std::max<size_t>(1, tiles.size()), 0);
+    for (int sh = 0; sh < n_shards; ++sh) {
+        int64_t acc = 0;
+        for (int t = v->shard_tile_begin[sh]; t < v->shard_tile_begin[sh + 1]; ++t) {
+            tile_coff[t] = (int32_t)std::min<int64_t>(acc, INT32_MAX);
+            acc += tiles[t].row_end - tiles[t].row_begin;
+        }
+    }
     OSK_REQUIRE(v->n_tiles < (1 << 24), "too many tiles");
 
     v->seg_doc_base.resize(n_segs);
@@ -610,6 +620,7 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
     OSK_HIP(v->d_tiles.reserve(sizeof(TileDev) * std::max<size_t>(1, tiles.size())));
     OSK_HIP(v->d_shard_tile_begin.reserve(sizeof(int32_t) * (n_shards + 1)));
     OSK_HIP(v->d_shard_index.reserve(sizeof(int32_t) * n_shards));
+    OSK_HIP(v->d_tile_coff.reserve(sizeof(int32_t) * tile_coff.size()));
     OSK_HIP(v->d_seg_vrow.reserve(sizeof(int64_t) * n_segs));
     OSK_HIP(v->d_counters.reserve(sizeof(unsigned long long) * 4));
     OSK_HIP(hipMemsetAsync(v->d_counters.p, 0, sizeof(unsigned long long) * 4, st));
@@ -621,6 +632,8 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
     OSK_HIP(hipMemcpyAsync(v->d_shard_tile_begin.p, v->shard_tile_begin.data(),
                            sizeof(int32_t) * (n_shards + 1), hipMemcpyHostToDevice, st));
     OSK_HIP(hipMemcpyAsync(v->d_shard_index.p, v->shard_index.data(), sizeof(int32_t) * n_shards,
+                           hipMemcpyHostToDevice, st));
+    OSK_HIP(hipMemcpyAsync(v->d_tile_coff.p, tile_coff.data(), sizeof(int32_t) * tile_coff.size(),
                            hipMemcpyHostToDevice, st));
     OSK_HIP(hipStreamSynchronize(st));
     for (osk_seg* sg : v->segs) sg->refs.fetch_add(1);   // released by ~osk_view
@@ -1310,13 +1323,16 @@ int32_t select_search(osk_view* v, const void* d_queries, int nq, int k, int UP,
         OSK_HIP(v->ws_sel_keys.reserve(sizeof(uint64_t) * std::max<int64_t>(1, total)));
     }
     OSK_HIP(v->ws_sel_state.reserve(sizeof(RadixState) * S));
-    OSK_HIP(v->ws_sel_hist.reserve(sizeof(uint32_t) * kSelBins * S));
+    OSK_HIP(v->ws_sel_hist.reserve(sizeof(uint32_t) * kSelBins * kSelRep * S));
     OSK_HIP(v->ws_sel_cand.reserve(sizeof(uint64_t) * (size_t)cap * S));
-    OSK_HIP(v->ws_sel_cnt.reserve(sizeof(int32_t) * S));
+    if (cap > kSelCap) OSK_HIP(v->ws_sel_cand2.reserve(sizeof(uint64_t) * (size_t)cap * S));
+    OSK_HIP(v->ws_sel_cnt.reserve(sizeof(int32_t) * std::max(1, v->n_tiles)));
     SelParams p{};
     p.segs = v->d_segs.as<SegDev>();
     p.tiles = v->d_tiles.as<TileDev>();
     p.seg_vrow = v->d_seg_vrow.as<int64_t>();
+    p.shard_tile_begin = v->d_shard_tile_begin.as<int32_t>();
+    p.tile_coff = v->d_tile_coff.as<int32_t>();
     p.accept = d_accept;
     p.n_tiles = v->n_tiles;
     p.n_shards = S;
@@ -1328,6 +1344,7 @@ int32_t select_search(osk_view* v, const void* d_queries, int nq, int k, int UP,
     p.units8 = u8;
     p.enc = v->enc;
     p.exact = bounds ? 0 : 1;
+    p.writer = g_tuning.sel_writer.load(std::memory_order_relaxed);
     p.rows8 = v->d_sq8_rows.as<const int4*>();
     p.aux = v->d_sq8_aux.as<const float4*>();
     p.gam = v->sq8_gam;
@@ -1338,7 +1355,8 @@ int32_t select_search(osk_view* v, const void* d_queries, int nq, int k, int UP,
     p.state = v->ws_sel_state.as<RadixState>();
     p.hist = v->ws_sel_hist.as<uint32_t>();
     p.cand = v->ws_sel_cand.as<uint64_t>();
-    p.cand_count = v->ws_sel_cnt.as<int32_t>();
+    p.cand2 = v->ws_sel_cand2.as<uint64_t>();
+    p.tile_count = v->ws_sel_cnt.as<int32_t>();
     p.cap = (int)cap;
     for (int q = 0; q < nq; ++q) {
         p.q = v->ws_q.as<char>() + (size_t)q * UP * 16;

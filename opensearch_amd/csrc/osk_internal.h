@@ -218,6 +218,10 @@ constexpr int kSelCap = 16384;       // candidates per (query, shard) the select
 constexpr int kSelDigit = 11;        // radix select digit width (2048-bin histograms)
 constexpr int kSelBins = 1 << kSelDigit;
 constexpr int kSelShift0 = 32 - kSelDigit;   // the first digit of a 32-bit LB
+// Global per-shard histograms are kept in kSelRep replicas (a tile adds into replica tile % kSelRep):
+// every tile of a shard adding into the same few bins serialised on those addresses (≈30 ns per
+// same-address device atomic: 40 µs per pass at C3)
+constexpr int kSelRep = 16;
 struct RadixState {
     uint64_t prefix;                 // the digits of the k-th largest value decided so far
     int32_t krem;                    // its rank among the values that share them
@@ -228,11 +232,14 @@ struct SelParams {
     const SegDev* segs;
     const TileDev* tiles;
     const int64_t* seg_vrow;
+    const int32_t* shard_tile_begin; // [n_shards + 1]: a shard's tiles are contiguous
+    const int32_t* tile_coff;        // [n_tiles]: the tile's first row's slot in its shard's candidate region
     const uint64_t* const* accept;
     unsigned long long* visited;     // [n_segs] or null
     int n_tiles, n_shards, n_segs;
     int k, sim, dim, units, units8, enc;
     int exact;                       // 1: 64-bit keys of exact scores; 0: int8 bounds LB/UB + exact re-score
+    int writer;                      // bounds writer variant (tune sel_writer)
     const void* q;                   // this query, padded (fp32 UP float4 / int8 16-B units)
     const float* qnorm;              // its |q|² in the device lane order (COSINE)
     const int4* q8;                  // bounds mode: its int8 copy and bound terms
@@ -244,9 +251,10 @@ struct SelParams {
     uint32_t* ub;
     uint64_t* keys;                  // exact mode, [view rows]
     RadixState* state;               // [n_shards]
-    uint32_t* hist;                  // [n_shards][kSelBins]
-    uint64_t* cand;                  // [n_shards][cap]
-    int32_t* cand_count;             // [n_shards]
+    uint32_t* hist;                  // [n_shards][kSelRep][kSelBins]
+    uint64_t* cand;                  // [n_shards][cap]: tile t's candidates at tile_coff[t] (no atomics)
+    uint64_t* cand2;                 // [n_shards][cap]: a shard's candidates packed (only past kSelCap)
+    int32_t* tile_count;             // [n_tiles]: candidates per tile
     int cap;                         // the largest shard's rows: a shard's candidates always fit
     uint64_t* out_keys;              // this query's [n_shards][k]
     int32_t* out_counts;             // [n_shards]
@@ -310,6 +318,8 @@ struct Tuning {
     std::atomic<int> sq8{1};              // certified int8 prefilter for float32 batches below mfma_min_batch
     std::atomic<int> gather_min{0};       // ...at most one gather tile per this many accepted rows (0 = every gather
                                           // tile; fewer, longer tiles were slower: profiles/r02c/gather_min_ab.jsonl)
+    std::atomic<int> sel_writer{1};       // select path bounds writer: 0 U4 + Java transform, 1 U4 fast COSINE
+                                          // bounds, 2 U2 fast, 3 U1 fast (same results; speed only)
     std::atomic<int> select_mid_k{1};     // float32 12 < k ≤ 64 with the prefilter on: the select path's int8
                                           // bounds pass instead of the fp32 streaming scan (0 = the scan)
     std::atomic<int> filter_gather{1};    // filtered prefilter scans (VALU sq8_scan) compact the accepted ordinals

@@ -151,7 +151,7 @@ struct osk_view {
     std::vector<int32_t> shard_index;
     std::vector<int32_t> shard_tile_begin;
     int n_tiles = 0;
-    osk::DevBuf d_segs, d_tiles, d_shard_tile_begin, d_shard_index;
+    osk::DevBuf d_segs, d_tiles, d_shard_tile_begin, d_shard_index, d_tile_coff;
     // workspace
     osk::DevBuf ws_cand, ws_q, ws_qnorm, ws_qin, ws_keys, ws_counts, ws_accept_ptrs, ws_accept,
         ws_out, ws_visited;
@@ -183,7 +183,7 @@ struct osk_view {
     // filter pushdown by compaction (osk_filter.hip): gather tiles over the compacted accepted ordinals
     // (one round of the chip, split over segments by rows), their settle slices, per-segment tile ranges
     // the select path (osk_select.hip, any k): per-row records of one query, radix state, candidates
-    osk::DevBuf ws_sel_lb, ws_sel_ub, ws_sel_keys, ws_sel_state, ws_sel_hist, ws_sel_cand, ws_sel_cnt;
+    osk::DevBuf ws_sel_lb, ws_sel_ub, ws_sel_keys, ws_sel_state, ws_sel_hist, ws_sel_cand, ws_sel_cand2, ws_sel_cnt;
     int64_t sel_calls = 0;
     bool gather_ready = false;
     int n_gtiles = 0, n_gslices = 0;

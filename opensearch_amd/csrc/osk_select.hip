@@ -140,11 +140,24 @@ __global__ __launch_bounds__(kSelThreads) void sel_keys_i8(SelParams p) {
     if (p.visited && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
 }
 
+// COSINE bounds without Java's double transform.  LB/UB only have to bracket the exact score: with
+// c = d/√(qn·xn) evaluated in fp32 (two v_rsq, two products: ≤ 2^-20·|c| from the real quotient) and
+// Java's (float)(d / sqrt((double)qn·xn)) then (1 + c)/2 within 2^-23 of the real value, an absolute
+// slack of 2^-17·max(1, |c|) keeps ub ≥ score(hi) ≥ the exact score ≥ score(lo) ≥ lb.  Degenerate norms
+// (0, inf, NaN) take the exact transform.
+__device__ __forceinline__ void cos_bounds_fast(float lo, float hi, float qn, float xn, float& lb, float& ub) {
+    const float r = rsqrtf(qn) * rsqrtf(xn);
+    const float ch = hi * r, cl = lo * r;
+    ub = fmaf(0.5f, ch, 0.5f) + 0x1p-17f * fmaxf(1.0f, fabsf(ch));
+    lb = fmaxf(0.0f, fmaf(0.5f, cl, 0.5f) - 0x1p-17f * fmaxf(1.0f, fabsf(cl)));
+}
+
 // bounds mode: the int8 prefilter copy's certified [lb, ub] score interval per row (sq8_scan's bound),
-// U row groups loaded before any is reduced (≈ U·V KiB in flight per wave, as sq8_scan)
-template <int L, int V, bool FILT>
+// U row groups loaded before any is reduced (≈ U·V KiB in flight per wave, as sq8_scan).  FAST: COSINE
+// through cos_bounds_fast instead of Java's double transform.
+template <int L, int V, bool FILT, int U, bool FAST>
 __global__ __launch_bounds__(kSelThreads) void sel_bounds(SelParams p) {
-    constexpr int R = 64 / L, U = 4;
+    constexpr int R = 64 / L;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int t = lane & (L - 1), g = lane / L;
     const TileDev tile = p.tiles[blockIdx.x];
@@ -208,8 +221,14 @@ __global__ __launch_bounds__(kSelThreads) void sel_bounds(SelParams p) {
             float lo, hi;
             sq8_bounds(sim, (float)acc, ax[u], qc, p.gam, p.g2, lo, hi);
             const float xnd = (sim == SIM_COSINE && valid[u]) ? seg.xnorm_f[row[u]] : 0.0f;
-            const float ub = sim == SIM_EUCLIDEAN ? score_f32_l2(lo) : score_f32(sim, hi, qnd, xnd);
-            const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qnd, xnd);
+            float ub, lb;
+            const bool degen = !(qnd > 0.0f && qnd < __builtin_inff() && xnd > 0.0f && xnd < __builtin_inff());
+            if (FAST && sim == SIM_COSINE && !__ballot(valid[u] && degen)) {   // (wave-uniform)
+                cos_bounds_fast(lo, hi, qnd, xnd, lb, ub);
+            } else {
+                ub = sim == SIM_EUCLIDEAN ? score_f32_l2(lo) : score_f32(sim, hi, qnd, xnd);
+                lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qnd, xnd);
+            }
             nvis += __popcll(__ballot(t == 0 && valid[u]));
             if (in[u] && t == 0) {   // every real score is ≥ 0, whose sortable form is ≥ 2^31: 0 = no row
                 p.lb[vbase + row[u]] = valid[u] ? float_to_sortable(lb) : 0u;
@@ -222,12 +241,13 @@ __global__ __launch_bounds__(kSelThreads) void sel_bounds(SelParams p) {
 
 // ---- radix select of the k-th largest LB (u32) / key (u64) per shard ---------------------------
 
+// grid: n_shards × kSelRep workgroups, each zeroing one replica (8 bins per thread)
 __global__ __launch_bounds__(256) void sel_init(SelParams p) {
-    for (int s = threadIdx.x; s < p.n_shards; s += 256) {
-        p.state[s] = RadixState{0ull, p.k, 0, 0};
-        p.cand_count[s] = 0;
-    }
-    for (int i = threadIdx.x; i < p.n_shards * kSelBins; i += 256) p.hist[i] = 0u;
+    if (blockIdx.x == 0)
+        for (int s = threadIdx.x; s < p.n_shards; s += 256) p.state[s] = RadixState{0ull, p.k, 0, 0};
+    uint4* h = reinterpret_cast<uint4*>(p.hist + (size_t)blockIdx.x * kSelBins);
+    h[2 * threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
+    h[2 * threadIdx.x + 1] = make_uint4(0u, 0u, 0u, 0u);
 }
 
 // digit `pass` of a 32-bit (bounds: LB) or 64-bit (exact: key) value: 11-bit digits from the top
@@ -284,48 +304,60 @@ __global__ __launch_bounds__(kSelThreads) void sel_hist(SelParams p, int pass) {
         }
     }
     __syncthreads();
+    uint32_t* g = p.hist + ((size_t)tile.shard * kSelRep + blockIdx.x % kSelRep) * kSelBins;
     for (int i = tid; i < kSelBins; i += kSelThreads)
-        if (h[i]) atomicAdd(&p.hist[(size_t)tile.shard * kSelBins + i], h[i]);
+        if (h[i]) atomicAdd(&g[i], h[i]);
 }
 
-// one wave per shard: the digit holding the krem-th largest value; lanes own 32 bins each, a suffix
-// scan over lanes finds the lane, that lane walks its bins
-__global__ __launch_bounds__(64) void sel_pick(SelParams p, int pass) {
-    const int s = blockIdx.x, lane = threadIdx.x;
+// one workgroup per shard: the digit holding the krem-th largest value.  Thread i sums bins
+// 8i … 8i+7 over the replicas (zeroing them for the next pass), a suffix scan over threads finds the
+// owner, the owner walks its bins.
+__global__ __launch_bounds__(256) void sel_pick(SelParams p, int pass) {
+    __shared__ uint32_t s_wave[4];
+    const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     RadixState st = p.state[s];
-    if (st.all) return;
+    if (st.all) return;   // (block-uniform)
     int shift, width;
     sel_digit(p.exact, pass, shift, width);
-    constexpr int kPer = kSelBins / 64;
-    uint32_t* hs = p.hist + (size_t)s * kSelBins;
-    uint32_t h[kPer];
+    uint32_t h[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    uint4* hs = reinterpret_cast<uint4*>(p.hist + (size_t)s * kSelRep * kSelBins);
+#pragma unroll
+    for (int r = 0; r < kSelRep; ++r) {
+        uint4* q = hs + (size_t)r * (kSelBins / 4) + 2 * tid;
+        const uint4 a = q[0], b = q[1];
+        q[0] = make_uint4(0u, 0u, 0u, 0u);
+        q[1] = make_uint4(0u, 0u, 0u, 0u);
+        h[0] += a.x; h[1] += a.y; h[2] += a.z; h[3] += a.w;
+        h[4] += b.x; h[5] += b.y; h[6] += b.z; h[7] += b.w;
+    }
     uint32_t sum = 0;
 #pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-        h[i] = hs[lane * kPer + i];
-        hs[lane * kPer + i] = 0u;   // ready for the next pass
-        sum += h[i];
-    }
-    uint32_t incl = sum;   // Σ over lanes ≥ this one
+    for (int i = 0; i < 8; ++i) sum += h[i];
+    uint32_t incl = sum;   // Σ over threads ≥ this one: within the wave, then the higher waves
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_down(incl, o);
         if (lane + o < 64) incl += y;
     }
-    const uint32_t total = __shfl(incl, 0);
+    if (lane == 0) s_wave[wave] = incl;
+    __syncthreads();
+    uint32_t total = 0;
+    for (int w = 0; w < 4; ++w) {
+        total += s_wave[w];
+        if (w > wave) incl += s_wave[w];
+    }
     const uint32_t above = incl - sum;
     if (pass == 0 && (int64_t)total <= (int64_t)st.krem) {   // ≤ k rows: take every one
-        if (lane == 0) {
+        if (tid == 0) {
             st.all = 1;
             p.state[s] = st;
         }
         return;
     }
-    const bool mine = (int64_t)above < (int64_t)st.krem && (int64_t)st.krem <= (int64_t)incl;
-    if (mine) {
+    if ((int64_t)above < (int64_t)st.krem && (int64_t)st.krem <= (int64_t)incl) {
         uint32_t cum = above;
-        for (int i = kPer - 1; i >= 0; --i) {
+        for (int i = 7; i >= 0; --i) {
             if ((int64_t)cum + h[i] >= (int64_t)st.krem) {
-                st.prefix |= (uint64_t)(lane * kPer + i) << shift;
+                st.prefix |= (uint64_t)(tid * 8 + i) << shift;
                 st.krem -= (int32_t)cum;
                 break;
             }
@@ -337,15 +369,20 @@ __global__ __launch_bounds__(64) void sel_pick(SelParams p, int pass) {
 
 // ---- collect / rescore / sort -----------------------------------------------------------------
 
+// Each tile appends its takes (in row order) to its own slots of the shard's candidate region,
+// [tile_coff, tile_coff + rows): no atomics.  (One device atomic per wave on a per-shard counter
+// serialised on those 8 addresses: 144 µs at C3, k = 100.)  Bounds mode stores the segment row.
 template <bool EXACT>
 __global__ __launch_bounds__(kSelThreads) void sel_collect(SelParams p) {
-    const int tid = threadIdx.x, lane = tid & 63;
+    __shared__ int s_wave[4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const TileDev tile = p.tiles[blockIdx.x];
     const int s = tile.shard;
     const RadixState st = p.state[s];
     const uint64_t thr = st.all ? 1ull : st.prefix;
     const int64_t vbase = p.seg_vrow[tile.seg];
-    uint64_t* out = p.cand + (size_t)s * p.cap;
+    uint64_t* out = p.cand + (size_t)s * p.cap + p.tile_coff[blockIdx.x];
+    int run = 0;   // takes so far (block-uniform)
     for (int64_t r0 = tile.row_begin; r0 < tile.row_end; r0 += 4 * kSelThreads) {
         uint64_t val[4];
         bool take[4];
@@ -353,16 +390,15 @@ __global__ __launch_bounds__(kSelThreads) void sel_collect(SelParams p) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int64_t r = r0 + u * kSelThreads + tid;
-            take[u] = false;
-            val[u] = 0ull;
             const int64_t rc = min(r, tile.row_end - 1);   // unconditional loads (see sel_hist)
-            const uint64_t v = EXACT ? p.keys[vbase + rc] : (uint64_t)p.ub[vbase + rc];   // the UB, then the row
+            const uint64_t v = EXACT ? p.keys[vbase + rc] : (uint64_t)p.ub[vbase + rc];
             val[u] = r < tile.row_end ? v : 0ull;
         }
+        // a thread's takes are ordered u-major; the tile's order only has to be deterministic
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             take[u] = val[u] && val[u] >= thr;
-            if (!EXACT) val[u] = (uint64_t)(vbase + r0 + u * kSelThreads + tid);
+            if (!EXACT) val[u] = (uint64_t)(r0 + u * kSelThreads + tid);
             c += take[u];
         }
         int incl = c;   // wave prefix of the takes
@@ -370,47 +406,44 @@ __global__ __launch_bounds__(kSelThreads) void sel_collect(SelParams p) {
             const int y = __shfl_up(incl, o);
             if (lane >= o) incl += y;
         }
-        const int tot = __shfl(incl, 63);
-        if (!tot) continue;
-        int base = 0;
-        if (lane == 63) base = atomicAdd(&p.cand_count[s], tot);
-        base = __shfl(base, 63) + incl - c;
+        if (lane == 63) s_wave[wave] = incl;
+        __syncthreads();
+        int base = run + incl - c, tot = 0;
+        for (int w = 0; w < 4; ++w) {
+            const int sw = s_wave[w];
+            tot += sw;
+            if (w < wave) base += sw;
+        }
+        __syncthreads();   // s_wave is rewritten by the next iteration
+        run += tot;
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            if (take[u]) {
-                if (base < p.cap) out[base] = val[u];   // (cap = the shard's rows: never exceeded)
-                ++base;
-            }
+            if (take[u]) out[base++] = val[u];   // ≤ the tile's rows: inside its slots
     }
+    if (tid == 0) p.tile_count[blockIdx.x] = run;
 }
 
+// bounds mode: one workgroup per tile re-scores its candidates (segment rows) exactly → hit keys
 template <int L, int V, bool L2K>
 __global__ __launch_bounds__(kSelThreads) void sel_rescore(SelParams p) {
-    constexpr int R = 64 / L, UP = L * V;
+    constexpr int R = 64 / L;
+    const int n = p.tile_count[blockIdx.x];
+    if (n == 0) return;   // (block-uniform; most tiles)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int t = lane & (L - 1), gr = lane / L;
-    const int s = blockIdx.x;
-    const int n = min(p.cand_count[s], p.cap);
+    const TileDev tile = p.tiles[blockIdx.x];
+    const SegDev seg = p.segs[tile.seg];
     const float4* __restrict__ Q = static_cast<const float4*>(p.q);
     float4 qf[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) qf[j] = Q[t + j * L];
-    (void)UP;
     const float qn = (!L2K && p.sim == SIM_COSINE) ? p.qnorm[0] : 0.0f;
-    uint64_t* c = p.cand + (size_t)s * p.cap;
-    const int stride = gridDim.y * 4 * R;
-    for (int i0 = (blockIdx.y * 4 + wave) * R; i0 < n; i0 += stride) {
+    uint64_t* c = p.cand + (size_t)tile.shard * p.cap + p.tile_coff[blockIdx.x];
+    for (int i0 = wave * R; i0 < n; i0 += 4 * R) {
         const int ci = i0 + gr;
         const bool valid = ci < n;
-        const int64_t vrow = valid ? (int64_t)c[ci] : 0;
-        // the row's segment: the last with seg_vrow ≤ vrow (binary search; ascending)
-        int lo = 0, hi = p.n_segs - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (p.seg_vrow[mid] <= vrow) lo = mid; else hi = mid - 1;
-        }
-        const SegDev seg = p.segs[lo];
-        const int64_t ord = vrow - p.seg_vrow[lo];
+        // (clamped into the tile: a row index outside it is never loaded)
+        const int64_t ord = min(max(valid ? (int64_t)c[ci] : tile.row_begin, tile.row_begin), tile.row_end - 1);
         const int32_t doc = valid ? (seg.ord_to_doc ? seg.ord_to_doc[ord] : (int32_t)ord) : 0;
         const float xn = (!L2K && p.sim == SIM_COSINE && valid) ? seg.xnorm_f[ord] : 0.0f;
         const float sc = settle_exact<L, V, L2K>(static_cast<const float4*>(seg.rows) + ord * p.units, valid, p.units,
@@ -443,19 +476,65 @@ __device__ __forceinline__ void bitonic_desc(uint64_t* sk, int np, int tid) {
 // (n ≤ 2k + 256, in LDS): one bitonic sort.  Otherwise: a radix select (8-bit digits, LDS histogram)
 // of the kk-th largest key over the candidates (in LDS when n ≤ kSelCap, else in global memory), the
 // kk keys ≥ it gathered into the output slots, then sorted in LDS.
+// The shard's tiles' candidate runs are packed first (into LDS, or cand2 past kSelCap): 1024 tiles
+// at a time, their counts block-scanned, one wave copying each tile's run.
 __global__ __launch_bounds__(1024) void sel_sort(SelParams p) {
     extern __shared__ __attribute__((aligned(16))) uint64_t sk[];
     __shared__ uint32_t h[256];
+    __shared__ int s_off[1024], s_coff[1024];
+    __shared__ int s_wsum[16];
     __shared__ uint64_t s_prefix;
     __shared__ int s_krem, s_ctr;
-    const int s = blockIdx.x, tid = threadIdx.x;
-    const int n = min(p.cand_count[s], p.cap);
+    const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tb = p.shard_tile_begin[s], te = p.shard_tile_begin[s + 1];
+    const uint64_t* c = p.cand + (size_t)s * p.cap;
+    // n = Σ tile counts
+    int part = 0;
+    for (int t = tb + tid; t < te; t += 1024) part += p.tile_count[t];
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+    if (lane == 0) s_wsum[wave] = part;
+    __syncthreads();
+    int n = 0;
+    for (int w = 0; w < 16; ++w) n += s_wsum[w];
+    n = min(n, p.cap);
     const int kk = min(p.k, n);
     uint64_t* ok = p.out_keys + (size_t)s * p.k;
-    const uint64_t* c = p.cand + (size_t)s * p.cap;
     const bool in_lds = n <= kSelCap;
-    if (in_lds)
-        for (int i = tid; i < n; i += 1024) sk[i] = c[i];
+    uint64_t* dst = in_lds ? sk : p.cand2 + (size_t)s * p.cap;
+    // pack: per 1024 tiles, their counts block-scanned into s_off, then every entry of the chunk copied
+    // by one thread (its tile found by binary search over s_off): all loads independent
+    int base = 0;
+    for (int t0 = tb; t0 < te; t0 += 1024) {
+        __syncthreads();   // s_wsum / s_off / s_coff of the previous round are consumed
+        const int t = t0 + tid;
+        const int cnt = t < te ? p.tile_count[t] : 0;
+        int incl = cnt;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) s_wsum[wave] = incl;
+        __syncthreads();
+        int pre = incl - cnt, tot = 0;
+        for (int w = 0; w < 16; ++w) {
+            tot += s_wsum[w];
+            if (w < wave) pre += s_wsum[w];
+        }
+        s_off[tid] = pre;   // chunk-relative start of tile t0 + tid's run
+        s_coff[tid] = t < te ? p.tile_coff[t] : 0;
+        __syncthreads();
+        const int nj = min(1024, te - t0);
+        for (int e = tid; e < tot; e += 1024) {
+            int lo = 0, hi = nj - 1;   // the last tile whose run starts at or before e
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (s_off[mid] <= e) lo = mid; else hi = mid - 1;
+            }
+            if (base + e < n) dst[base + e] = c[s_coff[lo] + (e - s_off[lo])];
+        }
+        base += tot;
+    }
+    __syncthreads();   // (cand2 is written and read by this workgroup only)
     if (in_lds && n <= 2 * kk + 256) {
         int np = 2;
         while (np < n) np <<= 1;
@@ -465,7 +544,7 @@ __global__ __launch_bounds__(1024) void sel_sort(SelParams p) {
         if (tid == 0) p.out_counts[s] = kk;
         return;
     }
-    const uint64_t* src = in_lds ? sk : c;
+    const uint64_t* src = dst;
     if (tid == 0) {
         s_prefix = 0ull;
         s_krem = kk;
@@ -653,10 +732,15 @@ static const SelFn kSelKeysI8[9] = {sel_keys_i8<4, 2>,  sel_keys_i8<8, 2>,  sel_
 static const SelFn kSelRescore[9][2] = {OSK_SEL_RS(4, 2),  OSK_SEL_RS(8, 2),  OSK_SEL_RS(8, 4),
                                         OSK_SEL_RS(16, 4), OSK_SEL_RS(16, 8), OSK_SEL_RS(16, 12),
                                         OSK_SEL_RS(32, 8), OSK_SEL_RS(64, 8), OSK_SEL_RS(64, 16)};
-// int8 prefilter lane configs by 16-byte units (sq8_cfg's)
-#define OSK_SEL_B(L, V) {sel_bounds<L, V, false>, sel_bounds<L, V, true>}
-static const SelFn kSelBounds[8][2] = {OSK_SEL_B(4, 1),  OSK_SEL_B(8, 1),  OSK_SEL_B(16, 1), OSK_SEL_B(16, 2),
-                                       OSK_SEL_B(16, 3), OSK_SEL_B(16, 4), OSK_SEL_B(32, 4), OSK_SEL_B(64, 4)};
+// int8 prefilter lane configs by 16-byte units (sq8_cfg's) × writer variant (tune sel_writer):
+// 0 = U 4, Java transform; 1 = U 4, fast COSINE bounds; 2 = U 2, fast; 3 = U 1, fast
+#define OSK_SEL_B(L, V)                                                                                          \
+    {{sel_bounds<L, V, false, 4, false>, sel_bounds<L, V, true, 4, false>},                                   \
+     {sel_bounds<L, V, false, 4, true>, sel_bounds<L, V, true, 4, true>},                                     \
+     {sel_bounds<L, V, false, 2, true>, sel_bounds<L, V, true, 2, true>},                                     \
+     {sel_bounds<L, V, false, 1, true>, sel_bounds<L, V, true, 1, true>}}
+static const SelFn kSelBounds[8][4][2] = {OSK_SEL_B(4, 1),  OSK_SEL_B(8, 1),  OSK_SEL_B(16, 1), OSK_SEL_B(16, 2),
+                                          OSK_SEL_B(16, 3), OSK_SEL_B(16, 4), OSK_SEL_B(32, 4), OSK_SEL_B(64, 4)};
 static int sel_bounds_cfg(int u8) {
     return u8 <= 4 ? 0 : u8 <= 8 ? 1 : u8 <= 16 ? 2 : u8 <= 32 ? 3 : u8 <= 48 ? 4 : u8 <= 64 ? 5 : u8 <= 128 ? 6 : 7;
 }
@@ -666,10 +750,10 @@ static int sel_bounds_cfg(int u8) {
 hipError_t launch_select_one(const SelParams& p, int cfg, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
     if (p.n_tiles <= 0) return hipSuccess;
     const dim3 tg(p.n_tiles), tb(kSelThreads);
-    hipLaunchKernelGGL(sel_init, dim3(1), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(sel_init, dim3(p.n_shards * kSelRep), dim3(256), 0, s, p);
     // the writer (stamped by the profile events when given)
     SelFn writer = p.exact ? (p.enc == ENC_BYTE ? kSelKeysI8[cfg] : kSelKeysF32[cfg][p.sim == SIM_EUCLIDEAN ? 1 : 0])
-                           : kSelBounds[sel_bounds_cfg(p.units8)][p.accept ? 1 : 0];
+                           : kSelBounds[sel_bounds_cfg(p.units8)][p.writer & 3][p.accept ? 1 : 0];
     if (ev_start || ev_stop)
         hipExtLaunchKernelGGL(writer, tg, tb, 0, s, ev_start, ev_stop, 0, p);
     else
@@ -677,11 +761,11 @@ hipError_t launch_select_one(const SelParams& p, int cfg, hipStream_t s, hipEven
     const int passes = ((p.exact ? 64 : 32) + kSelDigit - 1) / kSelDigit;   // 6 (u64) or 3 (u32)
     for (int i = 0; i < passes; ++i) {
         hipLaunchKernelGGL(p.exact ? sel_hist<true> : sel_hist<false>, tg, tb, 0, s, p, i);
-        hipLaunchKernelGGL(sel_pick, dim3(p.n_shards), dim3(64), 0, s, p, i);
+        hipLaunchKernelGGL(sel_pick, dim3(p.n_shards), dim3(256), 0, s, p, i);
     }
     hipLaunchKernelGGL(p.exact ? sel_collect<true> : sel_collect<false>, tg, tb, 0, s, p);
     if (!p.exact)
-        hipLaunchKernelGGL(kSelRescore[cfg][p.sim == SIM_EUCLIDEAN ? 1 : 0], dim3(p.n_shards, 64), tb, 0, s, p);
+        hipLaunchKernelGGL(kSelRescore[cfg][p.sim == SIM_EUCLIDEAN ? 1 : 0], tg, tb, 0, s, p);
     hipLaunchKernelGGL(sel_sort, dim3(p.n_shards), dim3(1024), (size_t)kSelCap * 8, s, p);
     return hipGetLastError();
 }

@@ -206,3 +206,19 @@ def test_select_multi_shard_large_merge(k, from_, size):
         ds.close()
         for r in readers:
             r.close()
+
+
+@pytest.mark.parametrize("writer", [0, 1, 2, 3])
+@pytest.mark.parametrize("sim", SIMS, ids=lambda s: s.name)
+def test_select_bounds_writer_variants(writer, sim):
+    """Every bounds writer (row groups in flight, Java or fp32 COSINE bound transform) gives the exact
+    answer.  (Zero vectors cannot reach a COSINE field: Lucene rejects them at index and query time.)"""
+    rows = corpus(20000, 192, sim, 390)
+    queries = corpus(2, 192, sim, 391)
+    r = LU.GpuFlatVectorsReader("v", rows, sim)
+    _lib.tune("sel_writer", writer)
+    try:
+        check_reader(r, rows, queries, 100, sim)
+    finally:
+        _lib.tune("sel_writer", 1)
+        r.close()

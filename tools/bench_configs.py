@@ -13,6 +13,9 @@ prefilter path, the rate of the bytes it actually reads (int8_prefilter_GBps).  
   C4  100M × 96 fp32 DOT_PRODUCT (unit rows), 8 shards        batch 1 and 1024 (one GPU holds all 100M)
   C5f 10M × 768 COSINE, Bernoulli(s) accept bitsets, s ∈ {1%, 10%, 50%}, batch 1
   C5i 10M × 768 int8 (U{−128..127}), EUCLIDEAN, batch 1
+  C3o C3 with outlier dimensions (robustness of the int8 prefilter): N(0,1) rows whose `dims` evenly
+      spaced dimensions are scaled ×`scale` before the rows are L2-normalised (--outlier dims:scale,...),
+      batch 1, prefilter on and off (the fp32 scan), with rescored rows and exactly re-scanned lists
 """
 import argparse
 import ctypes as C
@@ -48,6 +51,41 @@ class View:
         L.osk_view_release(self.v)
         for h in self.segs:
             L.osk_seg_release(C.c_void_p(h))
+
+
+class TorchView(View):
+    """A view whose shards are staged from device tensors (make(s) -> [rows, dim] float32 on cuda)."""
+
+    def __init__(self, n_shards, rows_per_shard, dim, sim, make):
+        self.segs = []
+        for s in range(n_shards):
+            x = make(s).contiguous()
+            torch.cuda.synchronize()   # the library's stream does not wait on torch's (osknn.h)
+            h = C.c_void_p()
+            _lib.check(L.osk_seg_stage_device(0, x.data_ptr(), dim * 4, rows_per_shard, dim, _lib.FLOAT32, sim, None,
+                                              rows_per_shard, C.byref(h)))
+            torch.cuda.synchronize()
+            del x
+            self.segs.append(h.value)
+        arr = (C.c_void_p * n_shards)(*self.segs)
+        ss = np.arange(n_shards, dtype=np.int32)
+        self.v = C.c_void_p()
+        _lib.check(L.osk_view_create(arr, n_shards, ss.ctypes.data, None, n_shards, None, C.byref(self.v)))
+        self.n_shards, self.rows, self.dim, self.enc = n_shards, rows_per_shard, dim, _lib.FLOAT32
+
+
+def outlier_rows(n, dim, n_out, scale, seed):
+    """N(0,1) rows, n_out evenly spaced dimensions ×scale, then L2-normalised."""
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    x = torch.randn((n, dim), generator=g, device="cuda", dtype=torch.float32)
+    if n_out:
+        x[:, torch.arange(n_out, device="cuda") * (dim // n_out)] *= scale
+    return x / x.norm(dim=1, keepdim=True)
+
+
+def qpool_dev(n, dim, dist):
+    return torch.from_numpy(synth_host(0, n, dim, 43, dist)).cuda()
 
 
 def run(view, queries, batch, steps, warmup, accept_ptrs=None, k=10):
@@ -108,6 +146,7 @@ def main():
     ap.add_argument("--c4-batches", default="1,1024")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE")
     ap.add_argument("--c5f-sel", default="0.01,0.1,0.5", help="C5f selectivities")
+    ap.add_argument("--outlier", default="0:1,8:10,8:30,32:10", help="C3o corpora dims:scale, comma-separated")
     ap.add_argument("--c5f-modes", default="1:0,0:0",
                     help="C5f filter modes filter_gather:gather_min, comma-separated (1:0 = compacted gather, 0:0 = "
                          "bitset window walk)")
@@ -166,6 +205,24 @@ def main():
                 _lib.tune("filter_gather", 1)
                 _lib.tune("gather_min", 0)
         v.close()
+    if "C3o" in only:
+        for spec in a.outlier.split(","):
+            n_out, scale = (float(x) for x in spec.split(":"))
+            n_out = int(n_out)
+            v = TorchView(8, 1_250_000, 768, _lib.COSINE, lambda s: outlier_rows(1_250_000, 768, n_out, scale, 100 + s))
+            q = outlier_rows(512, 768, n_out, scale, 99)
+            for sq8 in (1, 0):
+                _lib.tune("sq8", sq8)
+                r0, x0 = counter(v, "sq8_rescored_rows"), counter(v, "sq8_exact_tiles")
+                f0 = counter(v, "sq8_fallback_queries")
+                ms, km = run(v, q, 1, st, wu)
+                emit(f"C3o-{n_out}x{scale:g}", v, 1, ms, km, 10_000_000 * 768 * 4,
+                     {"outlier_dims": n_out, "outlier_scale": scale, "prefilter": sq8,
+                      "rescored_rows_per_query": (counter(v, "sq8_rescored_rows") - r0) / (st + wu),
+                      "exact_lists_per_query": (counter(v, "sq8_exact_tiles") - x0) / (st + wu),
+                      "fallback_queries": counter(v, "sq8_fallback_queries") - f0})
+            _lib.tune("sq8", 1)
+            v.close()
     if "C4" in only:
         v = View(8, 12_500_000, 96, _lib.DOT_PRODUCT, _lib.FLOAT32, _lib.DIST_NORMALISH_UNIT)
         q = qpool(2048, 96, _lib.DIST_NORMALISH_UNIT)
