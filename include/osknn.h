@@ -235,7 +235,7 @@ int32_t osk_view_scan_time(osk_view* view, double* total_ms, int64_t* calls);
  *   "select_mid_k"    0|1 float32 searches with 12 < k ≤ 64 take the select path over int8 bounds
  *                     (default 1) instead of the fp32 streaming scan; k > 64 always takes it
  *   "sel_writer"      select path bounds writer: 0 = 4 row groups in flight + Java's transform,
- *                     1 = 4 groups + fp32 COSINE bounds (default), 2 = 2 groups, 3 = 1 group (fast bounds)
+ *                     1 = 4 groups + fp32 COSINE bounds, 2 = 2 groups (default), 3 = 1 group (fast bounds)
  * The testing build (libosknn_testing.so) also accepts "sq8_mfma_ablate", "mfma_ablate" (A/B timing,
  * results wrong), "sq8_force_fallback" (every prefilter list re-scanned exactly) and "settle_trace";
  * the shipped library returns OSK_ERR_UNSUPPORTED for them. */

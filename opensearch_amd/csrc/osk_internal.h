@@ -318,7 +318,7 @@ struct Tuning {
     std::atomic<int> sq8{1};              // certified int8 prefilter for float32 batches below mfma_min_batch
     std::atomic<int> gather_min{0};       // ...at most one gather tile per this many accepted rows (0 = every gather
                                           // tile; fewer, longer tiles were slower: profiles/r02c/gather_min_ab.jsonl)
-    std::atomic<int> sel_writer{1};       // select path bounds writer: 0 U4 + Java transform, 1 U4 fast COSINE
+    std::atomic<int> sel_writer{2};       // select path bounds writer: 0 U4 + Java transform, 1 U4 fast COSINE
                                           // bounds, 2 U2 fast, 3 U1 fast (same results; speed only)
     std::atomic<int> select_mid_k{1};     // float32 12 < k ≤ 64 with the prefilter on: the select path's int8
                                           // bounds pass instead of the fp32 streaming scan (0 = the scan)

@@ -220,5 +220,5 @@ def test_select_bounds_writer_variants(writer, sim):
     try:
         check_reader(r, rows, queries, 100, sim)
     finally:
-        _lib.tune("sel_writer", 1)
+        _lib.tune("sel_writer", 2)
         r.close()
