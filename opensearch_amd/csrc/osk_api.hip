@@ -250,6 +250,7 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         {"sq8_mfma_nt", &g_tuning.sq8_mfma_nt, 0, 1, false},
         {"sq8_mfma_queries", &g_tuning.sq8_mfma_queries, 16, 32, false},
         {"sq8_mfma_min", &g_tuning.sq8_mfma_min, 0, 1 << 20, false},
+        {"sq8_mfma_ring", &g_tuning.sq8_mfma_ring, -1, 8, false},
         {"sq8_mfma_ablate", &g_tuning.sq8_mfma_ablate, 0, 3, true},
         {"sq8_force_fallback", &g_tuning.sq8_force_fallback, 0, 1, true},
         {"settle_trace", &g_tuning.settle_trace, 0, 1, true},
@@ -1228,6 +1229,7 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             p.k = k;
             p.n_shards = S;
             p.nt = g_tuning.sq8_mfma_nt;
+            p.ring_slots = sq8_ring_slots(u8, p.q_count > 16 ? 2 : 1, g_tuning.sq8_mfma_ring);
             p.ablate = g_tuning.sq8_mfma_ablate;
             p.pilot = 1;
             p.pilot_keys = v->ws_pilot.as<uint64_t>();

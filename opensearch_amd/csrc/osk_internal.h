@@ -149,6 +149,8 @@ struct Sq8Params {
     const int4* const* rows8t;       // sq8_mfma: per segment, the tiled int8 copy (launch_sq8_tile)
     int nt;                          // sq8_mfma: non-temporal row loads (A/B knob sq8_mfma_nt)
     int ablate;                      // A/B timing only (results wrong): 1 skip the epilogue, 2 skip the MFMAs
+    int ring_slots;                  // sq8_mfma: > 1 = LDS-DMA ring of this many 16-row groups per wave
+                                     // (unfiltered, ≤ 256 dims; tune sq8_mfma_ring), 0 = register loads
     int k;
     int n_shards;
     uint64_t* pilot_keys;
@@ -285,7 +287,8 @@ int sq8_lanes(int units8);         // lanes per row of the int8 scan
 constexpr int kMfmaQueries = 32;
 constexpr int kMfmaScanR = 16;      // its rows per wave-iteration (the settle's scan_R)
 int sq8_mfma_supported(int units8);
-int sq8_mfma_ks(int units8);        // its 64-dim k-steps per row for this row width
+int sq8_mfma_ks(int units8);
+int sq8_ring_slots(int units8, int qb, int want);   // sq8_mfma LDS-DMA ring depth (0 = register loads)        // its 64-dim k-steps per row for this row width
 // row-major int8 rows → blocks of 16 rows × ks slabs of 1 KiB (row r of a block at r·64 B; zero past
 // the last row and past units8)
 hipError_t launch_sq8_tile(const void* q8, int64_t n_rows, int units8, int ks, void* out, hipStream_t s);
@@ -325,6 +328,8 @@ struct Tuning {
     std::atomic<int> filter_gather{1};    // filtered prefilter scans (VALU sq8_scan) compact the accepted ordinals
                                           // first and scan them (osk_filter.hip); 0 = walk the bitset windows
     std::atomic<int> sq8_mfma_nt{1};      // A/B: non-temporal row loads in sq8_mfma
+    std::atomic<int> sq8_mfma_ring{-1};   // sq8_mfma LDS-DMA ring slots per wave (≤ 256 dims, unfiltered):
+                                          // -1 = as many as fit 2 workgroups per CU, 0 = off (register loads)
     std::atomic<int> sq8_mfma_queries{32};    // queries per sq8_mfma launch: 16 or 32 (two MFMA chains per row operand)
     std::atomic<int> sq8_mfma_ablate{0};  // TESTING. A/B timing only: 1 skip sq8_mfma's epilogue, 2 its MFMAs (results wrong)
     std::atomic<int> sq8_mfma_min{2};     // prefilter batches ≥ this scan on int8 MFMA, 16 queries per launch (0 = never)

@@ -49,7 +49,7 @@ __global__ __launch_bounds__(kBlock) void scan_f32(ScanParams p) {
     float4* sq = reinterpret_cast<float4*>(smem);
     uint64_t* slist = reinterpret_cast<uint64_t*>(smem + (QREG ? 0 : NQ * UP * 16));
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform: scalar loop control
     const int t = lane & (L - 1), g = lane / L;
     const TileDev tile = p.tiles[blockIdx.x];
     const SegDev seg = p.segs[tile.seg];
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(kBlock) void scan_i8(ScanParams p) {
     int4* sq = reinterpret_cast<int4*>(smem);
     uint64_t* slist = reinterpret_cast<uint64_t*>(smem + (QREG ? 0 : NQ * UP * 16));
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform: scalar loop control
     const int t = lane & (L - 1), g = lane / L;
     const TileDev tile = p.tiles[blockIdx.x];
     const SegDev seg = p.segs[tile.seg];
@@ -520,7 +520,7 @@ __global__ __launch_bounds__(kBlock) void merge_shards(const uint64_t* __restric
                                                        int32_t* __restrict__ shard_counts) {
     __shared__ uint64_t lists[4 * 64];
     const int s = blockIdx.x, b = blockIdx.y;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int t0 = shard_tile_begin[s], t1 = shard_tile_begin[s + 1];
     const uint64_t* c = cand + ((size_t)b * n_tiles + t0) * k;
     const int64_t n = (int64_t)(t1 - t0) * k;

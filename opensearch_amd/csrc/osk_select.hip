@@ -59,7 +59,7 @@ __device__ __forceinline__ void wave_rows(const TileDev& tile, int wave, int64_t
 template <int L, int V, bool L2K>
 __global__ __launch_bounds__(kSelThreads) void sel_keys_f32(SelParams p) {
     constexpr int R = 64 / L;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform: scalar loop control
     const int t = lane & (L - 1), g = lane / L;
     const TileDev tile = p.tiles[blockIdx.x];
     const SegDev seg = p.segs[tile.seg];
@@ -90,7 +90,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_keys_f32(SelParams p) {
 template <int L, int V>
 __global__ __launch_bounds__(kSelThreads) void sel_keys_i8(SelParams p) {
     constexpr int R = 64 / L;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform: scalar loop control
     const int t = lane & (L - 1), g = lane / L;
     const TileDev tile = p.tiles[blockIdx.x];
     const SegDev seg = p.segs[tile.seg];
@@ -158,7 +158,7 @@ __device__ __forceinline__ void cos_bounds_fast(float lo, float hi, float qn, fl
 template <int L, int V, bool FILT, int U, bool FAST>
 __global__ __launch_bounds__(kSelThreads) void sel_bounds(SelParams p) {
     constexpr int R = 64 / L;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform: scalar loop control
     const int t = lane & (L - 1), g = lane / L;
     const TileDev tile = p.tiles[blockIdx.x];
     const SegDev seg = p.segs[tile.seg];
@@ -314,7 +314,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_hist(SelParams p, int pass) {
 // owner, the owner walks its bins.
 __global__ __launch_bounds__(256) void sel_pick(SelParams p, int pass) {
     __shared__ uint32_t s_wave[4];
-    const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform: scalar loop control
     RadixState st = p.state[s];
     if (st.all) return;   // (block-uniform)
     int shift, width;
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(256) void sel_pick(SelParams p, int pass) {
 template <bool EXACT>
 __global__ __launch_bounds__(kSelThreads) void sel_collect(SelParams p) {
     __shared__ int s_wave[4];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform: scalar loop control
     const TileDev tile = p.tiles[blockIdx.x];
     const int s = tile.shard;
     const RadixState st = p.state[s];
@@ -429,7 +429,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_rescore(SelParams p) {
     constexpr int R = 64 / L;
     const int n = p.tile_count[blockIdx.x];
     if (n == 0) return;   // (block-uniform; most tiles)
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform: scalar loop control
     const int t = lane & (L - 1), gr = lane / L;
     const TileDev tile = p.tiles[blockIdx.x];
     const SegDev seg = p.segs[tile.seg];
@@ -485,7 +485,7 @@ __global__ __launch_bounds__(1024) void sel_sort(SelParams p) {
     __shared__ int s_wsum[16];
     __shared__ uint64_t s_prefix;
     __shared__ int s_krem, s_ctr;
-    const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform: scalar loop control
     const int tb = p.shard_tile_begin[s], te = p.shard_tile_begin[s + 1];
     const uint64_t* c = p.cand + (size_t)s * p.cap;
     // n = Σ tile counts

@@ -115,7 +115,7 @@ __global__ __launch_bounds__(kBlock) void sq8_prep(const float* __restrict__ src
     __shared__ float s_m[4];
     __shared__ long long s_a[4];
     __shared__ double s_e[4], s_x[4];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform: scalar loop control
     const int64_t r = blockIdx.x;
     const bool real = r < nq;
     const float* b = src + r * (int64_t)dim;
@@ -312,7 +312,7 @@ __device__ __forceinline__ void gather_wave_range(int64_t cnt, int j, int nj, in
 template <int L, int V, int NQ, int U, int MODE = kScanRows>
 __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
     constexpr int R = 64 / L;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform: scalar loop control
     const int t = lane & (L - 1), g = lane / L;
     TileDev tile;
     int4 gt = make_int4(0, 0, 0, 1);
@@ -417,7 +417,7 @@ __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 nvis += __popcll(__ballot(t == 0 && valid[u]));
-                const float sx = sim == SIM_COSINE ? sqrtf(ax[u].w) : 0.0f;
+                const float sx = sim == SIM_COSINE ? __builtin_amdgcn_sqrtf(ax[u].w) : 0.0f;   // (1 ulp ≪ the quick test's slack)
                 int acc = 0;
 #pragma unroll
                 for (int j = 0; j < V; ++j) {
@@ -469,7 +469,7 @@ __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 nvis += __popcll(__ballot(t == 0 && valid[u]));
-                const float sx = sim == SIM_COSINE ? sqrtf(ax[u].w) : 0.0f;
+                const float sx = sim == SIM_COSINE ? __builtin_amdgcn_sqrtf(ax[u].w) : 0.0f;   // (1 ulp ≪ the quick test's slack)
                 rs_reduce<L, NQ>(acc[u], t);
                 bool pass[P];
                 float lo[P], hi[P];
@@ -622,21 +622,72 @@ hipError_t launch_sq8_scan(int nq, const Sq8Params& p, hipStream_t s, hipEvent_t
 // numbering are sq8_scan's with R = 16 rows per wave-iteration (the settle re-scans with scan_R = 16).
 // Filter pushdown: accepted rows are compacted 64 at a time; any row can feed any MFMA row slot.
 // ------------------------------------------------------------------------------------------------
+// LDS-DMA (global_load_lds_dwordx4) from a per-lane source into a wave-uniform LDS base (+ lane·16 B).
+// Written as asm so the compiler keeps no bookkeeping for it (its own LDS-DMA tracking puts vmcnt(0)
+// before every LDS read of the buffer): completion is counted by hand (vm_wait), and only the issuing
+// wave reads what it loaded.  M0 is saved and restored inside the statement (compiler-reserved).
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_byte) {
+    lds_byte = __builtin_amdgcn_readfirstlane(lds_byte);   // wave-uniform by construction; make it an SGPR
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_byte)
+                 : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// sq8_mfma's LDS-DMA ring: a group slot holds the group's 16 rows (row-major, exact width) then their
+// 16 bound terms.  The rows take KS LDS-DMA instructions; a slot holds exactly 16·u8 units when the
+// last instruction still has a lane of real data (u8 > 4(KS − 1)), else all KS·64 lanes land (clamped
+// sources) — either way every instruction has an active lane, so each group is KS + 1 counted ops.
+__host__ __device__ __forceinline__ int ring_rows_units(int u8, int ks) {
+    return u8 > 4 * (ks - 1) ? 16 * u8 : ks * 64;
+}
+
+// wait until at most n·OPS of this wave's vector-memory operations are outstanding (n ≤ 7)
+template <int OPS>
+__device__ __forceinline__ void vm_wait_groups(int n) {
+    switch (n) {
+        case 0: vm_wait<0>(); break;
+        case 1: vm_wait<OPS>(); break;
+        case 2: vm_wait<2 * OPS>(); break;
+        case 3: vm_wait<3 * OPS>(); break;
+        case 4: vm_wait<4 * OPS>(); break;
+        case 5: vm_wait<5 * OPS>(); break;
+        case 6: vm_wait<6 * OPS>(); break;
+        default: vm_wait<7 * OPS>(); break;
+    }
+}
+
 // QB query blocks of 16 per launch (QB = 2: 32 queries, two MFMA chains sharing the row operand).
-template <int KS, int QB>
-__global__ __launch_bounds__(kBlock, QB == 1 ? 4 : 3) void sq8_mfma(Sq8Params p) {
+// RING (unfiltered launches, KS ≤ 4): rows are not loaded into VGPRs but streamed by LDS-DMA from the
+// row-major int8 copy (exact width: no tiled copy, no padding) into a per-wave ring of p.ring_slots
+// 16-row groups, ring_slots − 1 groups ahead of the one being scored, so a wave keeps several groups in
+// flight without holding their registers (the register path holds one group: latency-bound at small
+// dims, ≈2.8 TB/s loads-only at 96 dims).
+// SIM is compile-time: with the similarity a runtime value every (row, query) pair paid the COSINE
+// row-norm square root and a switch (≈ 50 VALU + 30 SALU per pair at 96 dims).
+template <int KS, int QB, bool RING, int SIM>
+__global__ __launch_bounds__(kBlock, QB == 1 ? 4 : (RING ? 2 : 3)) void sq8_mfma(Sq8Params p) {
     typedef int i32x4 __attribute__((ext_vector_type(4)));
     constexpr int NQ = 16 * QB, R = 16, UQ = 4 * KS;   // UQ: 16-B units per query in LDS
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform: scalar loop control
     const int col = lane & 15, grp = lane >> 4;
     const TileDev tile = p.tiles[blockIdx.x];
     const SegDev seg = p.segs[tile.seg];
     const int4* __restrict__ XT = p.rows8t[tile.seg];   // tiled: [row / 16][KS][16 rows][4 chunks]
     const float4* __restrict__ AX = p.aux[tile.seg];
     const uint32_t vbase = (uint32_t)p.seg_vrow[tile.seg];
-    const int u8 = p.units8, sim = p.sim;
+    const int u8 = p.units8;
+    constexpr int sim = SIM;
     extern __shared__ __attribute__((aligned(16))) int4 sq[];   // [NQ][UQ] (zero past u8 / q_count)
-    uint64_t* s_lk = reinterpret_cast<uint64_t*>(sq + NQ * UQ);
+    // RING: the ring overlays the query block (queries are copied into VGPRs first), lists follow both
+    const int ring_rows = RING ? ring_rows_units(u8, KS) : 0;
+    const int ring_slot = ring_rows + 16;
+    const int lists_off = RING ? max(NQ * UQ, 4 * p.ring_slots * ring_slot) : NQ * UQ;
+    uint64_t* s_lk = reinterpret_cast<uint64_t*>(sq + lists_off);
     uint32_t* s_lp = reinterpret_cast<uint32_t*>(s_lk + 4 * NQ * kKQ);
     for (int i = tid; i < NQ * UQ; i += kBlock) {
         const int b = i / UQ, f = i - b * UQ;
@@ -695,6 +746,19 @@ __global__ __launch_bounds__(kBlock, QB == 1 ? 4 : 3) void sq8_mfma(Sq8Params p)
 #pragma unroll
         for (int i = 0; i < 4; ++i) ax[i] = vo[i] ? load_f4_g(AX + ro[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
     };
+    // RING (KS ≤ 4): the queries' B fragments live in VGPRs for the whole scan (≤ 32), not re-read
+    // from LDS per group
+    i32x4 bfr[RING ? KS : 1][QB];
+    if constexpr (RING) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb) {
+                const int4 bv = sq[(qb * 16 + col) * UQ + s * 4 + grp];
+                bfr[s][qb] = i32x4{bv.x, bv.y, bv.z, bv.w};
+            }
+        __syncthreads();   // every wave holds its fragments before any ring write lands on the queries
+    }
     auto process_loaded = [&](const i32x4 (&a)[KS], const float4 (&ax)[4], bool vA, const int64_t (&ro)[4],
                               const bool (&vo)[4]) {
         nvis += __popcll(__ballot(lane < 16 && vA));
@@ -709,9 +773,14 @@ __global__ __launch_bounds__(kBlock, QB == 1 ? 4 : 3) void sq8_mfma(Sq8Params p)
             for (int s = 0; s < KS; ++s)
 #pragma unroll
                 for (int qb = 0; qb < QB; ++qb) {
-                    const int4 bv = sq[(qb * 16 + col) * UQ + s * 4 + grp];
-                    acc[qb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[s], i32x4{bv.x, bv.y, bv.z, bv.w}, acc[qb],
-                                                                    0, 0, 0);
+                    i32x4 b;
+                    if constexpr (RING) {
+                        b = bfr[s][qb];
+                    } else {
+                        const int4 bv = sq[(qb * 16 + col) * UQ + s * 4 + grp];
+                        b = i32x4{bv.x, bv.y, bv.z, bv.w};
+                    }
+                    acc[qb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[s], b, acc[qb], 0, 0, 0);
                 }
         }
         if (p.ablate & 1) {
@@ -726,7 +795,7 @@ __global__ __launch_bounds__(kBlock, QB == 1 ? 4 : 3) void sq8_mfma(Sq8Params p)
             bool anyp = false;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const float sx = sim == SIM_COSINE ? sqrtf(ax[i].w) : 0.0f;
+                const float sx = SIM == SIM_COSINE ? __builtin_amdgcn_sqrtf(ax[i].w) : 0.0f;   // (v_sqrt: 1 ulp ≪ the 2^-16 quick-test slack)
                 sq8_bounds(sim, (float)acc[qb][i], ax[i], qc[qb], p.gam, p.g2, lo[qb][i], hi[qb][i]);
                 pass[qb][i] = vo[i] && qv[qb] && sq8_pass(sim, lo[qb][i], hi[qb][i], tq[qb], sx);
                 anyp |= pass[qb][i];
@@ -821,6 +890,78 @@ __global__ __launch_bounds__(kBlock, QB == 1 ? 4 : 3) void sq8_mfma(Sq8Params p)
                 process(rowA, vA, ro, vo);
             }
         }
+    } else if constexpr (RING) {
+        // group slot: KS·64 units of rows (the group's 16·u8 units, lane-linear; lanes past them load unit
+        // 0 again, never read) then 16 units of bound terms.  Per group KS + 1 LDS-DMA instructions.
+        constexpr int OPS = KS + 1;
+        const int NS = p.ring_slots, SLOT = ring_slot;
+        int4* ring = sq + wave * NS * SLOT;
+        const uint32_t ring_lds =
+            __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(__attribute__((address_space(3))) int4*)ring);
+        const int4* __restrict__ X8 = p.rows8[tile.seg];
+        const int n_groups = pilot ? min<int64_t>(1, (we - wb + 15) / 16) : (int)((we - wb + 15) / 16);
+        auto issue = [&](int g, int slot_idx) {
+            // the slot's previous group was read by this wave's ds_reads: retire them before the DMA
+            // can overwrite it (the compiler may sink their consumers past this point)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const int64_t r0 = wb + (int64_t)g * 16;
+            const int nu = (int)min<int64_t>(16, we - r0) * u8;
+            const int4* src = X8 + r0 * u8;
+            const uint32_t dst = ring_lds + (uint32_t)(slot_idx * SLOT * 16);
+#pragma unroll
+            for (int i = 0; i < KS; ++i) {
+                const int u = i * 64 + lane;
+                if (u < ring_rows) glds16(src + (u < nu ? u : 0), dst + i * 1024);
+            }
+            const int nr = (int)min<int64_t>(16, we - r0);
+            if (lane < 16) glds16(AX + r0 + (lane < nr ? lane : 0), dst + ring_rows * 16);
+        };
+        const int D = NS - 1;
+        // slots are used round robin: group g in slot g mod NS (kept as running counters, no division)
+        int s_issue = 0, s_read = 0;
+        for (int g = 0; g < D && g < n_groups; ++g) {
+            issue(g, s_issue);
+            s_issue = s_issue + 1 == NS ? 0 : s_issue + 1;
+        }
+        for (int g = 0; g < n_groups; ++g) {
+            if (g + D < n_groups) {
+                issue(g + D, s_issue);
+                s_issue = s_issue + 1 == NS ? 0 : s_issue + 1;
+            }
+            // this wave's LDS-DMAs issued after group g's: (min(g + D, n − 1) − g) groups
+            vm_wait_groups<OPS>(min(g + D, n_groups - 1) - g);
+            const int64_t r0 = wb + (int64_t)g * 16;
+            const int nr = (int)min<int64_t>(16, we - r0);   // rows of this group (32-bit tests below)
+            const bool vA = col < nr;
+            int64_t ro[4];
+            bool vo[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                ro[i] = r0 + 4 * grp + i;
+                vo[i] = 4 * grp + i < nr;
+            }
+            const int4* slot = ring + s_read * SLOT;
+            s_read = s_read + 1 == NS ? 0 : s_read + 1;
+            // No masking: a chunk past the row's u8 units meets zero query bytes (the query block is
+            // zero-padded), so whatever it holds adds 0 to the exact int32 dot; rows past the group's end
+            // (and their bound terms) only produce lanes that vA / vo exclude.
+            i32x4 a[KS];
+#pragma unroll
+            for (int s8 = 0; s8 < KS; ++s8) {
+                const int f = s8 * 4 + grp;
+                const int4 v = slot[col * u8 + (f < u8 ? f : 0)];
+                a[s8] = i32x4{v.x, v.y, v.z, v.w};
+            }
+            float4 ax[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {   // unconditional reads (a read under vo[i] waited for each alone)
+                const int4 t4 = slot[ring_rows + 4 * grp + i];
+                ax[i] = make_float4(__int_as_float(t4.x), __int_as_float(t4.y), __int_as_float(t4.z),
+                                    __int_as_float(t4.w));
+            }
+            process_loaded(a, ax, vA, ro, vo);
+        }
+        vm_wait<0>();
     } else {
         for (int64_t r0 = wb; r0 < we && !sampled; r0 += R) {
             const int64_t rowA = r0 + col;
@@ -892,11 +1033,46 @@ __global__ __launch_bounds__(kBlock, QB == 1 ? 4 : 3) void sq8_mfma(Sq8Params p)
 
 using Sq8MfmaFn = void (*)(Sq8Params);
 static const int kMfmaKS[6] = {2, 4, 6, 8, 12, 16};
-#define OSK_MFMA_ROW(KS) {sq8_mfma<KS, 1>, sq8_mfma<KS, 2>}
-static const Sq8MfmaFn kSq8Mfma[6][2] = {OSK_MFMA_ROW(2), OSK_MFMA_ROW(4), OSK_MFMA_ROW(6),
-                                         OSK_MFMA_ROW(8), OSK_MFMA_ROW(12), OSK_MFMA_ROW(16)};
+#define OSK_MFMA_SIMS(KS, QB, RG) {sq8_mfma<KS, QB, RG, 0>, sq8_mfma<KS, QB, RG, 1>, sq8_mfma<KS, QB, RG, 2>, \
+                                   sq8_mfma<KS, QB, RG, 3>}
+#define OSK_MFMA_ROW(KS) {OSK_MFMA_SIMS(KS, 1, false), OSK_MFMA_SIMS(KS, 2, false)}
+static const Sq8MfmaFn kSq8Mfma[6][2][4] = {OSK_MFMA_ROW(2), OSK_MFMA_ROW(4), OSK_MFMA_ROW(6),
+                                            OSK_MFMA_ROW(8), OSK_MFMA_ROW(12), OSK_MFMA_ROW(16)};
+static const Sq8MfmaFn kSq8MfmaRing[2][2][4] = {{OSK_MFMA_SIMS(2, 1, true), OSK_MFMA_SIMS(2, 2, true)},
+                                                {OSK_MFMA_SIMS(4, 1, true), OSK_MFMA_SIMS(4, 2, true)}};
 
 int sq8_mfma_supported(int u8) { return u8 <= 4 * kMfmaKS[5]; }
+// dynamic LDS of an sq8_mfma launch: queries [NQ][4·KS] units (overlaid by the ring when ns > 1) and
+// the 4 waves' lists [4][NQ][kKQ] keys + lower bounds
+static size_t sq8_mfma_lds(int u8, int qb, int ns) {
+    int c = 0;
+    while (c < 5 && 4 * kMfmaKS[c] < u8) ++c;
+    const int ks = kMfmaKS[c];
+    const size_t queries = (size_t)16 * qb * 4 * ks * 16, lists = (size_t)4 * 16 * qb * kKQ * 12;
+    if (ns <= 1) return queries + lists;
+    const size_t ring = (size_t)4 * ns * (ring_rows_units(u8, ks) + 16) * 16;
+    return std::max(queries, ring) + lists;
+}
+// LDS-DMA ring depth for sq8_mfma: `want` (> 1), 0 (off), or -1: as many 16-row groups per wave as leave
+// two 4-wave workgroups per CU within 160 KiB of LDS (KS = 2, 32 queries: 5; KS = 4: 2)
+int sq8_ring_slots(int u8, int qb, int want) {
+    int c = 0;
+    while (c < 5 && 4 * kMfmaKS[c] < u8) ++c;
+    if (c > 1 || want == 0) return 0;
+    const int ks = kMfmaKS[c];
+    auto lds = [&](int ns) { return sq8_mfma_lds(u8, qb, ns); };
+    if (want > 1) {   // at most one workgroup's worth of LDS
+        int ns = std::min(want, 8);
+        while (ns > 2 && lds(ns) > 160 * 1024) --ns;
+        return ns;
+    }
+    // default: the most workgroups per CU (LDS), then the deepest ring at that count
+    int best = 2;
+    for (int ns = 3; ns <= 8; ++ns)
+        if ((160 * 1024) / lds(ns) >= (160 * 1024) / lds(best)) best = ns;
+    (void)ks;
+    return best;
+}
 int sq8_mfma_ks(int u8) {
     int c = 0;
     while (c < 5 && 4 * kMfmaKS[c] < u8) ++c;
@@ -931,8 +1107,15 @@ hipError_t launch_sq8_mfma(const Sq8Params& p, hipStream_t s, hipEvent_t ev_star
     while (c < 5 && 4 * kMfmaKS[c] < p.units8) ++c;
     if (4 * kMfmaKS[c] < p.units8) return hipErrorInvalidValue;
     const int qb = p.q_count > 16 ? 2 : 1;
-    const size_t lds = (size_t)16 * qb * 4 * kMfmaKS[c] * 16 + (size_t)4 * 16 * qb * kKQ * 12;
-    const auto fn = kSq8Mfma[c][qb - 1];
+    size_t lds = sq8_mfma_lds(p.units8, qb, 0);
+    if (p.sim < 0 || p.sim > 3) return hipErrorInvalidValue;
+    auto fn = kSq8Mfma[c][qb - 1][p.sim];
+    if (p.ring_slots >= 2 && !p.accept && c <= 1) {   // LDS-DMA ring (unfiltered, ≤ 256 dims)
+        if (p.ring_slots > 8) return hipErrorInvalidValue;
+        fn = kSq8MfmaRing[c][qb - 1][p.sim];
+        lds = sq8_mfma_lds(p.units8, qb, p.ring_slots);
+        if (lds > 160 * 1024) return hipErrorInvalidValue;
+    }
     if (ev_start || ev_stop)
         hipExtLaunchKernelGGL(fn, dim3(p.n_tiles), dim3(kBlock), lds, s, ev_start, ev_stop, 0, p);
     else
@@ -968,7 +1151,7 @@ __global__ __launch_bounds__(kSettleThreads) void sq8_settle(SettleParams p) {
     __shared__ uint32_t s_L;
     __shared__ uint32_t s_exact;   // bit i: list l0 + i of the slice is re-scanned exactly
     const int g = blockIdx.x, q = blockIdx.y;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform: scalar loop control
     const int t = lane & (L - 1), gr = lane / L;
     const int k = p.k, sim = p.sim;
     if (p.trace && tid == 0) p.trace[((size_t)q * p.n_slices + g) * 8 + 0] = wall_clock64();
@@ -1151,7 +1334,7 @@ __global__ __launch_bounds__(kSettleThreads) void sq8_settle_merge(SettleParams 
     __shared__ int s_ns;
     __shared__ uint64_t s_t;
     const int sh = blockIdx.x, q = blockIdx.y, S = p.n_shards, k = p.k;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform: scalar loop control
     const int g0 = p.shard_slice_begin[sh], g1 = p.shard_slice_begin[sh + 1];
     const uint64_t* __restrict__ src = p.part + ((size_t)q * p.n_slices + g0) * k;
     const int nl = g1 - g0, n = nl * k;

@@ -6,9 +6,10 @@ the same tie order — which the oracle's ORDER_DEVICE restatement pins.  These 
 two paths (tune "sq8" 1 vs 0) and the oracle over similarities, ragged dims, batch sizes, k,
 filters, sparse doc maps, multi-segment multi-shard views, heavy ties and adversarial data where
 the certificate cannot exclude a whole tile and the settle re-scans that tile exactly instead.
-Every test runs three times: batches scanned by the int8 MFMA kernel (sq8_mfma, tune "sq8_mfma_min"
-2, the default) with 32 and with 16 queries per launch, and by the VALU kernel (sq8_scan,
-"sq8_mfma_min" 0).
+Every test runs four times: batches scanned by the int8 MFMA kernel (sq8_mfma, tune "sq8_mfma_min"
+2, the default) with 32 and with 16 queries per launch (rows ≤ 256 dims streamed by the LDS-DMA ring,
+the default), with 32 queries and register row loads ("sq8_mfma_ring" 0), and by the VALU kernel
+(sq8_scan, "sq8_mfma_min" 0).
 """
 import numpy as np
 import pytest
@@ -22,15 +23,17 @@ SIMS = [LU.VectorSimilarityFunction(s) for s in range(4)]
 COS = LU.VectorSimilarityFunction.COSINE
 
 
-@pytest.fixture(autouse=True, params=["mfma32", "mfma16", "valu"])
+@pytest.fixture(autouse=True, params=["mfma32", "mfma16", "mfma32reg", "valu"])
 def scan_kernel(request):
     """The int8 scan kernel of batched prefilter searches (single queries always take sq8_scan):
-    sq8_mfma with 32 or 16 queries per launch, or the VALU sq8_scan."""
+    sq8_mfma with 32 or 16 queries per launch (LDS-DMA ring), with register row loads, or sq8_scan."""
     _lib.tune("sq8_mfma_min", 0 if request.param == "valu" else 2)
     _lib.tune("sq8_mfma_queries", 16 if request.param == "mfma16" else 32)
+    _lib.tune("sq8_mfma_ring", 0 if request.param == "mfma32reg" else -1)
     yield request.param
     _lib.tune("sq8_mfma_min", 2)
     _lib.tune("sq8_mfma_queries", 32)
+    _lib.tune("sq8_mfma_ring", -1)
 
 
 def corpus(n, dim, sim, seed):
@@ -235,3 +238,37 @@ def test_prefilter_multi_shard_from_size():
             assert_same(ds.search(queries, k, f, sz), with_tune("sq8", 0, lambda: ds.search(queries, k, f, sz)))
     finally:
         close_all(ds, readers)
+
+
+@pytest.mark.parametrize("slots", [2, 3, 5, 8])
+@pytest.mark.parametrize("dim,sim", [(17, COS), (96, LU.VectorSimilarityFunction.DOT_PRODUCT),
+                                     (128, LU.VectorSimilarityFunction.EUCLIDEAN),
+                                     (256, LU.VectorSimilarityFunction.MAXIMUM_INNER_PRODUCT)])
+def test_mfma_ring_depths(slots, dim, sim, scan_kernel):
+    """The LDS-DMA ring at every depth: ragged segment sizes (partial 16-row groups at wave ends),
+    several segments and shards, a sparse field without a filter; equal to the fp32 scan and the oracle."""
+    if scan_kernel != "mfma32":
+        pytest.skip("ring depth sweep runs once")
+    sizes = [5000, 1237, 16, 3, 777]
+    segs = [corpus(n, dim, sim, 700 + i) for i, n in enumerate(sizes)]
+    queries = corpus(33, dim, sim, 710)
+    ds, readers = view_of(segs, sim, shard_of=[0, 0, 1, 2, 2])
+    rng = np.random.default_rng(5)
+    docs = np.sort(rng.choice(9000, 4000, replace=False)).astype(np.int32)
+    sp_rows = corpus(4000, dim, sim, 720)
+    sparse = LU.GpuFlatVectorsReader("v", sp_rows, sim, ord_to_doc=docs, max_doc=9000)
+    _lib.tune("sq8_mfma_ring", slots)
+    try:
+        got = ds.search(queries, 10, 0, 10)
+        want = with_tune("sq8", 0, lambda: ds.search(queries, 10, 0, 10))
+        assert_same(got, want)
+        s, d, c, _ = sparse.search_batch(queries, 10)
+        for i in range(0, len(queries), 8):
+            os_, od, _ = O.exact_search(sp_rows, queries[i], 10, int(sim), ord_to_doc=docs)
+            assert np.array_equal(d[i, : c[i]], od) and np.array_equal(bits(s[i, : c[i]]), bits(os_))
+    finally:
+        _lib.tune("sq8_mfma_ring", -1)
+        ds.close()
+        for r in readers:
+            r.close()
+        sparse.close()
