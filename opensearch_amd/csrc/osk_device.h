@@ -40,6 +40,22 @@ __device__ __forceinline__ void sq8_bounds(int sim, float I, float4 ax, float4 q
     }
 }
 
+// The one side of sq8_bounds the quick test reads (EUCLIDEAN: the d² lower bound; else the dot upper
+// bound), bit-identical to sq8_bounds' value of it: hot loops need not compute the other side.
+__device__ __forceinline__ float sq8_bound_side(int sim, float I, float4 ax, float4 qc, float gam, float g2) {
+    const float approx = I * (ax.x * qc.x);
+    const float eq = fmaf(ax.y, qc.y, ax.z * qc.z);
+    if (sim == SIM_EUCLIDEAN) {
+        const float base = ax.w + qc.w;
+        const float sl = 0x1p-20f * (base + 2.0f * (fabsf(approx) + eq));
+        const float d2lo = base - 2.0f * (approx + eq) - sl;
+        return fmaxf(d2lo, 0.0f) * (1.0f - g2);
+    }
+    const float e = eq + gam * (ax.w + qc.w);
+    const float sl = 0x1p-20f * (fabsf(approx) + e);
+    return approx + e + sl;
+}
+
 // Global-address-space loads (global_load, not flat_load): a flat load also counts in lgkmcnt, so
 // the first LDS read after it would wait for every row load in flight, prefetched ones included.
 __device__ __forceinline__ int4 load_i4_g(const int4* p, bool nt) {

@@ -788,16 +788,19 @@ __global__ __launch_bounds__(kBlock, QB == 1 ? 4 : (RING ? 2 : 3)) void sq8_mfma
             return;
         }
         bool pass[QB][4];
-        float lo[QB][4], hi[QB][4];
         uint32_t qm = 0u;   // queries with a passing lane (wave-uniform after the ballots)
+        // both bounds of a pair, for the rare list insertions and the pilot (the quick test reads one)
+        auto bounds = [&](int qb, int i, float& lo, float& hi) {
+            sq8_bounds(sim, (float)acc[qb][i], ax[i], qc[qb], p.gam, p.g2, lo, hi);
+        };
 #pragma unroll
         for (int qb = 0; qb < QB; ++qb) {
             bool anyp = false;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const float sx = SIM == SIM_COSINE ? __builtin_amdgcn_sqrtf(ax[i].w) : 0.0f;   // (v_sqrt: 1 ulp ≪ the 2^-16 quick-test slack)
-                sq8_bounds(sim, (float)acc[qb][i], ax[i], qc[qb], p.gam, p.g2, lo[qb][i], hi[qb][i]);
-                pass[qb][i] = vo[i] && qv[qb] && sq8_pass(sim, lo[qb][i], hi[qb][i], tq[qb], sx);
+                const float side = sq8_bound_side(sim, (float)acc[qb][i], ax[i], qc[qb], p.gam, p.g2);
+                pass[qb][i] = vo[i] && qv[qb] && sq8_pass(sim, side, side, tq[qb], sx);
                 anyp |= pass[qb][i];
             }
             if (!pilot) {
@@ -813,8 +816,9 @@ __global__ __launch_bounds__(kBlock, QB == 1 ? 4 : (RING ? 2 : 3)) void sq8_mfma
                 for (int i = 0; i < 4; ++i) {
                     float xnd = 0.0f;
                     if (sim == SIM_COSINE && vo[i]) xnd = seg.xnorm_f[ro[i]];
-                    const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi[qb][i])
-                                                          : score_f32(sim, lo[qb][i], qnd[qb], xnd);
+                    float lo, hi;
+                    bounds(qb, i, lo, hi);
+                    const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qnd[qb], xnd);
                     s_lk[(qb * 16 + col) * 64 + wave * 16 + 4 * grp + i] =
                         vo[i] ? make_key(lb, vbase + (uint32_t)ro[i]) : 0ull;
                 }
@@ -838,10 +842,10 @@ __global__ __launch_bounds__(kBlock, QB == 1 ? 4 : (RING ? 2 : 3)) void sq8_mfma
                     const bool o = pass[qb][i] && col == bc;
                     float xnd = 0.0f;
                     if (sim == SIM_COSINE && o) xnd = seg.xnorm_f[ro[i]];
-                    const float ub = sim == SIM_EUCLIDEAN ? score_f32_l2(lo[qb][i])
-                                                          : score_f32(sim, hi[qb][i], qnd[qb], xnd);
-                    const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi[qb][i])
-                                                          : score_f32(sim, lo[qb][i], qnd[qb], xnd);
+                    float lo, hi;
+                    bounds(qb, i, lo, hi);
+                    const float ub = sim == SIM_EUCLIDEAN ? score_f32_l2(lo) : score_f32(sim, hi, qnd[qb], xnd);
+                    const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qnd[qb], xnd);
                     const uint64_t key = o ? make_key(ub, vbase + (uint32_t)ro[i]) : 0ull;
                     wave_offer2(key, float_to_sortable(lb), o, lkb, lpb, thrb, lane, kKQ);
                 }
