@@ -229,6 +229,9 @@ int32_t osk_view_scan_time(osk_view* view, double* total_ms, int64_t* calls);
  *                     default 2; 0 = always the VALU sq8_scan)
  *   "sq8_mfma_queries"  16 | 32 queries per sq8_mfma launch (default 32)
  *   "sq8_mfma_nt"     0|1 non-temporal row loads in sq8_mfma (default 1)
+ *   "sq8_mfma_ring"   LDS-DMA ring slots per wave in sq8_mfma for rows of ≤ 256 dims (default -1 = as many
+ *                     as keep 4 workgroups per CU, 0 = register row loads)
+ *   "i8_stream"       0|1 single unfiltered byte-vector queries on scan_i8_stream (default 1) or scan_i8
  *   "filter_gather"   0|1 filtered prefilter scans over the device-compacted accepted ordinals
  *                     (osk_filter.hip; default 1) instead of a walk over 64-row bitset windows
  *   "gather_min"      accepted rows per gather tile at least (default 0 = every tile of the segment)

@@ -251,6 +251,7 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         {"sq8_mfma_queries", &g_tuning.sq8_mfma_queries, 16, 32, false},
         {"sq8_mfma_min", &g_tuning.sq8_mfma_min, 0, 1 << 20, false},
         {"sq8_mfma_ring", &g_tuning.sq8_mfma_ring, -1, 8, false},
+        {"i8_stream", &g_tuning.i8_stream, 0, 1, false},
         {"sq8_mfma_ablate", &g_tuning.sq8_mfma_ablate, 0, 3, true},
         {"sq8_force_fallback", &g_tuning.sq8_force_fallback, 0, 1, true},
         {"settle_trace", &g_tuning.settle_trace, 0, 1, true},

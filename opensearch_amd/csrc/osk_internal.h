@@ -328,6 +328,7 @@ struct Tuning {
     std::atomic<int> filter_gather{1};    // filtered prefilter scans (VALU sq8_scan) compact the accepted ordinals
                                           // first and scan them (osk_filter.hip); 0 = walk the bitset windows
     std::atomic<int> sq8_mfma_nt{1};      // A/B: non-temporal row loads in sq8_mfma
+    std::atomic<int> i8_stream{1};        // byte fields, one query, no filter: scan_i8_stream (0 = scan_i8)
     std::atomic<int> sq8_mfma_ring{-1};   // sq8_mfma LDS-DMA ring slots per wave (≤ 256 dims, unfiltered):
                                           // -1 = as many as fit 2 workgroups per CU, 0 = off (register loads)
     std::atomic<int> sq8_mfma_queries{32};    // queries per sq8_mfma launch: 16 or 32 (two MFMA chains per row operand)

@@ -19,6 +19,7 @@
 //     score beats the threshold (rare after the first few hundred rows).
 #include <hip/hip_ext.h>
 
+#include "osk_device.h"
 #include "osk_internal.h"
 #include "osk_wave.h"
 
@@ -272,6 +273,90 @@ __global__ __launch_bounds__(kBlock) void scan_i8(ScanParams p) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// byte vectors, one query, no filter (the C5 int8 case): scan_i8's arithmetic on sq8_scan's loop —
+// exact-width lane configs (L lanes × V 16-B units ≥ the row's units, not the fp32 table's), U row
+// groups loaded (non-temporal, clamped rows, masked values) before any is scored, so a wave keeps
+// ≈ U·V KiB in flight.  Scores are exact int32 sums, so results equal scan_i8's bit for bit.
+// ------------------------------------------------------------------------------------------------
+template <int L, int V, int U>
+__global__ __launch_bounds__(kBlock) void scan_i8_stream(ScanParams p) {
+    constexpr int R = 64 / L;
+    __shared__ uint64_t slist[4 * 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int t = lane & (L - 1), g = lane / L;
+    const TileDev tile = p.tiles[blockIdx.x];
+    const SegDev seg = p.segs[tile.seg];
+    const int4* __restrict__ X = static_cast<const int4*>(seg.rows);
+    const int4* __restrict__ Q = static_cast<const int4*>(p.q);
+    const int units = p.units;
+    int4 qf[V];
+    int qn = 0;   // Σq² (exact)
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+        const int f = t + j * L;
+        const int m = f < units ? -1 : 0;
+        const int4 v = Q[f < units ? f : 0];
+        qf[j] = make_int4(v.x & m, v.y & m, v.z & m, v.w & m);
+        qn = dot4_i8(qf[j].x, qf[j].x, qn); qn = dot4_i8(qf[j].y, qf[j].y, qn);
+        qn = dot4_i8(qf[j].z, qf[j].z, qn); qn = dot4_i8(qf[j].w, qf[j].w, qn);
+    }
+#pragma unroll
+    for (int m = 1; m < L; m <<= 1) qn += __shfl_xor(qn, m);
+    const int64_t rows = tile.row_end - tile.row_begin;
+    const int64_t per_wave = ((rows + 4 * R - 1) / (4 * R)) * R;
+    const int64_t wb = tile.row_begin + wave * per_wave;
+    const int64_t we = min(wb + per_wave, tile.row_end);
+    const int sim = p.sim, k = p.k, dim = p.dim;
+    uint64_t lk = 0ull, thr = 0ull;
+    uint32_t nvis = 0;
+    for (int64_t r0 = wb; r0 < we; r0 += R * U) {
+        int64_t row[U];
+        bool valid[U];
+        int4 xv[U][V];
+        int32_t xn[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            row[u] = r0 + u * R + g;
+            valid[u] = row[u] < we;
+            const int64_t rc = valid[u] ? row[u] : wb;   // clamped row: every load is unconditional
+            const int4* xr = X + rc * units;
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                const int f = t + j * L;
+                const int4 x = load_i4_nt(xr + (f < units ? f : 0));
+                const int m = f < units ? -1 : 0;
+                xv[u][j] = make_int4(x.x & m, x.y & m, x.z & m, x.w & m);
+            }
+            xn[u] = seg.xnorm_i[rc];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int acc = 0;
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                acc = dot4_i8(xv[u][j].x, qf[j].x, acc); acc = dot4_i8(xv[u][j].y, qf[j].y, acc);
+                acc = dot4_i8(xv[u][j].z, qf[j].z, acc); acc = dot4_i8(xv[u][j].w, qf[j].w, acc);
+            }
+#pragma unroll
+            for (int m = 1; m < L; m <<= 1) acc += __shfl_xor(acc, m);
+            nvis += __popcll(__ballot(t == 0 && valid[u]));
+            const int32_t s = sim == SIM_EUCLIDEAN ? qn + xn[u] - 2 * acc : acc;
+            const float sc = score_i8(sim, s, qn, xn[u], dim);
+            const int32_t doc = seg.ord_to_doc ? seg.ord_to_doc[valid[u] ? row[u] : wb] : (int32_t)row[u];
+            const uint64_t key = valid[u] ? make_key(sc, (uint32_t)(seg.doc_base + doc)) : 0ull;
+            wave_offer(key, t == 0, lk, thr, lane, k);
+        }
+    }
+    if (p.visited && p.q0 == 0 && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
+    slist[wave * 64 + lane] = lane < k ? lk : 0ull;
+    __syncthreads();
+    if (wave == 0) {
+        block_fold(slist, lk, thr, lane, k);
+        if (lane < k) p.cand[((size_t)p.q0 * p.n_tiles + blockIdx.x) * k + lane] = lk;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // dispatch tables: lane configs × NQ ∈ {1,2,4,8} × {L2, dot-family}
 // ------------------------------------------------------------------------------------------------
 int cfg_index(int units) {
@@ -306,6 +391,15 @@ static const ScanFn kScanI8[9][4] = {
 static const int kCfgLV[9][2] = {{4, 2}, {8, 2}, {8, 4}, {16, 4}, {16, 8}, {16, 12},
                                  {32, 8}, {64, 8}, {64, 16}};
 
+// scan_i8_stream's exact-width configs by 16-byte units (sq8_scan's): ≤4 (4,1) ≤8 (8,1) ≤16 (16,1)
+// ≤32 (16,2) ≤48 (16,3) ≤64 (16,4) ≤128 (32,4) ≤256 (64,4)
+static const ScanFn kScanI8Stream[8] = {scan_i8_stream<4, 1, 4>,  scan_i8_stream<8, 1, 4>,  scan_i8_stream<16, 1, 4>,
+                                        scan_i8_stream<16, 2, 4>, scan_i8_stream<16, 3, 4>, scan_i8_stream<16, 4, 4>,
+                                        scan_i8_stream<32, 4, 4>, scan_i8_stream<64, 4, 4>};
+static int i8_stream_cfg(int u) {
+    return u <= 4 ? 0 : u <= 8 ? 1 : u <= 16 ? 2 : u <= 32 ? 3 : u <= 48 ? 4 : u <= 64 ? 5 : u <= 128 ? 6 : 7;
+}
+
 static int nq_slot(int nq) { return nq <= 1 ? 0 : nq <= 2 ? 1 : nq <= 4 ? 2 : 3; }
 static int nq_of_slot(int s) { return 1 << s; }
 
@@ -322,6 +416,8 @@ hipError_t launch_scan(int enc, int cfg, int nq, const ScanParams& p, hipStream_
     if (enc == ENC_FLOAT32) {
         const bool l2 = p.sim == SIM_EUCLIDEAN;
         fn = kScanF32[cfg][(g_tuning.scan_nt ? 8 : 0) + (l2 ? 0 : 4) + slot];
+    } else if (NQ == 1 && !p.accept && p.units <= 256 && g_tuning.i8_stream) {
+        fn = kScanI8Stream[i8_stream_cfg(p.units)];
     } else {
         fn = kScanI8[cfg][slot];
     }

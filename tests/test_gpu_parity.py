@@ -73,6 +73,30 @@ def test_i8_exact(dim, sim):
         r.close()
 
 
+@pytest.mark.parametrize("stream", [1, 0], ids=["i8_stream", "scan_i8"])
+@pytest.mark.parametrize("dim", [1, 15, 64, 96, 100, 257, 512, 768, 1000, 2048, 4096])
+@pytest.mark.parametrize("sim", SIMS, ids=lambda s: s.name)
+def test_i8_single_query_stream(dim, sim, stream):
+    """One byte query per search, no filter: scan_i8_stream (exact-width lanes, 4 row groups in flight)
+    and scan_i8 both equal the oracle; ragged row counts leave partial row groups at wave ends."""
+    rows = corpus(3000 + dim % 13, dim, sim, 23, I8)
+    queries = corpus(3, dim, sim, 24, I8)
+    r = LU.GpuFlatVectorsReader("v", rows, sim, I8)
+    _lib.tune("i8_stream", stream)
+    try:
+        for i in range(len(queries)):
+            assert_exact(r, rows, queries[i: i + 1], 10 if i else 64, sim)
+        rd = np.sort(np.random.default_rng(dim).choice(9000, len(rows), replace=False)).astype(np.int32)
+        sp = LU.GpuFlatVectorsReader("v", rows, sim, I8, ord_to_doc=rd, max_doc=9000)
+        try:
+            assert_exact(sp, rows, queries[:1], 10, sim, ord_to_doc=rd)
+        finally:
+            sp.close()
+    finally:
+        _lib.tune("i8_stream", 1)
+        r.close()
+
+
 @pytest.mark.parametrize("nq", [1, 2, 3, 4, 7, 8, 9, 13, 32])
 @pytest.mark.parametrize("dim", [128, 768])
 def test_batch_sizes_same_bits(nq, dim):
