@@ -310,7 +310,7 @@ __device__ __forceinline__ void gather_wave_range(int64_t cnt, int j, int nj, in
 }
 
 template <int L, int V, int NQ, int U, int MODE = kScanRows>
-__global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
+__global__ __launch_bounds__(kBlock, NQ == 1 && V <= 3 ? 4 : 1) void sq8_scan(Sq8Params p) {   // ≤ 128 VGPRs: 4 waves/SIMD
     constexpr int R = 64 / L;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform: scalar loop control
     const int t = lane & (L - 1), g = lane / L;
@@ -397,6 +397,10 @@ __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
             }
         }
         const bool known = filt;
+        // every load is unconditional, on a clamped in-range row, and masked after: a load under a
+        // per-lane condition made the compiler wait for each row group before issuing the next
+        // (lane 0's entry of a compacted window is always a real row; else the wave's first row)
+        const int64_t safe = filt ? base + __shfl(pos, 0) : wb;
         int4 xv[U][V];
         float4 ax[U];
 #pragma unroll
@@ -405,13 +409,17 @@ __global__ __launch_bounds__(kBlock) void sq8_scan(Sq8Params p) {
                 const int32_t doc = seg.ord_to_doc ? seg.ord_to_doc[row[u]] : (int32_t)row[u];
                 valid[u] = (abits[doc >> 6] >> (doc & 63)) & 1ull;
             }
-            const int4* xr = X + row[u] * u8;
+            const int64_t rc = valid[u] ? row[u] : safe;
+            const int4* xr = X + rc * u8;
 #pragma unroll
             for (int j = 0; j < V; ++j) {
                 const int f = t + j * L;
-                xv[u][j] = (valid[u] && f < u8) ? load_i4_nt(xr + f) : make_int4(0, 0, 0, 0);
+                const int4 x = load_i4_nt(xr + (f < u8 ? f : 0));
+                const int m = (valid[u] && f < u8) ? -1 : 0;
+                xv[u][j] = make_int4(x.x & m, x.y & m, x.z & m, x.w & m);
             }
-            ax[u] = valid[u] ? AX[row[u]] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 a = AX[rc];
+            ax[u] = valid[u] ? a : make_float4(0.f, 0.f, 0.f, 0.f);
         }
         if constexpr (NQ == 1) {
 #pragma unroll
