@@ -23,6 +23,7 @@ OSK_ERR_OOM = -3
 OSK_ERR_UNSUPPORTED = -4
 OSK_ERR_NO_DEVICE = -5
 OSK_MAX_K = 10000
+OSK_ABI_VERSION = 2        # include/osknn.h OSK_ABI_VERSION
 OSK_MAX_DIM = 4096
 OSK_COMM_ID_BYTES = 128
 

@@ -36,13 +36,13 @@ def test_library_exports_every_header_symbol():
 
 
 def test_abi_version_and_constants():
-    assert _lib.lib().osk_abi_version() == 2
+    assert _lib.lib().osk_abi_version() == _lib.OSK_ABI_VERSION == 2
     text = HEADER.read_text()
-    for name in ["OSK_COMM_ID_BYTES", "OSK_WARM_PREFILTER", "OSK_WARM_PREFILTER_MFMA", "OSK_WARM_BATCHED",
+    for name in ["OSK_ABI_VERSION", "OSK_COMM_ID_BYTES", "OSK_WARM_PREFILTER", "OSK_WARM_PREFILTER_MFMA", "OSK_WARM_BATCHED",
                  "OSK_WARM_ALL", "OSK_MAX_K", "OSK_EUCLIDEAN", "OSK_DOT_PRODUCT", "OSK_COSINE", "OSK_MAXIMUM_INNER_PRODUCT",
                  "OSK_FLOAT32", "OSK_BYTE", "OSK_ERR_NO_DEVICE"]:
         val = int(re.search(rf"#define {name}\s+(-?\d+)", text).group(1))
-        py = name if name.startswith(("OSK_ERR", "OSK_MAX_", "OSK_COMM", "OSK_WARM")) else name[4:]
+        py = name if name.startswith(("OSK_ERR", "OSK_MAX_", "OSK_COMM", "OSK_WARM", "OSK_ABI")) else name[4:]
         assert getattr(_lib, py) == val
 
 
