@@ -62,7 +62,8 @@ def pmc_traffic(rows_local: int, batch: int, prefilter: bool):
     if batch != 1 or not os.path.exists(PMC_SUMMARY):
         return None, None
     data = json.load(open(PMC_SUMMARY))
-    want = "sq8_scan<16, 3, 1, 4>" if prefilter else "scan_f32<16, 12, 1, false"
+    # (a prefix: the headline instance is sq8_scan<16, 3, 1, 4, MODE>)
+    want = "sq8_scan<16, 3, 1, 4" if prefilter else "scan_f32<16, 12, 1, false"
     for name, v in data.items():
         if want in name:
             return v["hbm_bytes"] * rows_local / (N_SHARDS * ROWS_PER_SHARD), os.path.relpath(PMC_SUMMARY, ROOT)
