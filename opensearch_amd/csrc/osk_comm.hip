@@ -40,7 +40,22 @@ struct osk_comm {
     int rank = 0, world = 1;             // rank of local device 0, communicator size
     std::vector<int> devices;            // local devices: 1 (one process per GPU) or all (one process)
     std::vector<ncclComm_t> comms;       // one per local device
+    // one exchange stream per local device: every collective of the communicator is issued on it, in
+    // call order, whatever stream (search thread) the call arrived on — RCCL needs one issue order per
+    // communicator, and a search's scan on its own stream overlaps the previous search's exchange
+    std::vector<hipStream_t> xstreams;
+    // per local device: "inputs ready" (caller stream → exchange stream) and "outputs ready" (back);
+    // reused by every call: calls are serialised by `mu`, and a stream wait binds the record before it
+    std::vector<hipEvent_t> ev_in, ev_out;
     std::mutex mu;                       // one collective sequence at a time
+    ~osk_comm() {
+        for (size_t i = 0; i < devices.size(); ++i) {
+            (void)hipSetDevice(devices[i]);
+            if (i < xstreams.size() && xstreams[i]) (void)hipStreamDestroy(xstreams[i]);
+            if (i < ev_in.size() && ev_in[i]) (void)hipEventDestroy(ev_in[i]);
+            if (i < ev_out.size() && ev_out[i]) (void)hipEventDestroy(ev_out[i]);
+        }
+    }
 };
 
 namespace {
@@ -110,6 +125,32 @@ const Rccl* rccl() {
         }                                                                                      \
     } while (0)
 
+int32_t make_xstreams(osk_comm* c) {
+    const size_t n = c->devices.size();
+    c->xstreams.assign(n, nullptr);
+    c->ev_in.assign(n, nullptr);
+    c->ev_out.assign(n, nullptr);
+    for (size_t i = 0; i < n; ++i) {
+        OSK_HIP(hipSetDevice(c->devices[i]));
+        OSK_HIP(hipStreamCreateWithFlags(&c->xstreams[i], hipStreamNonBlocking));
+        OSK_HIP(hipEventCreateWithFlags(&c->ev_in[i], hipEventDisableTiming));
+        OSK_HIP(hipEventCreateWithFlags(&c->ev_out[i], hipEventDisableTiming));
+    }
+    return OSK_OK;
+}
+
+// Work enqueued on `st` so far → before the next operation on local device i's exchange stream.
+hipError_t enter_xstream(osk_comm* c, size_t i, hipStream_t st) {
+    hipError_t e = hipEventRecord(c->ev_in[i], st);
+    return e != hipSuccess ? e : hipStreamWaitEvent(c->xstreams[i], c->ev_in[i], 0);
+}
+
+// Everything enqueued on the exchange stream so far → before the next operation on `st`.
+hipError_t leave_xstream(osk_comm* c, size_t i, hipStream_t st) {
+    hipError_t e = hipEventRecord(c->ev_out[i], c->xstreams[i]);
+    return e != hipSuccess ? e : hipStreamWaitEvent(st, c->ev_out[i], 0);
+}
+
 // The per-shard lists of one view, padded to `spr` shards per rank: ws_xkeys [nq][spr][k].
 int32_t search_padded(osk_view* v, const void* d_queries, int nq, int k, const uint64_t* const* d_accept, int spr,
                       hipStream_t st) {
@@ -132,7 +173,8 @@ int32_t search_padded(osk_view* v, const void* d_queries, int nq, int k, const u
 
 // The shardIndex of every gathered slot (rank r's slot j ↔ its view's shard_index[j]; pads INT32_MAX),
 // exchanged once per (comm, spr) and kept in every local view's d_xsi.
-int32_t exchange_shard_index(osk_comm* c, osk_view* const* views, int spr, const hipStream_t* sts) {
+int32_t exchange_shard_index(osk_comm* c, osk_view* const* views, int spr) {
+    const hipStream_t* sts = c->xstreams.data();   // synchronous: behind every earlier collective
     bool fresh = true;
     for (size_t i = 0; i < c->devices.size(); ++i)
         fresh &= views[i]->xsi_comm == c->id && views[i]->xsi_spr == spr;
@@ -141,6 +183,7 @@ int32_t exchange_shard_index(osk_comm* c, osk_view* const* views, int spr, const
     for (size_t i = 0; i < c->devices.size(); ++i) {
         osk_view* v = views[i];
         OSK_HIP(hipSetDevice(v->device));
+        OSK_HIP(hipDeviceSynchronize());   // one-time: no earlier reduce still reads d_xsi
         std::vector<int32_t> mine(spr, 0x7FFFFFFF);
         for (int j = 0; j < v->n_shards; ++j) mine[j] = v->shard_index[j];
         OSK_HIP(v->d_xsi.reserve(sizeof(int32_t) * (size_t)spr * (c->world + 1)));
@@ -226,6 +269,8 @@ int32_t osk_comm_init_rank(int32_t device, int32_t rank, int32_t world, const ui
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof(u));
     OSK_NCCL(R->CommInitRank(&c->comms[0], world, u, rank));
+    rc = make_xstreams(c.get());
+    if (rc) return rc;
     *out = c.release();
     return OSK_OK;
     OSK_GUARD_END
@@ -249,6 +294,8 @@ int32_t osk_comm_init_all(const int32_t* devices, int32_t n, osk_comm** out) {
     c->devices.assign(devices, devices + n);
     c->comms.assign(n, nullptr);
     OSK_NCCL(R->CommInitAll(c->comms.data(), n, devices));
+    int32_t rc = make_xstreams(c.get());
+    if (rc) return rc;
     *out = c.release();
     return OSK_OK;
     OSK_GUARD_END
@@ -286,7 +333,9 @@ int32_t osk_comm_all_gather(osk_comm* comm, const void* d_send, void* d_recv, in
     if (rc) return rc;
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : device_stream(comm->devices[0]);
     std::lock_guard<std::mutex> lk(comm->mu);
-    OSK_NCCL(g_rccl.AllGather(d_send, d_recv, (size_t)bytes, ncclUint8, comm->comms[0], st));
+    OSK_HIP(enter_xstream(comm, 0, st));
+    OSK_NCCL(g_rccl.AllGather(d_send, d_recv, (size_t)bytes, ncclUint8, comm->comms[0], comm->xstreams[0]));
+    OSK_HIP(leave_xstream(comm, 0, st));
     return OSK_OK;
     OSK_GUARD_END
 }
@@ -314,7 +363,7 @@ int32_t osk_shards_search_merge_device(osk_comm* comm, osk_view* view, const voi
     if (rc) return rc;
     osk_view* const vs[1] = {view};
     if (comm->world > 1) {
-        rc = exchange_shard_index(comm, vs, shards_per_rank, &st);
+        rc = exchange_shard_index(comm, vs, shards_per_rank);
         if (rc) return rc;
     } else if (view->xsi_comm != comm->id || view->xsi_spr != shards_per_rank) {
         std::vector<int32_t> mine(shards_per_rank, 0x7FFFFFFF);
@@ -329,8 +378,13 @@ int32_t osk_shards_search_merge_device(osk_comm* comm, osk_view* view, const voi
     if (rc) return rc;
     const uint64_t* image = view->ws_xkeys.as<uint64_t>();
     if (comm->world > 1) {   // world 1: the local lists are the whole image
-        rc = gather_keys(comm, vs, n_queries, k, shards_per_rank, &st);
+        // lists ready on st → the all-gather on the communicator's exchange stream → the reduce on st.
+        // The view's next search (same view, any stream) is ordered after this call's reduce on st
+        // (order_after_last), which waits for this gather, so ws_xkeys / ws_xgath are never raced.
+        OSK_HIP(enter_xstream(comm, 0, st));
+        rc = gather_keys(comm, vs, n_queries, k, shards_per_rank, comm->xstreams.data());
         if (rc) return rc;
+        OSK_HIP(leave_xstream(comm, 0, st));
         image = view->ws_xgath.as<uint64_t>();
     }
     OSK_HIP(launch_coord_reduce(image, nullptr, view->d_xsi.as<int32_t>(), n_queries, comm->world, shards_per_rank, k,
@@ -380,7 +434,7 @@ int32_t osk_shards_search_merge(osk_comm* comm, osk_view* const* views, int32_t 
         OSK_HIP(v->ws_qin.reserve(std::max<size_t>(16, qbytes)));
         OSK_HIP(hipMemcpyAsync(v->ws_qin.p, queries, qbytes, hipMemcpyHostToDevice, sts[i]));
     }
-    rc = exchange_shard_index(comm, views, spr, sts.data());
+    rc = exchange_shard_index(comm, views, spr);
     if (rc) return rc;
     for (int i = 0; i < n_views; ++i) {
         osk_view* v = views[i];
@@ -416,8 +470,16 @@ int32_t osk_shards_search_merge(osk_comm* comm, osk_view* const* views, int32_t 
     }
     const uint64_t* image = views[0]->ws_xkeys.as<uint64_t>();
     if (comm->world > 1) {
-        rc = gather_keys(comm, views, n_queries, k, spr, sts.data());
+        for (int i = 0; i < n_views; ++i) {
+            OSK_HIP(hipSetDevice(views[i]->device));
+            OSK_HIP(enter_xstream(comm, i, sts[i]));
+        }
+        rc = gather_keys(comm, views, n_queries, k, spr, comm->xstreams.data());
         if (rc) return rc;
+        for (int i = 0; i < n_views; ++i) {   // every view's next search reuses its ws_xkeys / ws_xgath
+            OSK_HIP(hipSetDevice(views[i]->device));
+            OSK_HIP(leave_xstream(comm, i, sts[i]));
+        }
         image = views[0]->ws_xgath.as<uint64_t>();
     }
     // the coordinator reduce on local device 0 (every local device holds the same image)

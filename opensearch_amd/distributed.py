@@ -228,13 +228,8 @@ class LocalShards:
             check(lib().osk_seg_synth(device, rows_per_shard, dim, encoding, similarity, seed, dist_kind,
                                       s * rows_per_shard, C.byref(h)))
             self.segs.append(h.value)
-        arr = (C.c_void_p * len(self.segs))(*self.segs)
-        seg_shard = np.arange(len(self.segs), dtype=np.int32)
-        seg_base = np.zeros(len(self.segs), np.int32)
-        sidx = np.asarray(self.shards, np.int32)
-        self.view = C.c_void_p()
-        check(lib().osk_view_create(arr, len(self.segs), ptr(seg_shard), ptr(seg_base), len(self.segs),
-                                    ptr(sidx), C.byref(self.view)))
+        self.extra_views = []
+        self.view = self._new_view()
         # global shardIndex of every gathered slot: rank r's slot j ↔ owned_shards(r)[j]; pad slots (a rank
         # owning fewer shards) get INT32_MAX — their lists are all-zero keys, so they never contribute a hit
         gi = []
@@ -242,6 +237,24 @@ class LocalShards:
             own = owned_shards(r, n_shards, world)
             gi += own + [2**31 - 1] * (self.s_pad - len(own))
         self.global_shard_index = torch.tensor(gi, dtype=torch.int32)
+
+    def _new_view(self) -> C.c_void_p:
+        arr = (C.c_void_p * len(self.segs))(*self.segs)
+        seg_shard = np.arange(len(self.segs), dtype=np.int32)
+        seg_base = np.zeros(len(self.segs), np.int32)
+        sidx = np.asarray(self.shards, np.int32)
+        v = C.c_void_p()
+        check(lib().osk_view_create(arr, len(self.segs), ptr(seg_shard), ptr(seg_base), len(self.segs),
+                                    ptr(sidx), C.byref(v)))
+        return v
+
+    def add_view(self) -> C.c_void_p:
+        """Another view over the same staged segments (its own workspace; the segments are shared and
+        retained): one per search thread, so searches issued on different streams run concurrently on
+        the device instead of waiting for each other's workspace."""
+        v = self._new_view()
+        self.extra_views.append(v)
+        return v
 
     def search(self, d_queries: int, nq: int, k: int, keys: torch.Tensor, counts: torch.Tensor,
                stream: int | None) -> None:
@@ -265,6 +278,9 @@ class LocalShards:
         counts[:, :sl].copy_(tc)
 
     def close(self):
+        for v in self.extra_views:
+            lib().osk_view_release(v)
+        self.extra_views = []
         if self.view:
             lib().osk_view_release(self.view)
             self.view = C.c_void_p()

@@ -125,3 +125,60 @@ def test_comm_errors_are_codes(shardset):
             D.DeviceComm.init_all([0, 0])
     finally:
         comm.close()
+
+
+def test_queries_in_flight_on_views_and_streams(shardset):
+    """bench.py's serving mode: F search threads, each with its own view over the same segments and its
+    own stream, issue single-query steps round-robin through osk_shards_search_merge_device, so
+    consecutive queries overlap on the device.  Every step must equal the serial search."""
+    ds, segs, si = shardset
+    leaves = ds.leaves
+    extra = [LU.DeviceShardSet([[lf] for lf in leaves], si) for _ in range(2)]
+    handles = [ds.handle] + [e.handle for e in extra]
+    comm = D.DeviceComm.init_rank(0, 0, 1, D.DeviceComm.unique_id())
+    try:
+        F, n = len(handles), 24
+        queries = O.synth(0, n, 768, 91, 3)
+        dq = torch.from_numpy(queries).cuda()
+        streams = [torch.cuda.Stream() for _ in range(F)]
+        steps = [D.ShardSearchMerge(comm, h, 3, 1, 10, 0, 10, device=0) for h in handles]
+        torch.cuda.synchronize()
+        got = []
+        for i in range(n):
+            j = i % F
+            res = steps[j](dq[i:i + 1].data_ptr(), streams[j].cuda_stream)
+            with torch.cuda.stream(streams[j]):   # snapshot on the producing stream before slot j is reused
+                got.append([t.clone() for t in res])
+        torch.cuda.synchronize()
+        want = ds.search(queries, 10, 0, 10)
+        for i in range(n):
+            g = [t.cpu().numpy()[0] for t in got[i]]
+            assert np.array_equal(bits(g[0]), bits(want[0][i])) and np.array_equal(g[1], want[1][i])
+            assert np.array_equal(g[2], want[2][i]) and g[3] == want[3][i] and g[4] == want[4][i]
+    finally:
+        comm.close()
+        for e in extra:
+            e.close()
+
+
+def test_raw_all_gather_from_two_streams_keeps_call_order():
+    """Collectives issued from different caller streams run in call order on the communicator's own
+    exchange stream, each after the work its caller stream had enqueued."""
+    comm = D.DeviceComm.init_rank(0, 0, 1, D.DeviceComm.unique_id())
+    try:
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        a = torch.zeros(1 << 20, dtype=torch.int64, device="cuda")
+        b = torch.empty_like(a)
+        c = torch.empty_like(a)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s1):
+            a.fill_(7)                       # enqueued on s1 before its gather
+            comm.all_gather(a, b, s1.cuda_stream)
+        with torch.cuda.stream(s2):
+            s2.wait_stream(s1)
+            comm.all_gather(b, c, s2.cuda_stream)
+            d = c.sum()
+        torch.cuda.synchronize()
+        assert int(d) == 7 * (1 << 20) and torch.equal(b, a)
+    finally:
+        comm.close()

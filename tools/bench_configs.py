@@ -3,7 +3,8 @@
 
   python tools/bench_configs.py [--only C2,C3,...] [--steps N]
 
-Prints one JSON line per (config, batch): QPS, ms per batch, the scan's mean duration per batch
+Prints one JSON line per (config, batch): QPS (with --inflight F batches in flight, each on its own
+stream and view, as concurrent search threads issue them), ms per batch, the scan's mean duration per batch
 (HIP events, osk_view_profile), the fp32-equivalent rate (rows × dim × 4 B per 256 queries ÷ that time:
 what an fp32 scan would have to stream, so it exceeds HBM peak on the int8 prefilter path) and, on the
 prefilter path, the rate of the bytes it actually reads (int8_prefilter_GBps).  Synthetic data from the device generator:
@@ -46,8 +47,21 @@ class View:
         self.v = C.c_void_p()
         _lib.check(L.osk_view_create(arr, n_shards, ss.ctypes.data, None, n_shards, None, C.byref(self.v)))
         self.n_shards, self.rows, self.dim, self.enc = n_shards, rows_per_shard, dim, enc
+        self.extra = []
+
+    def views(self, n):
+        """n views over the same segments (own workspaces): one per query in flight."""
+        while len(self.extra) < n - 1:
+            arr = (C.c_void_p * self.n_shards)(*self.segs)
+            ss = np.arange(self.n_shards, dtype=np.int32)
+            v = C.c_void_p()
+            _lib.check(L.osk_view_create(arr, self.n_shards, ss.ctypes.data, None, self.n_shards, None, C.byref(v)))
+            self.extra.append(v)
+        return [self.v] + self.extra[:n - 1]
 
     def close(self):
+        for v in self.extra:
+            L.osk_view_release(v)
         L.osk_view_release(self.v)
         for h in self.segs:
             L.osk_seg_release(C.c_void_p(h))
@@ -72,6 +86,7 @@ class TorchView(View):
         self.v = C.c_void_p()
         _lib.check(L.osk_view_create(arr, n_shards, ss.ctypes.data, None, n_shards, None, C.byref(self.v)))
         self.n_shards, self.rows, self.dim, self.enc = n_shards, rows_per_shard, dim, _lib.FLOAT32
+        self.extra = []
 
 
 def outlier_rows(n, dim, n_out, scale, seed):
@@ -88,43 +103,66 @@ def qpool_dev(n, dim, dist):
     return torch.from_numpy(synth_host(0, n, dim, 43, dist)).cuda()
 
 
-def run(view, queries, batch, steps, warmup, accept_ptrs=None, k=10):
+INFLIGHT = 1
+
+
+def run_slots(view, queries, batch, steps, warmup, accept_ptrs, k, slots):
+    """ms per batch with `slots` queries in flight (round-robin over views and streams) and the scan
+    kernel's mean launch duration."""
     S = view.n_shards
-    keys = torch.empty((batch, S, k), dtype=torch.int64, device="cuda")
-    cnt = torch.empty((batch, S), dtype=torch.int32, device="cuda")
-    torch.cuda.set_stream(torch.cuda.Stream())   # non-null: 0 would mean the library's own stream
-    stream = torch.cuda.current_stream().cuda_stream
+    views = view.views(slots)
+    keys = [torch.empty((batch, S, k), dtype=torch.int64, device="cuda") for _ in range(slots)]
+    cnt = [torch.empty((batch, S), dtype=torch.int32, device="cuda") for _ in range(slots)]
+    streams = [torch.cuda.Stream() for _ in range(slots)]   # non-null: 0 would mean the library's own stream
     nq_pool = queries.shape[0] // batch
     acc = None if accept_ptrs is None else accept_ptrs.data_ptr()
 
     def step(i):
+        j = i % slots
         q = queries[(i % nq_pool) * batch:(i % nq_pool + 1) * batch]
-        _lib.check(L.osk_view_search_device(view.v, q.data_ptr(), batch, k, acc, keys.data_ptr(), cnt.data_ptr(), None, stream))
+        _lib.check(L.osk_view_search_device(views[j], q.data_ptr(), batch, k, acc, keys[j].data_ptr(),
+                                            cnt[j].data_ptr(), None, streams[j].cuda_stream))
 
-    for i in range(warmup):
+    for i in range(max(warmup, slots)):
         step(i)
     torch.cuda.synchronize()
-    _lib.check(L.osk_view_profile(view.v, 1))
+    for v in views:
+        _lib.check(L.osk_view_profile(v, 1))
     t0 = time.perf_counter()
     for i in range(steps):
         step(i)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    ms, calls = C.c_double(), C.c_int64()
-    _lib.check(L.osk_view_scan_time(view.v, C.byref(ms), C.byref(calls)))
-    _lib.check(L.osk_view_profile(view.v, 0))
-    assert int(cnt.min()) >= 0
-    return dt / steps * 1e3, ms.value / max(1, calls.value)
+    tot, n = 0.0, 0
+    for v in views:
+        ms, calls = C.c_double(), C.c_int64()
+        _lib.check(L.osk_view_scan_time(v, C.byref(ms), C.byref(calls)))
+        _lib.check(L.osk_view_profile(v, 0))
+        tot, n = tot + ms.value, n + calls.value
+    assert all(int(c.min()) >= 0 for c in cnt)
+    return dt / steps * 1e3, tot / max(1, n)
+
+
+def run(view, queries, batch, steps, warmup, accept_ptrs=None, k=10):
+    """(ms per batch with INFLIGHT queries in flight, the scan's isolated mean launch duration)."""
+    ms, km = run_slots(view, queries, batch, steps, warmup, accept_ptrs, k, INFLIGHT)
+    if INFLIGHT > 1:   # overlapped launches share HBM: the kernel's own duration from a one-in-flight pass
+        _, km = run_slots(view, queries, batch, max(3, steps // 2), 2, accept_ptrs, k, 1)
+    return ms, km
 
 
 def counter(view, name):
-    v = C.c_int64()
-    _lib.check(L.osk_view_counter(view.v, name.encode(), C.byref(v)))
-    return v.value
+    tot = 0
+    for h in [view.v] + view.extra:
+        v = C.c_int64()
+        _lib.check(L.osk_view_counter(h, name.encode(), C.byref(v)))
+        tot += v.value
+    return tot
 
 
 def emit(name, view, batch, ms_step, kernel_ms, bytes_per_launch, extra=None):
-    rec = {"config": name, "batch": batch, "qps": batch / (ms_step * 1e-3), "ms_per_batch": ms_step,
+    rec = {"config": name, "batch": batch, "inflight": INFLIGHT, "qps": batch / (ms_step * 1e-3),
+           "ms_per_batch": ms_step,
            "kernel_ms": kernel_ms, "fp32_equiv_GBps": bytes_per_launch / (kernel_ms * 1e-3) / 1e9,
            "rows": view.n_shards * view.rows, "dim": view.dim, "shards": view.n_shards}
     rows = view.n_shards * view.rows
@@ -150,7 +188,10 @@ def main():
     ap.add_argument("--c5f-modes", default="1:0,0:0",
                     help="C5f filter modes filter_gather:gather_min, comma-separated (1:0 = compacted gather, 0:0 = "
                          "bitset window walk)")
+    ap.add_argument("--inflight", type=int, default=1, help="queries (batches) in flight: one view + stream each")
     a = ap.parse_args()
+    global INFLIGHT
+    INFLIGHT = a.inflight
     a.c5f_modes = [tuple(int(x) for x in m.split(":")) for m in a.c5f_modes.split(",")]
     for kv in a.tune:
         key, val = kv.split("=")
@@ -194,13 +235,15 @@ def main():
                     _lib.tune("filter_gather", gmode)
                     _lib.tune("gather_min", gmin)
                     r0, x0 = counter(v, "sq8_rescored_rows"), counter(v, "sq8_exact_tiles")
+                    c0 = counter(v, "sq8_calls")
                     ms, km = run(v, q, 1, st, wu, accept_ptrs=ptrs)
+                    nc = max(1, counter(v, "sq8_calls") - c0)
                     # the prefilter's own bytes: accepted int8 rows + 16-B bound terms + the bitset
                     b8 = int(10_000_000 * sel) * (768 + 16) + 10_000_000 // 8
                     emit(f"C5f-{int(sel * 100)}%", v, 1, ms, km, int(10_000_000 * sel) * 768 * 4 + 10_000_000 // 8,
                          {"selectivity": sel, "filter_gather": gmode, "gather_min": gmin,
-                          "rescored_rows_per_query": (counter(v, "sq8_rescored_rows") - r0) / (st + wu),
-                          "exact_lists_per_query": (counter(v, "sq8_exact_tiles") - x0) / (st + wu),
+                          "rescored_rows_per_query": (counter(v, "sq8_rescored_rows") - r0) / nc,
+                          "exact_lists_per_query": (counter(v, "sq8_exact_tiles") - x0) / nc,
                           "int8_prefilter_GBps": b8 / (km * 1e-3) / 1e9})
                 _lib.tune("filter_gather", 1)
                 _lib.tune("gather_min", 0)
@@ -215,11 +258,13 @@ def main():
                 _lib.tune("sq8", sq8)
                 r0, x0 = counter(v, "sq8_rescored_rows"), counter(v, "sq8_exact_tiles")
                 f0 = counter(v, "sq8_fallback_queries")
+                c0 = counter(v, "sq8_calls")
                 ms, km = run(v, q, 1, st, wu)
+                nc = max(1, counter(v, "sq8_calls") - c0)
                 emit(f"C3o-{n_out}x{scale:g}", v, 1, ms, km, 10_000_000 * 768 * 4,
                      {"outlier_dims": n_out, "outlier_scale": scale, "prefilter": sq8,
-                      "rescored_rows_per_query": (counter(v, "sq8_rescored_rows") - r0) / (st + wu),
-                      "exact_lists_per_query": (counter(v, "sq8_exact_tiles") - x0) / (st + wu),
+                      "rescored_rows_per_query": (counter(v, "sq8_rescored_rows") - r0) / nc,
+                      "exact_lists_per_query": (counter(v, "sq8_exact_tiles") - x0) / nc,
                       "fallback_queries": counter(v, "sq8_fallback_queries") - f0})
             _lib.tune("sq8", 1)
             v.close()
