@@ -12,7 +12,8 @@ import os
 import threading
 from pathlib import Path
 
-LIB_PATH = Path(__file__).resolve().with_name("libosknn.so")
+# OSKNN_LIB: another build of the same ABI (A/B timing of two builds in one GPU call; tools only)
+LIB_PATH = Path(os.environ.get("OSKNN_LIB") or Path(__file__).resolve().with_name("libosknn.so")).resolve()
 # same ABI plus the test/A-B-only knobs (osknn.h): loaded only inside `with testing():`
 TESTING_LIB_PATH = Path(__file__).resolve().with_name("libosknn_testing.so")
 

@@ -5,8 +5,8 @@
 
 The product library lands at opensearch_amd/libosknn.so (git-ignored, shipped to the GPU box by
 gpurun).  A second library, opensearch_amd/libosknn_testing.so, links the same objects except the C-ABI
-translation unit, which is compiled with -DOSK_TESTING: it adds the result-corrupting A/B and test
-knobs (ablations, forced exact fallback, settle traces, workspace debug copies) that the shipped
+and prefilter translation units, which are compiled with -DOSK_TESTING: it adds the result-corrupting
+A/B and test knobs (ablations, forced exact fallback, settle traces, workspace debug copies) that the shipped
 library refuses.  Objects are compiled in parallel into build/osknn/.
 """
 from __future__ import annotations
@@ -24,7 +24,8 @@ CSRC = PKG / "csrc"
 INCLUDE = ROOT / "include"
 LIB = PKG / "libosknn.so"
 LIB_TESTING = PKG / "libosknn_testing.so"
-TESTING_VARIANT = "osk_api.hip"   # the only source whose object differs in the testing build
+# the sources whose objects differ in the testing build (the C-ABI's test knobs; sq8_mfma's A/B ablations)
+TESTING_VARIANTS = ("osk_api.hip", "osk_sq8.hip")
 OBJDIR = ROOT / "build" / "osknn"
 
 SOURCES = ["osk_kernels.hip", "osk_mfma.hip", "osk_sq8.hip", "osk_filter.hip", "osk_select.hip", "osk_api.hip", "osk_comm.hip", "osk_host.cpp"]
@@ -63,11 +64,11 @@ def _compile(job) -> Path:
 def build(force: bool = False, verbose: bool = True) -> Path:
     if not force and not _stale():
         return LIB
-    jobs = [(s, False) for s in SOURCES] + [(TESTING_VARIANT, True)]
+    jobs = [(s, False) for s in SOURCES] + [(s, True) for s in TESTING_VARIANTS]
     with cf.ThreadPoolExecutor(max_workers=len(jobs)) as ex:
         objs = dict(zip(jobs, ex.map(_compile, jobs)))
     for lib, testing in ((LIB, False), (LIB_TESTING, True)):
-        parts = [objs[(s, testing and s == TESTING_VARIANT)] for s in SOURCES]
+        parts = [objs[(s, testing and s in TESTING_VARIANTS)] for s in SOURCES]
         tmp = lib.with_suffix(".so.tmp")
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp)] + [str(o) for o in parts]
         r = subprocess.run(cmd, capture_output=True, text=True)

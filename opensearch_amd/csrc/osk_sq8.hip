@@ -654,31 +654,42 @@ __host__ __device__ __forceinline__ int ring_rows_units(int u8, int ks) {
     return u8 > 4 * (ks - 1) ? 16 * u8 : ks * 64;
 }
 
-// wait until at most n·OPS of this wave's vector-memory operations are outstanding (n ≤ 7)
-template <int OPS>
-__device__ __forceinline__ void vm_wait_groups(int n) {
-    switch (n) {
-        case 0: vm_wait<0>(); break;
-        case 1: vm_wait<OPS>(); break;
-        case 2: vm_wait<2 * OPS>(); break;
-        case 3: vm_wait<3 * OPS>(); break;
-        case 4: vm_wait<4 * OPS>(); break;
-        case 5: vm_wait<5 * OPS>(); break;
-        case 6: vm_wait<6 * OPS>(); break;
-        default: vm_wait<7 * OPS>(); break;
+// A lane's 4 rows' bound terms {s, s·|q|, |x − s·q|, |x|²} as row pairs (rows 0/1, rows 2/3) per component,
+// the layout packed fp32 math (v_pk_fma_f32) takes without register shuffles.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+struct AuxQ {
+    f32x2 x[2], y[2], z[2], w[2];
+    __device__ __forceinline__ float4 row(int i) const {
+        const int h = i >> 1, j = i & 1;
+        return make_float4(x[h][j], y[h][j], z[h][j], w[h][j]);
     }
-}
+    __device__ __forceinline__ void set(float4 a0, float4 a1, float4 a2, float4 a3) {
+        x[0] = f32x2{a0.x, a1.x};
+        y[0] = f32x2{a0.y, a1.y};
+        z[0] = f32x2{a0.z, a1.z};
+        w[0] = f32x2{a0.w, a1.w};
+        x[1] = f32x2{a2.x, a3.x};
+        y[1] = f32x2{a2.y, a3.y};
+        z[1] = f32x2{a2.z, a3.z};
+        w[1] = f32x2{a2.w, a3.w};
+    }
+};
 
 // QB query blocks of 16 per launch (QB = 2: 32 queries, two MFMA chains sharing the row operand).
 // RING (unfiltered launches, KS ≤ 4): rows are not loaded into VGPRs but streamed by LDS-DMA from the
-// row-major int8 copy (exact width: no tiled copy, no padding) into a per-wave ring of p.ring_slots
-// 16-row groups, ring_slots − 1 groups ahead of the one being scored, so a wave keeps several groups in
+// row-major int8 copy (exact width: no tiled copy, no padding) into a per-wave ring of NS
+// 16-row groups, NS − 1 groups ahead of the one being scored, so a wave keeps several groups in
 // flight without holding their registers (the register path holds one group: latency-bound at small
 // dims, ≈2.8 TB/s loads-only at 96 dims).
 // SIM is compile-time: with the similarity a runtime value every (row, query) pair paid the COSINE
 // row-norm square root and a switch (≈ 50 VALU + 30 SALU per pair at 96 dims).
-template <int KS, int QB, bool RING, int SIM>
-__global__ __launch_bounds__(kBlock, QB == 1 ? 4 : (RING ? 2 : 3)) void sq8_mfma(Sq8Params p) {
+// NS: ring depth in 16-row groups per wave (0 = register loads), compile-time so that the per-group
+// completion wait is one s_waitcnt of a constant count.
+template <int KS, int QB, int NS, int SIM>
+// KS = 2 ring instances are capped at 128 VGPRs: their LDS holds four workgroups per CU, and 4 waves per
+// SIMD need ≤ 128 (C4 b32: 123 VGPRs 2.71 ms, 131 VGPRs 2.89 ms per 32 queries).  KS = 4 rings fit two.
+__global__ __launch_bounds__(kBlock, QB == 1 || (NS && KS == 2) ? 4 : (NS ? 2 : 3)) void sq8_mfma(Sq8Params p) {
+    constexpr bool RING = NS > 0;
     typedef int i32x4 __attribute__((ext_vector_type(4)));
     constexpr int NQ = 16 * QB, R = 16, UQ = 4 * KS;   // UQ: 16-B units per query in LDS
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform: scalar loop control
@@ -694,7 +705,7 @@ __global__ __launch_bounds__(kBlock, QB == 1 ? 4 : (RING ? 2 : 3)) void sq8_mfma
     // RING: the ring overlays the query block (queries are copied into VGPRs first), lists follow both
     const int ring_rows = RING ? ring_rows_units(u8, KS) : 0;
     const int ring_slot = ring_rows + 16;
-    const int lists_off = RING ? max(NQ * UQ, 4 * p.ring_slots * ring_slot) : NQ * UQ;
+    const int lists_off = RING ? max(NQ * UQ, 4 * NS * ring_slot) : NQ * UQ;
     uint64_t* s_lk = reinterpret_cast<uint64_t*>(sq + lists_off);
     uint32_t* s_lp = reinterpret_cast<uint32_t*>(s_lk + 4 * NQ * kKQ);
     for (int i = tid; i < NQ * UQ; i += kBlock) {
@@ -729,6 +740,32 @@ __global__ __launch_bounds__(kBlock, QB == 1 ? 4 : (RING ? 2 : 3)) void sq8_mfma
         tkey[qb] = t;
         tq[qb] = sq8_quick(sim, t, sqn[qb], p.cos_slack);
     }
+    // Quick test of DOT / COSINE / MIP as one fma chain per (row, query): hq = I·s_x·s_b + E with
+    //   E = |x|_q·QY + |δ_x|·QZ + |x|²·QW + Q0, per-query coefficients rounded up from
+    //   QY = (s_b|δ_b| + 2^-18·(s_b|q_b| + |δ_b|))(1 + 2^-18), QZ = (s_b|q_b| + |δ_b|)(1 + 2^-18),
+    //   QW = γ(1 + 2^-18), Q0 = γ|b|²(1 + 2^-18).
+    // hq ≥ the upper bound sq8_bound_side computes, whatever the rounding: E exceeds its error terms by
+    // 2^-18 of themselves plus 2^-18·s_x|q_x|·(s_b|q_b| + |δ_b|) ≥ 2^-18·|I·s_x·s_b| (Cauchy–Schwarz on
+    // the integer vectors), more than its 2^-20 slack and every float rounding of both computations
+    // (< 2^-21 relative).  So a pair the precise bound would pass always passes here; the rare
+    // insertions then evaluate sq8_bounds exactly as before.
+    // per query block: the lane's query coefficients (broadcast to both halves of the packed row-pair math)
+    float QY[QB], QZ[QB], Q0[QB];
+    uint64_t qvm[QB];
+    const float QW = __double2float_ru((double)p.gam * (1.0 + 0x1p-18));
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+        const double r = 1.0 + 0x1p-18;
+        QY[qb] = __double2float_ru(((double)qc[qb].y + 0x1p-18 * (double)qc[qb].z) * r);
+        QZ[qb] = __double2float_ru((double)qc[qb].z * r);
+        Q0[qb] = __double2float_ru((double)p.gam * (double)qc[qb].w * r);
+        qvm[qb] = __ballot(qv[qb]);
+    }
+#ifdef OSK_TESTING
+    const int ablate = p.ablate;
+#else
+    constexpr int ablate = 0;   // A/B knobs exist only in libosknn_testing.so
+#endif
     const bool pilot = p.pilot != 0;
     bool sampled = false;   // pilot: this wave's first group is done
 
@@ -752,7 +789,8 @@ __global__ __launch_bounds__(kBlock, QB == 1 ? 4 : (RING ? 2 : 3)) void sq8_mfma
     };
     auto load_aux = [&](const int64_t (&ro)[4], const bool (&vo)[4], float4 (&ax)[4]) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ax[i] = vo[i] ? load_f4_g(AX + ro[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int i = 0; i < 4; ++i)   // unconditional (clamped) loads: one wait for all four, not four
+            ax[i] = load_f4_g(AX + (vo[i] ? ro[i] : (int64_t)tile.row_begin));
     };
     // RING (KS ≤ 4): the queries' B fragments live in VGPRs for the whole scan (≤ 32), not re-read
     // from LDS per group
@@ -767,13 +805,13 @@ __global__ __launch_bounds__(kBlock, QB == 1 ? 4 : (RING ? 2 : 3)) void sq8_mfma
             }
         __syncthreads();   // every wave holds its fragments before any ring write lands on the queries
     }
-    auto process_loaded = [&](const i32x4 (&a)[KS], const float4 (&ax)[4], bool vA, const int64_t (&ro)[4],
+    auto process_loaded = [&](const i32x4 (&a)[KS], const AuxQ& aq, bool vA, const int64_t (&ro)[4],
                               const bool (&vo)[4]) {
         nvis += __popcll(__ballot(lane < 16 && vA));
         i32x4 acc[QB];
 #pragma unroll
         for (int qb = 0; qb < QB; ++qb) acc[qb] = i32x4{0, 0, 0, 0};
-        if (p.ablate & 2) {
+        if (ablate & 2) {
 #pragma unroll
             for (int s = 0; s < KS; ++s) acc[0] ^= a[s];
         } else {
@@ -791,28 +829,54 @@ __global__ __launch_bounds__(kBlock, QB == 1 ? 4 : (RING ? 2 : 3)) void sq8_mfma
                     acc[qb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[s], b, acc[qb], 0, 0, 0);
                 }
         }
-        if (p.ablate & 1) {
-            if (acc[0][0] + acc[0][1] + acc[0][2] + acc[0][3] == 0x7FFFFFFF && ax[0].x == 1.0f) nvis += 1;
+        if (ablate & 1) {
+            if (acc[0][0] + acc[0][1] + acc[0][2] + acc[0][3] == 0x7FFFFFFF && aq.x[0].x == 1.0f) nvis += 1;
             return;
         }
-        bool pass[QB][4];
-        uint32_t qm = 0u;   // queries with a passing lane (wave-uniform after the ballots)
+        uint64_t pm[QB][4];   // lanes whose (row i, query) pair passes the quick test (lane masks; rows
+                              // past a partial group's end may be set: insertions re-check vo)
+        uint32_t qm = 0u;     // queries with a passing lane (wave-uniform)
         // both bounds of a pair, for the rare list insertions and the pilot (the quick test reads one)
         auto bounds = [&](int qb, int i, float& lo, float& hi) {
-            sq8_bounds(sim, (float)acc[qb][i], ax[i], qc[qb], p.gam, p.g2, lo, hi);
+            sq8_bounds(sim, (float)acc[qb][i], aq.row(i), qc[qb], p.gam, p.g2, lo, hi);
         };
-#pragma unroll
-        for (int qb = 0; qb < QB; ++qb) {
-            bool anyp = false;
+        if constexpr (SIM == SIM_EUCLIDEAN || QB == 1) {
+            // (one query block: the register-capped 4-workgroup instances keep the precise side)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const float sx = SIM == SIM_COSINE ? __builtin_amdgcn_sqrtf(ax[i].w) : 0.0f;   // (v_sqrt: 1 ulp ≪ the 2^-16 quick-test slack)
-                const float side = sq8_bound_side(sim, (float)acc[qb][i], ax[i], qc[qb], p.gam, p.g2);
-                pass[qb][i] = vo[i] && qv[qb] && sq8_pass(sim, side, side, tq[qb], sx);
-                anyp |= pass[qb][i];
+                const float4 axi = aq.row(i);
+                const float sx = SIM == SIM_COSINE ? __builtin_amdgcn_sqrtf(axi.w) : 0.0f;
+#pragma unroll
+                for (int qb = 0; qb < QB; ++qb) {
+                    const float side = sq8_bound_side(sim, (float)acc[qb][i], axi, qc[qb], p.gam, p.g2);
+                    pm[qb][i] = __ballot(sq8_pass(sim, side, side, tq[qb], sx));
+                }
             }
-            if (!pilot) {
-                const uint64_t bl = __ballot(anyp);
+        } else {
+            // packed over row pairs: 3 + 2 v_pk_fma/mul per (row pair, query block)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                f32x2 sx2 = {1.0f, 1.0f};
+                if constexpr (SIM == SIM_COSINE)   // (v_sqrt: 1 ulp ≪ the 2^-16 quick-test slack)
+                    sx2 = f32x2{__builtin_amdgcn_sqrtf(aq.w[h].x), __builtin_amdgcn_sqrtf(aq.w[h].y)};
+#pragma unroll
+                for (int qb = 0; qb < QB; ++qb) {
+                    const f32x2 I2 = {(float)acc[qb][2 * h], (float)acc[qb][2 * h + 1]};
+                    const f32x2 E = __builtin_elementwise_fma(
+                        aq.y[h], f32x2{QY[qb], QY[qb]},
+                        __builtin_elementwise_fma(aq.z[h], f32x2{QZ[qb], QZ[qb]},
+                                                  __builtin_elementwise_fma(aq.w[h], f32x2{QW, QW}, f32x2{Q0[qb], Q0[qb]})));
+                    const f32x2 hq = __builtin_elementwise_fma(I2, aq.x[h] * f32x2{qc[qb].x, qc[qb].x}, E);
+                    const f32x2 thr = SIM == SIM_COSINE ? sx2 * f32x2{tq[qb], tq[qb]} : f32x2{tq[qb], tq[qb]};
+                    pm[qb][2 * h] = __ballot(!(hq.x < thr.x));
+                    pm[qb][2 * h + 1] = __ballot(!(hq.y < thr.y));
+                }
+            }
+        }
+        if (!pilot) {
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb) {
+                const uint64_t bl = (pm[qb][0] | pm[qb][1] | pm[qb][2] | pm[qb][3]) & qvm[qb];
                 qm |= (uint32_t)((bl | (bl >> 16) | (bl >> 32) | (bl >> 48)) & 0xFFFFull) << (16 * qb);
             }
         }
@@ -847,7 +911,7 @@ __global__ __launch_bounds__(kBlock, QB == 1 ? 4 : (RING ? 2 : 3)) void sq8_mfma
                 if (qb != bq) continue;   // (wave-uniform)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const bool o = pass[qb][i] && col == bc;
+                    const bool o = ((pm[qb][i] >> lane) & 1ull) && vo[i] && col == bc;
                     float xnd = 0.0f;
                     if (sim == SIM_COSINE && o) xnd = seg.xnorm_f[ro[i]];
                     float lo, hi;
@@ -870,10 +934,93 @@ __global__ __launch_bounds__(kBlock, QB == 1 ? 4 : (RING ? 2 : 3)) void sq8_mfma
         load_group(rowA, vA, a);
         float4 ax[4];
         load_aux(ro, vo, ax);
-        process_loaded(a, ax, vA, ro, vo);
+        AuxQ aq;
+        aq.set(ax[0], ax[1], ax[2], ax[3]);
+        process_loaded(a, aq, vA, ro, vo);
     };
 
-    if (abits && !seg.ord_to_doc) {
+    if constexpr (RING) {   // (launched unfiltered only: the filter paths are not compiled in)
+        // group slot: KS·64 units of rows (the group's 16·u8 units, lane-linear; lanes past them load unit
+        // 0 again, never read) then 16 units of bound terms.  Per group KS + 1 LDS-DMA instructions.
+        constexpr int OPS = KS + 1;
+        const int SLOT = ring_slot;
+        int4* ring = sq + wave * NS * SLOT;
+        const uint32_t ring_lds =
+            __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(__attribute__((address_space(3))) int4*)ring);
+        const int4* __restrict__ X8 = p.rows8[tile.seg];
+        const int n_groups = pilot ? min<int64_t>(1, (we - wb + 15) / 16) : (int)((we - wb + 15) / 16);
+        auto issue = [&](int g, int slot_idx) {
+            // the slot's previous group was read by this wave's ds_reads: retire them before the DMA
+            // can overwrite it (the compiler may sink their consumers past this point)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const int64_t r0 = wb + (int64_t)g * 16;
+            const int nu = (int)min<int64_t>(16, we - r0) * u8;
+            const int4* src = X8 + r0 * u8;
+            const uint32_t dst = ring_lds + (uint32_t)(slot_idx * SLOT * 16);
+#pragma unroll
+            for (int i = 0; i < KS; ++i) {
+                const int u = i * 64 + lane;
+                if (u < ring_rows) glds16(src + (u < nu ? u : 0), dst + i * 1024);
+            }
+            const int nr = (int)min<int64_t>(16, we - r0);
+            if (lane < 16) glds16(AX + r0 + (lane < nr ? lane : 0), dst + ring_rows * 16);
+        };
+        constexpr int D = NS - 1;
+        // slots are used round robin: group g in slot g mod NS (kept as running counters, no division)
+        int s_issue = 0, s_read = 0;
+        for (int g = 0; g < D && g < n_groups; ++g) {
+            issue(g, s_issue);
+            s_issue = s_issue + 1 == NS ? 0 : s_issue + 1;
+        }
+        for (int g = 0; g < n_groups; ++g) {
+            if (g + D < n_groups) {
+                issue(g + D, s_issue);
+                s_issue = s_issue + 1 == NS ? 0 : s_issue + 1;
+            }
+            // this wave's LDS-DMAs issued after group g's: (min(g + D, n − 1) − g) groups
+            // groups issued after this one: D in the steady state (one wait of a constant count); in the
+            // last D groups nothing more is issued and waiting for everything is exact enough
+            if (g + D < n_groups)
+                vm_wait<D * OPS>();
+            else
+                vm_wait<0>();
+            const int64_t r0 = wb + (int64_t)g * 16;
+            const int nr = (int)min<int64_t>(16, we - r0);   // rows of this group (32-bit tests below)
+            const bool vA = col < nr;
+            int64_t ro[4];
+            bool vo[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                ro[i] = r0 + 4 * grp + i;
+                vo[i] = 4 * grp + i < nr;
+            }
+            const int4* slot = ring + s_read * SLOT;
+            s_read = s_read + 1 == NS ? 0 : s_read + 1;
+            // No masking: a chunk past the row's u8 units meets zero query bytes (the query block is
+            // zero-padded), so whatever it holds adds 0 to the exact int32 dot; rows past the group's end
+            // (and their bound terms) only produce lanes that vA / vo exclude.
+            i32x4 a[KS];
+#pragma unroll
+            for (int s8 = 0; s8 < KS; ++s8) {
+                const int f = s8 * 4 + grp;
+                const int4 v = slot[col * u8 + (f < u8 ? f : 0)];
+                a[s8] = i32x4{v.x, v.y, v.z, v.w};
+            }
+            // bound terms of rows 4·grp + 0..3, read as row pairs per component (ds_read2_b32); unconditional
+            // reads (a read under vo[i] waited for each alone)
+            const float* af = reinterpret_cast<const float*>(slot + ring_rows + 4 * grp);
+            AuxQ aq;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                aq.x[h] = f32x2{af[8 * h + 0], af[8 * h + 4]};
+                aq.y[h] = f32x2{af[8 * h + 1], af[8 * h + 5]};
+                aq.z[h] = f32x2{af[8 * h + 2], af[8 * h + 6]};
+                aq.w[h] = f32x2{af[8 * h + 3], af[8 * h + 7]};
+            }
+            process_loaded(a, aq, vA, ro, vo);
+        }
+        vm_wait<0>();
+    } else if (abits && !seg.ord_to_doc) {
         // filter pushdown: the accepted rows of each 64-row window, compacted (positions in `pos`)
         for (int64_t w0 = wb; w0 < we && !sampled; w0 += 64) {
             const int64_t word = w0 >> 6;
@@ -902,78 +1049,6 @@ __global__ __launch_bounds__(kBlock, QB == 1 ? 4 : (RING ? 2 : 3)) void sq8_mfma
                 process(rowA, vA, ro, vo);
             }
         }
-    } else if constexpr (RING) {
-        // group slot: KS·64 units of rows (the group's 16·u8 units, lane-linear; lanes past them load unit
-        // 0 again, never read) then 16 units of bound terms.  Per group KS + 1 LDS-DMA instructions.
-        constexpr int OPS = KS + 1;
-        const int NS = p.ring_slots, SLOT = ring_slot;
-        int4* ring = sq + wave * NS * SLOT;
-        const uint32_t ring_lds =
-            __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(__attribute__((address_space(3))) int4*)ring);
-        const int4* __restrict__ X8 = p.rows8[tile.seg];
-        const int n_groups = pilot ? min<int64_t>(1, (we - wb + 15) / 16) : (int)((we - wb + 15) / 16);
-        auto issue = [&](int g, int slot_idx) {
-            // the slot's previous group was read by this wave's ds_reads: retire them before the DMA
-            // can overwrite it (the compiler may sink their consumers past this point)
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            const int64_t r0 = wb + (int64_t)g * 16;
-            const int nu = (int)min<int64_t>(16, we - r0) * u8;
-            const int4* src = X8 + r0 * u8;
-            const uint32_t dst = ring_lds + (uint32_t)(slot_idx * SLOT * 16);
-#pragma unroll
-            for (int i = 0; i < KS; ++i) {
-                const int u = i * 64 + lane;
-                if (u < ring_rows) glds16(src + (u < nu ? u : 0), dst + i * 1024);
-            }
-            const int nr = (int)min<int64_t>(16, we - r0);
-            if (lane < 16) glds16(AX + r0 + (lane < nr ? lane : 0), dst + ring_rows * 16);
-        };
-        const int D = NS - 1;
-        // slots are used round robin: group g in slot g mod NS (kept as running counters, no division)
-        int s_issue = 0, s_read = 0;
-        for (int g = 0; g < D && g < n_groups; ++g) {
-            issue(g, s_issue);
-            s_issue = s_issue + 1 == NS ? 0 : s_issue + 1;
-        }
-        for (int g = 0; g < n_groups; ++g) {
-            if (g + D < n_groups) {
-                issue(g + D, s_issue);
-                s_issue = s_issue + 1 == NS ? 0 : s_issue + 1;
-            }
-            // this wave's LDS-DMAs issued after group g's: (min(g + D, n − 1) − g) groups
-            vm_wait_groups<OPS>(min(g + D, n_groups - 1) - g);
-            const int64_t r0 = wb + (int64_t)g * 16;
-            const int nr = (int)min<int64_t>(16, we - r0);   // rows of this group (32-bit tests below)
-            const bool vA = col < nr;
-            int64_t ro[4];
-            bool vo[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                ro[i] = r0 + 4 * grp + i;
-                vo[i] = 4 * grp + i < nr;
-            }
-            const int4* slot = ring + s_read * SLOT;
-            s_read = s_read + 1 == NS ? 0 : s_read + 1;
-            // No masking: a chunk past the row's u8 units meets zero query bytes (the query block is
-            // zero-padded), so whatever it holds adds 0 to the exact int32 dot; rows past the group's end
-            // (and their bound terms) only produce lanes that vA / vo exclude.
-            i32x4 a[KS];
-#pragma unroll
-            for (int s8 = 0; s8 < KS; ++s8) {
-                const int f = s8 * 4 + grp;
-                const int4 v = slot[col * u8 + (f < u8 ? f : 0)];
-                a[s8] = i32x4{v.x, v.y, v.z, v.w};
-            }
-            float4 ax[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {   // unconditional reads (a read under vo[i] waited for each alone)
-                const int4 t4 = slot[ring_rows + 4 * grp + i];
-                ax[i] = make_float4(__int_as_float(t4.x), __int_as_float(t4.y), __int_as_float(t4.z),
-                                    __int_as_float(t4.w));
-            }
-            process_loaded(a, ax, vA, ro, vo);
-        }
-        vm_wait<0>();
     } else {
         for (int64_t r0 = wb; r0 < we && !sampled; r0 += R) {
             const int64_t rowA = r0 + col;
@@ -1047,11 +1122,13 @@ using Sq8MfmaFn = void (*)(Sq8Params);
 static const int kMfmaKS[6] = {2, 4, 6, 8, 12, 16};
 #define OSK_MFMA_SIMS(KS, QB, RG) {sq8_mfma<KS, QB, RG, 0>, sq8_mfma<KS, QB, RG, 1>, sq8_mfma<KS, QB, RG, 2>, \
                                    sq8_mfma<KS, QB, RG, 3>}
-#define OSK_MFMA_ROW(KS) {OSK_MFMA_SIMS(KS, 1, false), OSK_MFMA_SIMS(KS, 2, false)}
+#define OSK_MFMA_ROW(KS) {OSK_MFMA_SIMS(KS, 1, 0), OSK_MFMA_SIMS(KS, 2, 0)}
 static const Sq8MfmaFn kSq8Mfma[6][2][4] = {OSK_MFMA_ROW(2), OSK_MFMA_ROW(4), OSK_MFMA_ROW(6),
                                             OSK_MFMA_ROW(8), OSK_MFMA_ROW(12), OSK_MFMA_ROW(16)};
-static const Sq8MfmaFn kSq8MfmaRing[2][2][4] = {{OSK_MFMA_SIMS(2, 1, true), OSK_MFMA_SIMS(2, 2, true)},
-                                                {OSK_MFMA_SIMS(4, 1, true), OSK_MFMA_SIMS(4, 2, true)}};
+// ring depths 2 (the default: four workgroups per CU) and 4
+static const Sq8MfmaFn kSq8MfmaRing[2][2][2][4] = {
+    {{OSK_MFMA_SIMS(2, 1, 2), OSK_MFMA_SIMS(2, 2, 2)}, {OSK_MFMA_SIMS(4, 1, 2), OSK_MFMA_SIMS(4, 2, 2)}},
+    {{OSK_MFMA_SIMS(2, 1, 4), OSK_MFMA_SIMS(2, 2, 4)}, {OSK_MFMA_SIMS(4, 1, 4), OSK_MFMA_SIMS(4, 2, 4)}}};
 
 int sq8_mfma_supported(int u8) { return u8 <= 4 * kMfmaKS[5]; }
 // dynamic LDS of an sq8_mfma launch: queries [NQ][4·KS] units (overlaid by the ring when ns > 1) and
@@ -1071,19 +1148,10 @@ int sq8_ring_slots(int u8, int qb, int want) {
     int c = 0;
     while (c < 5 && 4 * kMfmaKS[c] < u8) ++c;
     if (c > 1 || want == 0) return 0;
-    const int ks = kMfmaKS[c];
-    auto lds = [&](int ns) { return sq8_mfma_lds(u8, qb, ns); };
-    if (want > 1) {   // at most one workgroup's worth of LDS
-        int ns = std::min(want, 8);
-        while (ns > 2 && lds(ns) > 160 * 1024) --ns;
-        return ns;
-    }
-    // default: the most workgroups per CU (LDS), then the deepest ring at that count
-    int best = 2;
-    for (int ns = 3; ns <= 8; ++ns)
-        if ((160 * 1024) / lds(ns) >= (160 * 1024) / lds(best)) best = ns;
-    (void)ks;
-    return best;
+    // the kernel is instantiated at depths 2 and 4: 2 by default (four workgroups per CU; deeper rings
+    // measured slower), 4 when asked for a deeper one and it fits one workgroup's LDS
+    if (want > 2 && sq8_mfma_lds(u8, qb, 4) <= 160 * 1024) return 4;
+    return 2;
 }
 int sq8_mfma_ks(int u8) {
     int c = 0;
@@ -1123,8 +1191,8 @@ hipError_t launch_sq8_mfma(const Sq8Params& p, hipStream_t s, hipEvent_t ev_star
     if (p.sim < 0 || p.sim > 3) return hipErrorInvalidValue;
     auto fn = kSq8Mfma[c][qb - 1][p.sim];
     if (p.ring_slots >= 2 && !p.accept && c <= 1) {   // LDS-DMA ring (unfiltered, ≤ 256 dims)
-        if (p.ring_slots > 8) return hipErrorInvalidValue;
-        fn = kSq8MfmaRing[c][qb - 1][p.sim];
+        if (p.ring_slots != 2 && p.ring_slots != 4) return hipErrorInvalidValue;
+        fn = kSq8MfmaRing[p.ring_slots == 4][c][qb - 1][p.sim];
         lds = sq8_mfma_lds(p.units8, qb, p.ring_slots);
         if (lds > 160 * 1024) return hipErrorInvalidValue;
     }
