@@ -220,8 +220,9 @@ int32_t osk_view_scan_time(osk_view* view, double* total_ms, int64_t* calls);
  *   "tile_large_slots" views of >= CUs x this x tile_min_rows rows get CUs x this tiles (24; 0 = off)
  *   "mfma_min_batch"  batches of at least this many float32 queries (and k ≤ 12) may take the bf16×3
  *                     MFMA path (default 96; 0 = never)...
- *   "sq8_cost_pct"    ...when its 256-query blocks cost ≤ this % of the int8 prefilter's time for the
- *                     same queries (default 174, measured at C3)
+ *   "sq8_cost_pct"    ...when its 256-query blocks cost no more than the int8 prefilter's launches for
+ *                     the same queries, by a per-row cost model of both measured on MI355X with the
+ *                     prefilter's side scaled by this / 100 (default 100)
  *   "mfma_units"      workgroup units of the MFMA candidate pass per view (default 512)
  *   "sq8"             0|1 certified int8 prefilter for float32 searches with k ≤ 12 that do not take
  *                     the bf16×3 path (default 1; results are bit-identical either way)

@@ -314,9 +314,9 @@ struct Tuning {
     std::atomic<int> tile_min_rows{1024}; // ...and at least this many rows per tile (1.25M rows: 1024 tiles of 1221
                               // rows, 4360 QPS vs 3968 for 4096 tiles of 305 rows — profiles/r01e/tiles_ab.txt)
     std::atomic<int> mfma_min_batch{96};  // batches ≥ this may take the bf16×3 MFMA candidate path (0 = never)...
-    std::atomic<int> sq8_cost_pct{174};   // ...when ⌈nq/256⌉·256 ≤ nq · this / 100 (prefilter cost per 256 queries over a
-                              // bf16×3 block's: C3 20 ms vs 11.5 ms; b128 11.8k vs 6.0k QPS, b256 11.8k vs
-                              // 22.1k), else the int8 prefilter
+    std::atomic<int> sq8_cost_pct{100};   // ...when its blocks cost no more than the int8 prefilter's launches (a
+                              // per-row cost model of both, view_search_device), the prefilter's side scaled
+                              // by this / 100; else the int8 prefilter
     std::atomic<int> mfma_units{512};     // workgroup units of the MFMA candidate pass per view
     std::atomic<int> sq8{1};              // certified int8 prefilter for float32 batches below mfma_min_batch
     std::atomic<int> gather_min{0};       // ...at most one gather tile per this many accepted rows (0 = every gather

@@ -30,7 +30,7 @@ def bf16x3_from_16():
     _lib.tune("sq8_cost_pct", 100000)
     yield
     _lib.tune("mfma_min_batch", 96)
-    _lib.tune("sq8_cost_pct", 174)
+    _lib.tune("sq8_cost_pct", 100)
 
 
 def streaming(ds_or_reader, fn):
