@@ -182,6 +182,7 @@ def main():
     ap.add_argument("--only", default="C1,C2,C3,C4,C5f,C5i")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--c4-batches", default="1,1024")
+    ap.add_argument("--c2-batches", default="1,256")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE")
     ap.add_argument("--c5f-sel", default="0.01,0.1,0.5", help="C5f selectivities")
     ap.add_argument("--outlier", default="0:1,8:10,8:30,32:10", help="C3o corpora dims:scale, comma-separated")
@@ -212,10 +213,9 @@ def main():
     if "C2" in only:
         v = View(1, 1_000_000, 128, _lib.EUCLIDEAN, _lib.FLOAT32, _lib.DIST_UNIFORM01_X128)
         q = qpool(1024, 128, _lib.DIST_UNIFORM01_X128)
-        ms, km = run(v, q, 1, st * 5, wu)
-        emit("C2", v, 1, ms, km, 1_000_000 * 128 * 4)
-        ms, km = run(v, q, 256, st, wu)
-        emit("C2", v, 256, ms, km, 1_000_000 * 128 * 4)
+        for b in [int(x) for x in a.c2_batches.split(",")]:
+            ms, km = run(v, q, b, st * 5 if b == 1 else st, wu)
+            emit("C2", v, b, ms, km, 1_000_000 * 128 * 4 * ((b + 255) // 256))
         v.close()
     if "C3" in only or "C5f" in only:
         v = View(8, 1_250_000, 768, _lib.COSINE, _lib.FLOAT32, _lib.DIST_NORMALISH_UNIT)
