@@ -77,6 +77,17 @@ def pmc_traffic(rows_local: int, batch: int, prefilter: bool):
     return None, None
 
 
+READ_CEILING = os.path.join(ROOT, "profiles", "r02j", "hbm_read_ceiling.json")
+
+
+def read_ceiling():
+    """The best pure HBM read stream measured on this MI355X (tools/hbm_read.hip: 16-B non-temporal loads,
+    8 GB buffer), GB/s — the practical ceiling a streaming scan can reach, beside the 8 TB/s spec."""
+    if not os.path.exists(READ_CEILING):
+        return None
+    return max(r["TBps"] for r in json.load(open(READ_CEILING))["results"]) * 1000.0
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -389,6 +400,7 @@ def main():
                      total=np.stack([o[4] for o in outs]), max_score=np.stack([o[5] for o in outs]))
 
     traffic, traffic_src = pmc_traffic(rows_local, B, prefilter)
+    ceiling = read_ceiling()
     if rank == 0:
         res = {
             "metric": "exact k-NN QPS@k=10 (recall=1.0), 10M×768 fp32, 1/2/4/8 GPUs; % HBM roofline",
@@ -414,6 +426,9 @@ def main():
                            if a.exchange == "osk" else f"torch.distributed {a.dist_backend} all-gather + device merge"))},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                         "measured_read_ceiling_GBps": ceiling,
+                         "frac_of_measured_read_ceiling": achieved / ceiling if ceiling else None,
+                         "read_ceiling_source": os.path.relpath(READ_CEILING, ROOT) if ceiling else None,
                          "kernel": kernel_name, "scan_ms_avg": scan_avg_ms,
                          "scan_ms_measured_in": ("the one-in-flight pass of this run (isolated launches)" if F > 1
                                                  else "the timed region"),
