@@ -39,6 +39,8 @@
 #define ORDER_DEVICE 0
 #define ORDER_SCALAR 1
 #define ORDER_PANAMA512 2
+#define ORDER_SCALAR_NOFMA 3      /* Lucene's orders on a CPU without fast FMA (mul, then add) */
+#define ORDER_PANAMA512_NOFMA 4
 
 enum { SIM_EUCLIDEAN = 0, SIM_DOT_PRODUCT = 1, SIM_COSINE = 2, SIM_MIP = 3 };
 
@@ -128,9 +130,15 @@ static float device_sum(const float* a, const float* b, int dim, int kind) {
     return p[0];
 }
 
+/* [L] Lucene fuses the multiply-add only where the CPU has fast FMA (Constants.HAS_FAST_SCALAR_FMA /
+ * HAS_FAST_VECTOR_FMA); elsewhere it is a rounded multiply then an add.  `fused` selects which
+ * (ORDER_SCALAR / ORDER_PANAMA512 fuse, the *_NOFMA orders do not; -ffp-contract=off keeps a*b + c
+ * two roundings). */
+static inline float mac(float a, float b, float c, int fused) { return fused ? fmaf(a, b, c) : a * b + c; }
+
 /* [L] DefaultVectorUtilSupport: 4 fma accumulators over a 4-aligned prefix when dim > 32, summed
  * ((a1+a2)+a3)+a4 and added to 0, then a scalar fma tail. */
-static float scalar_sum(const float* a, const float* b, int dim, int kind) {
+static float scalar_sum(const float* a, const float* b, int dim, int kind, int fused) {
     float res = 0.0f;
     int i = 0;
     if (dim > 32) {
@@ -138,14 +146,14 @@ static float scalar_sum(const float* a, const float* b, int dim, int kind) {
         const int ub = dim & ~3;
         for (; i < ub; i += 4)
             for (int e = 0; e < 4; ++e) {
-                if (kind == 0) acc[e] = fmaf(a[i + e], b[i + e], acc[e]);
-                else { const float d = a[i + e] - b[i + e]; acc[e] = fmaf(d, d, acc[e]); }
+                if (kind == 0) acc[e] = mac(a[i + e], b[i + e], acc[e], fused);
+                else { const float d = a[i + e] - b[i + e]; acc[e] = mac(d, d, acc[e], fused); }
             }
         res += ((acc[0] + acc[1]) + acc[2]) + acc[3];
     }
     for (; i < dim; ++i) {
-        if (kind == 0) res = fmaf(a[i], b[i], res);
-        else { const float d = a[i] - b[i]; res = fmaf(d, d, res); }
+        if (kind == 0) res = mac(a[i], b[i], res, fused);
+        else { const float d = a[i] - b[i]; res = mac(d, d, res, fused); }
     }
     return res;
 }
@@ -153,7 +161,7 @@ static float scalar_sum(const float* a, const float* b, int dim, int kind) {
 /* [L] PanamaVectorUtilSupport with FLOAT_SPECIES of 16 lanes (AVX-512): vector body when
  * dim > 2·16, unrolled by 4 accumulators, vector tail into acc1, lane-wise (acc1+acc2)+(acc3+acc4),
  * reduceLanes(ADD) (modelled left to right), scalar fma tail. */
-static float panama_sum(const float* a, const float* b, int dim, int kind) {
+static float panama_sum(const float* a, const float* b, int dim, int kind, int fused) {
     const int S = 16;
     float res = 0.0f;
     int i = 0;
@@ -166,29 +174,30 @@ static float panama_sum(const float* a, const float* b, int dim, int kind) {
             for (int u = 0; u < 4; ++u)
                 for (int l = 0; l < S; ++l) {
                     const int ix = i + u * S + l;
-                    if (kind == 0) acc[u][l] = fmaf(a[ix], b[ix], acc[u][l]);
-                    else { const float d = a[ix] - b[ix]; acc[u][l] = fmaf(d, d, acc[u][l]); }
+                    if (kind == 0) acc[u][l] = mac(a[ix], b[ix], acc[u][l], fused);
+                    else { const float d = a[ix] - b[ix]; acc[u][l] = mac(d, d, acc[u][l], fused); }
                 }
         for (; i < limit; i += S)
             for (int l = 0; l < S; ++l) {
                 const int ix = i + l;
-                if (kind == 0) acc[0][l] = fmaf(a[ix], b[ix], acc[0][l]);
-                else { const float d = a[ix] - b[ix]; acc[0][l] = fmaf(d, d, acc[0][l]); }
+                if (kind == 0) acc[0][l] = mac(a[ix], b[ix], acc[0][l], fused);
+                else { const float d = a[ix] - b[ix]; acc[0][l] = mac(d, d, acc[0][l], fused); }
             }
         float r = 0.0f;
         for (int l = 0; l < S; ++l) r += (acc[0][l] + acc[1][l]) + (acc[2][l] + acc[3][l]);
         res += r;
     }
     for (; i < dim; ++i) {
-        if (kind == 0) res = fmaf(a[i], b[i], res);
-        else { const float d = a[i] - b[i]; res = fmaf(d, d, res); }
+        if (kind == 0) res = mac(a[i], b[i], res, fused);
+        else { const float d = a[i] - b[i]; res = mac(d, d, res, fused); }
     }
     return res;
 }
 
 static float fsum(const float* a, const float* b, int dim, int kind, int order) {
-    if (order == ORDER_SCALAR) return scalar_sum(a, b, dim, kind);
-    if (order == ORDER_PANAMA512) return panama_sum(a, b, dim, kind);
+    if (order == ORDER_SCALAR || order == ORDER_SCALAR_NOFMA) return scalar_sum(a, b, dim, kind, order == ORDER_SCALAR);
+    if (order == ORDER_PANAMA512 || order == ORDER_PANAMA512_NOFMA)
+        return panama_sum(a, b, dim, kind, order == ORDER_PANAMA512);
     return device_sum(a, b, dim, kind);
 }
 
@@ -206,15 +215,16 @@ static void cos_parts(const float* a, const float* b, int dim, int order, float*
     }
     float s = 0.0f, x = 0.0f, y = 0.0f;
     int i = 0;
-    if (order == ORDER_SCALAR) {
+    const int fused = order == ORDER_SCALAR || order == ORDER_PANAMA512;
+    if (order == ORDER_SCALAR || order == ORDER_SCALAR_NOFMA) {
         if (dim > 32) {
             float as[4] = {0}, ax[4] = {0}, ay[4] = {0};
             const int ub = dim & ~3;
             for (; i < ub; i += 4)
                 for (int e = 0; e < 4; ++e) {
-                    as[e] = fmaf(a[i + e], b[i + e], as[e]);
-                    ax[e] = fmaf(a[i + e], a[i + e], ax[e]);
-                    ay[e] = fmaf(b[i + e], b[i + e], ay[e]);
+                    as[e] = mac(a[i + e], b[i + e], as[e], fused);
+                    ax[e] = mac(a[i + e], a[i + e], ax[e], fused);
+                    ay[e] = mac(b[i + e], b[i + e], ay[e], fused);
                 }
             s += ((as[0] + as[1]) + as[2]) + as[3];
             x += ((ax[0] + ax[1]) + ax[2]) + ax[3];
@@ -231,16 +241,16 @@ static void cos_parts(const float* a, const float* b, int dim, int order, float*
                 for (int u = 0; u < 2; ++u)
                     for (int l = 0; l < S; ++l) {
                         const int ix = i + u * S + l;
-                        vs[u][l] = fmaf(a[ix], b[ix], vs[u][l]);
-                        vx[u][l] = fmaf(a[ix], a[ix], vx[u][l]);
-                        vy[u][l] = fmaf(b[ix], b[ix], vy[u][l]);
+                        vs[u][l] = mac(a[ix], b[ix], vs[u][l], fused);
+                        vx[u][l] = mac(a[ix], a[ix], vx[u][l], fused);
+                        vy[u][l] = mac(b[ix], b[ix], vy[u][l], fused);
                     }
             for (; i < limit; i += S)
                 for (int l = 0; l < S; ++l) {
                     const int ix = i + l;
-                    vs[0][l] = fmaf(a[ix], b[ix], vs[0][l]);
-                    vx[0][l] = fmaf(a[ix], a[ix], vx[0][l]);
-                    vy[0][l] = fmaf(b[ix], b[ix], vy[0][l]);
+                    vs[0][l] = mac(a[ix], b[ix], vs[0][l], fused);
+                    vx[0][l] = mac(a[ix], a[ix], vx[0][l], fused);
+                    vy[0][l] = mac(b[ix], b[ix], vy[0][l], fused);
                 }
             float rs = 0.0f, rx = 0.0f, ry = 0.0f;
             for (int l = 0; l < S; ++l) {
@@ -252,9 +262,9 @@ static void cos_parts(const float* a, const float* b, int dim, int order, float*
         }
     }
     for (; i < dim; ++i) {
-        s = fmaf(a[i], b[i], s);
-        x = fmaf(a[i], a[i], x);
-        y = fmaf(b[i], b[i], y);
+        s = mac(a[i], b[i], s, fused);
+        x = mac(a[i], a[i], x, fused);
+        y = mac(b[i], b[i], y, fused);
     }
     *sum = s; *n1 = x; *n2 = y;
 }

@@ -20,6 +20,8 @@ LIB_PATH = HERE / "liboracle.so"
 ORDER_DEVICE = 0
 ORDER_SCALAR = 1
 ORDER_PANAMA512 = 2
+ORDER_SCALAR_NOFMA = 3      # Lucene's orders where Constants.HAS_FAST_*_FMA is false: multiply, then add
+ORDER_PANAMA512_NOFMA = 4
 
 _lock = threading.Lock()
 _lib = None

@@ -210,7 +210,8 @@ def test_sparse_ord_to_doc_and_deletes():
         r.close()
 
 
-@pytest.mark.parametrize("order", [O.ORDER_PANAMA512, O.ORDER_SCALAR], ids=["panama512", "scalar"])
+@pytest.mark.parametrize("order", [O.ORDER_PANAMA512, O.ORDER_SCALAR, O.ORDER_PANAMA512_NOFMA, O.ORDER_SCALAR_NOFMA],
+                         ids=["panama512", "scalar", "panama512_nofma", "scalar_nofma"])
 @pytest.mark.parametrize("sim", SIMS, ids=lambda s: s.name)
 def test_lucene_orders_within_tolerance(order, sim):
     dim = 768

@@ -138,3 +138,21 @@ def test_cpu_baseline_driver_matches_single_thread():
     for i in range(4):
         s, d, _ = O.exact_search(rows, qs[i], 10, 2, O.ORDER_PANAMA512)
         assert np.array_equal(dc[i], d) and np.array_equal(sc[i], s)
+
+
+@pytest.mark.parametrize("sim", range(4))
+def test_nofma_orders_differ_only_by_rounding(sim):
+    """Lucene fuses multiply-adds only where the CPU has fast FMA (Constants.HAS_FAST_*_FMA): the
+    *_NOFMA orders (multiply, then add) must stay within the north star's 1e-5 of the fused ones, and
+    must actually round differently somewhere (the flag is live)."""
+    dist = {0: 1, 1: 3, 2: 3, 3: 2}[sim]
+    rows = O.synth(0, 3000, 768, 31, dist)
+    qs = O.synth(0, 4, 768, 32, dist)
+    differ = False
+    for fused, plain in ((O.ORDER_SCALAR, O.ORDER_SCALAR_NOFMA), (O.ORDER_PANAMA512, O.ORDER_PANAMA512_NOFMA)):
+        for q in qs:
+            a = np.array([O.score(q, x, sim, fused) for x in rows[:200]], np.float32)
+            b = np.array([O.score(q, x, sim, plain) for x in rows[:200]], np.float32)
+            np.testing.assert_allclose(a, b, rtol=1e-5, atol=0)
+            differ |= not np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert differ
