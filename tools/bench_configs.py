@@ -104,6 +104,8 @@ def qpool_dev(n, dim, dist):
 
 
 INFLIGHT = 1
+HOST_MS = 0.0
+HOST_ISSUE = 0.0
 
 
 def run_slots(view, queries, batch, steps, warmup, accept_ptrs, k, slots):
@@ -131,6 +133,8 @@ def run_slots(view, queries, batch, steps, warmup, accept_ptrs, k, slots):
     t0 = time.perf_counter()
     for i in range(steps):
         step(i)
+    global HOST_MS
+    HOST_MS = (time.perf_counter() - t0) / steps * 1e3   # issue time per batch (host-bound if ≈ ms per batch)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     tot, n = 0.0, 0
@@ -146,6 +150,8 @@ def run_slots(view, queries, batch, steps, warmup, accept_ptrs, k, slots):
 def run(view, queries, batch, steps, warmup, accept_ptrs=None, k=10):
     """(ms per batch with INFLIGHT queries in flight, the scan's isolated mean launch duration)."""
     ms, km = run_slots(view, queries, batch, steps, warmup, accept_ptrs, k, INFLIGHT)
+    global HOST_ISSUE
+    HOST_ISSUE = HOST_MS
     if INFLIGHT > 1:   # overlapped launches share HBM: the kernel's own duration from a one-in-flight pass
         _, km = run_slots(view, queries, batch, max(3, steps // 2), 2, accept_ptrs, k, 1)
     return ms, km
@@ -162,7 +168,7 @@ def counter(view, name):
 
 def emit(name, view, batch, ms_step, kernel_ms, bytes_per_launch, extra=None):
     rec = {"config": name, "batch": batch, "inflight": INFLIGHT, "qps": batch / (ms_step * 1e-3),
-           "ms_per_batch": ms_step,
+           "ms_per_batch": ms_step, "host_issue_ms_per_batch": HOST_ISSUE,
            "kernel_ms": kernel_ms, "fp32_equiv_GBps": bytes_per_launch / (kernel_ms * 1e-3) / 1e9,
            "rows": view.n_shards * view.rows, "dim": view.dim, "shards": view.n_shards}
     rows = view.n_shards * view.rows
