@@ -8,10 +8,18 @@
  * A Java caller maps a negative code to an IOException, which OpenSearch turns into a shard
  * failure (S/search/query/QueryPhase.java:307-309) — the library never brings the node down.
  *
- * Concurrency: calls on one view (or segment) are serialised by its mutex, and a search whose stream
- * differs from the previous search's first waits for the work already enqueued on that stream (the
- * view's workspace is reused), so a caller stream must stay valid until the next search on the view
- * has been issued, or the view released.
+ * Concurrency:
+ *   - host entries (osk_seg_search, osk_view_search, osk_shards_search_merge's per-view work): every
+ *     concurrent call leases a workspace slot of the view (the view itself, or a replica view over
+ *     the same segments, created on demand, at most 8) together with that slot's own stream, so
+ *     concurrent synchronous searches of one segment or shard set run concurrently on the device;
+ *     a call waits only when all 8 slots are busy;
+ *   - device entries (osk_view_search_device, osk_shards_search_merge_device) run on the caller's
+ *     stream with the view's own workspace: calls on one view are serialised by its mutex, and a
+ *     search whose stream differs from the previous search's first waits for the work already
+ *     enqueued on that stream, so a caller stream must stay valid until the next search on the view
+ *     has been issued, or the view released.  Callers that want device-side concurrency create one
+ *     view per search thread over the same segments (views share the segments' HBM).
  *
  * Citation convention: `S/` = /root/reference/server/src/main/java/org/opensearch/ ;
  * [L] = behaviour of the un-vendored lucene-core 10.3.0 jar (gradle/libs.versions.toml:3) whose

@@ -130,6 +130,9 @@ int64_t osk_seg::hbm_bytes() const {
 }
 
 osk_view::~osk_view() {
+    for (osk_view* r : replicas) delete r;   // (no lease is live: the caller's release contract)
+    for (hipStream_t st : lease_streams)
+        if (st) (void)hipStreamDestroy(st);
     if (xs_event) (void)hipEventDestroy(xs_event);
     for (int i = 0; i < kEvRing; ++i) {
         if (ev_start[i]) (void)hipEventDestroy(ev_start[i]);
@@ -1380,6 +1383,57 @@ int32_t select_search(osk_view* v, const void* d_queries, int nq, int k, int UP,
 
 namespace osk {
 
+// Lease a workspace slot of `root` for one synchronous host call: a free slot if there is one, else a
+// new replica (up to kMaxLeases slots), else wait for a slot to come free.
+int32_t lease_view(osk_view* root, ViewLease& out) {
+    std::unique_lock<std::mutex> lk(root->lease_mu);
+    for (;;) {
+        int slot = -1;
+        for (size_t i = 0; i < root->lease_busy.size(); ++i)
+            if (!root->lease_busy[i]) {
+                slot = (int)i;
+                break;
+            }
+        if (slot < 0 && (int)root->lease_busy.size() < osk_view::kMaxLeases) {
+            osk_view* v = root;
+            if (!root->lease_busy.empty()) {   // slots 1..: a replica over the same segments
+                std::vector<osk_seg*> segs = root->segs;
+                int32_t rc = osk_view_create(segs.data(), (int32_t)segs.size(), root->seg_shard.data(),
+                                             root->seg_doc_base.data(), root->n_shards, root->shard_index.data(), &v);
+                if (rc) return rc;
+                if (!root->holds_refs) {   // a segment's self view: its replicas must not keep it alive
+                    v->holds_refs = false;
+                    for (osk_seg* sg : segs) sg->refs.fetch_sub(1);
+                }
+                root->replicas.push_back(v);
+            }
+            hipStream_t st = nullptr;
+            OSK_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+            root->lease_streams.push_back(st);
+            root->lease_busy.push_back(0);
+            slot = (int)root->lease_busy.size() - 1;
+        }
+        if (slot >= 0) {
+            root->lease_busy[slot] = 1;
+            out.root = root;
+            out.slot = slot;
+            out.v = slot == 0 ? root : root->replicas[slot - 1];
+            out.st = root->lease_streams[slot];
+            return OSK_OK;
+        }
+        root->lease_cv.wait(lk);
+    }
+}
+
+ViewLease::~ViewLease() {
+    if (!root) return;
+    {
+        std::lock_guard<std::mutex> lk(root->lease_mu);
+        root->lease_busy[slot] = 0;
+    }
+    root->lease_cv.notify_one();
+}
+
 // Every search on a view reuses its workspace.  Calls are serialised by the view mutex on the host,
 // but a call on stream B could still overtake a call on stream A on the device, so a search whose
 // stream differs from the previous one first waits for everything enqueued on that stream so far
@@ -1596,8 +1650,13 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
     OSK_REQUIRE(v != nullptr && name != nullptr && value != nullptr, "null argument");
     int32_t rc = check_device(v->device);
     if (rc) return rc;
-    std::lock_guard<std::mutex> lk(v->mu);
     const std::string n(name);
+    if (n == "host_slots") {   // workspace slots the host entries have leased so far (1 + replicas)
+        std::lock_guard<std::mutex> lk(v->lease_mu);
+        *value = (int64_t)v->lease_busy.size();
+        return OSK_OK;
+    }
+    std::lock_guard<std::mutex> lk(v->mu);
     if (n == "mfma_calls") *value = v->mfma_calls;
     else if (n == "mfma_fallback_queries") *value = v->mfma_fallback_queries;
     else if (n == "sq8_calls") *value = v->sq8_calls;
@@ -1646,7 +1705,11 @@ int32_t osk_view_search(osk_view* v, const void* queries, int32_t n_queries, int
     OSK_REQUIRE(from >= 0 && size >= 1, "bad from/size");
     int32_t rc = check_device(v->device);
     if (rc) return rc;
-    hipStream_t st = device_stream(v->device);
+    ViewLease lease;   // a workspace slot (this view or a replica) and its stream, for this call
+    rc = lease_view(v, lease);
+    if (rc) return rc;
+    v = lease.v;
+    hipStream_t st = lease.st;
     std::lock_guard<std::mutex> lk(v->mu);
     rc = order_after_last(v, st);
     if (rc) return rc;
@@ -1740,7 +1803,11 @@ int32_t osk_seg_search(osk_seg* seg, const void* queries, int32_t n_queries, int
         v = seg->self_view;
     }
     (void)hipSetDevice(seg->device);
-    hipStream_t st = device_stream(seg->device);
+    ViewLease lease;   // a workspace slot (the self view or a replica) and its stream, for this call
+    rc = lease_view(v, lease);
+    if (rc) return rc;
+    v = lease.v;
+    hipStream_t st = lease.st;
     std::lock_guard<std::mutex> lk(v->mu);
     rc = order_after_last(v, st);
     if (rc) return rc;

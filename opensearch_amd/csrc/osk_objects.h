@@ -14,6 +14,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <atomic>
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -211,6 +212,16 @@ struct osk_view {
     // on it when a search arrives on another stream (order_after_last)
     hipStream_t last_stream = nullptr;
     hipEvent_t xs_event = nullptr;
+    // Host entries (osk_view_search, osk_seg_search) are synchronous calls from the search thread
+    // pools.  Each concurrent call leases a workspace slot — slot 0 is this view, slot i > 0 a replica
+    // view over the same segments (own workspace) — and the slot's own stream, so concurrent searches
+    // of one shard set run concurrently on the device instead of queueing on one workspace.
+    static constexpr int kMaxLeases = 8;
+    std::mutex lease_mu;
+    std::condition_variable lease_cv;
+    std::vector<osk_view*> replicas;          // slots 1.. (created on demand)
+    std::vector<hipStream_t> lease_streams;   // one per slot
+    std::vector<char> lease_busy;             // per slot
     ~osk_view();
 };
 
@@ -219,6 +230,19 @@ namespace osk {
 void seg_unref(osk_seg* s);
 // Order this call's use of the view's workspace after the previous call's (another stream).
 int32_t order_after_last(osk_view* v, hipStream_t st);
+// A leased workspace slot of a view (host entries): `v` is the view or one of its replicas, `st` the
+// slot's stream.  Released (and a waiting caller woken) when the lease goes out of scope.
+struct ViewLease {
+    osk_view* root = nullptr;
+    osk_view* v = nullptr;
+    hipStream_t st = nullptr;
+    int slot = -1;
+    ViewLease() = default;
+    ViewLease(const ViewLease&) = delete;
+    ViewLease& operator=(const ViewLease&) = delete;
+    ~ViewLease();
+};
+int32_t lease_view(osk_view* root, ViewLease& out);
 // Per-shard exact top-k on the device (caller holds v->mu; device current).
 int32_t view_search_device(osk_view* v, const void* d_queries, int nq, int k, const uint64_t* const* d_accept,
                            uint64_t* d_shard_keys, int32_t* d_shard_counts, int64_t* d_visited, hipStream_t st);

@@ -151,3 +151,46 @@ def test_warm_builds_copies_ahead_and_results_do_not_change():
     finally:
         ds.close()
         r.close()
+
+
+def test_host_entries_lease_concurrent_workspaces():
+    """Concurrent synchronous host calls on ONE view / ONE segment each lease a workspace slot (the
+    view or a replica over the same segments) with its own stream (osk_objects.h ViewLease): they run
+    concurrently on the device, more slots appear under load (≤ 8), and every result equals the
+    serial one."""
+    rows = O.synth(0, 60000, 384, 210, 3)
+    r = LU.GpuFlatVectorsReader("v", rows, COS)
+    ds = LU.DeviceShardSet([[LU.LeafReaderContext(0, 0, r)]], [0])
+    pool = O.synth(0, 32, 384, 211, 3)
+    want_v = [ds.search(pool[i:i + 1], 10, 0, 10) for i in range(32)]
+    want_s = [r.search_batch(pool[i:i + 1], 10) for i in range(32)]
+    errors, barrier = [], threading.Barrier(8)
+
+    def worker(t):
+        try:
+            barrier.wait()
+            for rep in range(40):
+                i = (t * 7 + rep) % 32
+                if (t + rep) % 2:
+                    got = ds.search(pool[i:i + 1], 10, 0, 10)
+                    if not same(got, want_v[i]):
+                        errors.append(("view", t, rep))
+                else:
+                    got = r.search_batch(pool[i:i + 1], 10)
+                    if not same(got, want_s[i]):
+                        errors.append(("seg", t, rep))
+        except Exception as e:   # noqa: BLE001
+            errors.append(repr(e))
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    try:
+        assert not errors, errors[:5]
+        slots = ds.counter("host_slots")
+        assert 1 <= slots <= 8
+    finally:
+        ds.close()
+        r.close()
