@@ -13,7 +13,10 @@
  *     concurrent call leases a workspace slot of the view (the view itself, or a replica view over
  *     the same segments, created on demand, at most 8) together with that slot's own stream, so
  *     concurrent synchronous searches of one segment or shard set run concurrently on the device;
- *     a call waits only when all 8 slots are busy;
+ *     a call waits only when all 8 slots are busy.  Concurrent unfiltered calls with the same k /
+ *     from / size are moreover batched opportunistically: while a batch runs, the calls that arrive
+ *     queue up and the next batch takes them all (≤ 32 queries, one corpus pass for all of them;
+ *     results identical to unbatched calls; tune "host_batching", "host_batch_leaders");
  *   - device entries (osk_view_search_device, osk_shards_search_merge_device) run on the caller's
  *     stream with the view's own workspace: calls on one view are serialised by its mutex, and a
  *     search whose stream differs from the previous search's first waits for the work already
@@ -237,6 +240,9 @@ int32_t osk_view_scan_time(osk_view* view, double* total_ms, int64_t* calls);
  *   "sq8_mfma_min"    prefilter batches of at least this many queries scan on int8 MFMA (sq8_mfma,
  *                     default 2; 0 = always the VALU sq8_scan)
  *   "sq8_mfma_queries"  16 | 32 queries per sq8_mfma launch (default 32)
+ *   "host_batching"   0|1 opportunistic batching of concurrent unfiltered host calls (default 1)
+ *   "host_batch_leaders"  batches of host calls in flight per view (default 1; more overlap, smaller
+ *                     batches)
  *   "sq8_mfma_nt"     0|1 non-temporal row loads in sq8_mfma (default 1)
  *   "sq8_mfma_ring"   LDS-DMA ring slots per wave in sq8_mfma for rows of ≤ 256 dims (default -1 = as many
  *                     as keep 4 workgroups per CU, 0 = register row loads)

@@ -237,6 +237,8 @@ int32_t osk_tune_set(const char* key, int64_t value) {
     struct Knob { const char* name; std::atomic<int>* v; int64_t lo, hi; bool testing; };
     const Knob knobs[] = {
         {"scan_nt", &g_tuning.scan_nt, 0, 1, false},
+        {"host_batching", &g_tuning.host_batching, 0, 1, false},
+        {"host_batch_leaders", &g_tuning.host_batch_leaders, 1, 8, false},
         {"tiles_target", &g_tuning.tiles_target, 0, 1 << 22, false},
         {"tile_slots_per_cu", &g_tuning.tile_slots_per_cu, 1, 64, false},
         {"tile_max_rounds", &g_tuning.tile_max_rounds, 1, 1024, false},
@@ -1656,6 +1658,11 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
         *value = (int64_t)v->lease_busy.size();
         return OSK_OK;
     }
+    if (n == "host_batches" || n == "host_batched_requests") {   // opportunistic batching of host calls
+        std::lock_guard<std::mutex> lk(v->batcher.mu);
+        *value = n == "host_batches" ? v->batcher.batches : v->batcher.requests;
+        return OSK_OK;
+    }
     std::lock_guard<std::mutex> lk(v->mu);
     if (n == "mfma_calls") *value = v->mfma_calls;
     else if (n == "mfma_fallback_queries") *value = v->mfma_fallback_queries;
@@ -1692,10 +1699,10 @@ int32_t osk_view_scan_time(osk_view* v, double* total_ms, int64_t* calls) {
 }
 
 // Host-buffer search + coordinator merge on one device (synchronous).
-int32_t osk_view_search(osk_view* v, const void* queries, int32_t n_queries, int32_t k, int32_t from,
-                        int32_t size, const uint64_t* const* accept, float* out_scores,
-                        int32_t* out_docs, int32_t* out_shard_index, int32_t* out_count,
-                        int64_t* out_total_hits, float* out_max_score) {
+static int32_t view_search_host(osk_view* v, const void* queries, int32_t n_queries, int32_t k, int32_t from,
+                                int32_t size, const uint64_t* const* accept, float* out_scores,
+                                int32_t* out_docs, int32_t* out_shard_index, int32_t* out_count,
+                                int64_t* out_total_hits, float* out_max_score) {
     OSK_GUARD_BEGIN
     clear_error();
     OSK_REQUIRE(v != nullptr && queries != nullptr, "null argument");
@@ -1777,10 +1784,9 @@ int32_t osk_view_search(osk_view* v, const void* queries, int32_t n_queries, int
     OSK_GUARD_END
 }
 
-// [L] KnnVectorsReader.search on one segment (host buffers, synchronous).
-int32_t osk_seg_search(osk_seg* seg, const void* queries, int32_t n_queries, int32_t k,
-                       const uint64_t* accept_bits, float* out_scores, int32_t* out_docs,
-                       int32_t* out_count, int64_t* out_visited) {
+static int32_t seg_search_host(osk_seg* seg, const void* queries, int32_t n_queries, int32_t k,
+                               const uint64_t* accept_bits, float* out_scores, int32_t* out_docs,
+                               int32_t* out_count, int64_t* out_visited) {
     OSK_GUARD_BEGIN
     clear_error();
     OSK_REQUIRE(seg != nullptr && queries != nullptr, "null argument");
@@ -1860,6 +1866,186 @@ int32_t osk_seg_search(osk_seg* seg, const void* queries, int32_t n_queries, int
         if (out_visited) out_visited[q] = visited;
     }
     return OSK_OK;
+    OSK_GUARD_END
+}
+
+// Opportunistic batching of concurrent host calls ("batches concurrent single-query
+// calls opportunistically").  A call queues its request on the view; while fewer than host_batch_leaders
+// batches are in flight, a waiting caller becomes a leader, takes the compatible requests queued so far
+// (FIFO, same k / from / size, no filter, ≤ 32 queries) and runs them as ONE batched search (the int8
+// MFMA prefilter reads the corpus once for all of them), then hands every request its rows (at most
+// host_batch_leaders batches in flight per view).  No
+// artificial delay: requests batch up only while the device is busy with earlier ones.  Results are
+// identical to unbatched calls (every path is exact).
+}  // extern "C"
+
+namespace {
+
+constexpr int kBatchMaxQueries = 32;
+
+struct BatchReq {
+    const void* queries;
+    int nq, k, from, size;
+    float* sc;
+    int32_t* docs;
+    int32_t* shard;
+    int32_t* cnt;
+    int64_t* tot;
+    float* mx;
+    int64_t* visited;
+    int32_t rc = OSK_OK;
+    std::string err;
+    bool done = false;
+};
+
+// run `fn(batch, total_queries)` as a leader whenever possible until `me` is done
+template <class Fn>
+int32_t batched_call(osk_view* root, BatchReq& me, Fn&& fn) {
+    auto& B = root->batcher;
+    std::unique_lock<std::mutex> lk(B.mu);
+    B.queue.push_back(&me);
+    while (!me.done) {
+        if (!B.queue.empty() && B.leaders < (int)g_tuning.host_batch_leaders) {
+            std::vector<BatchReq*> batch;
+            int total = 0;
+            const BatchReq* f = static_cast<const BatchReq*>(B.queue.front());
+            for (auto it = B.queue.begin(); it != B.queue.end();) {
+                BatchReq* r = static_cast<BatchReq*>(*it);
+                if (r->k == f->k && r->from == f->from && r->size == f->size && total + r->nq <= kBatchMaxQueries) {
+                    batch.push_back(r);
+                    total += r->nq;
+                    it = B.queue.erase(it);
+                } else {
+                    ++it;
+                }
+            }
+            ++B.leaders;
+            lk.unlock();
+            const int32_t rc = fn(batch, total);
+            const std::string err = rc ? std::string(osk_last_error()) : std::string();
+            lk.lock();
+            for (BatchReq* r : batch) {
+                r->rc = rc;
+                r->err = err;
+                r->done = true;
+            }
+            --B.leaders;
+            B.batches += 1;
+            B.requests += (int64_t)batch.size();
+            B.cv.notify_all();
+        } else {
+            B.cv.wait(lk);
+        }
+    }
+    if (me.rc) set_error("batched search: " + me.err);
+    return me.rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t osk_view_search(osk_view* v, const void* queries, int32_t n_queries, int32_t k, int32_t from,
+                        int32_t size, const uint64_t* const* accept, float* out_scores,
+                        int32_t* out_docs, int32_t* out_shard_index, int32_t* out_count,
+                        int64_t* out_total_hits, float* out_max_score) {
+    OSK_GUARD_BEGIN
+    clear_error();
+    OSK_REQUIRE(v != nullptr && queries != nullptr, "null argument");
+    bool any_bits = false;
+    for (int i = 0; accept && i < (int)v->segs.size(); ++i) any_bits |= accept[i] != nullptr;
+    if (any_bits || !g_tuning.host_batching || n_queries < 1 || n_queries > kBatchMaxQueries)
+        return view_search_host(v, queries, n_queries, k, from, size, accept, out_scores, out_docs, out_shard_index,
+                                out_count, out_total_hits, out_max_score);
+    BatchReq me{queries, n_queries, k, from, size, out_scores, out_docs, out_shard_index, out_count,
+                out_total_hits, out_max_score, nullptr};
+    const size_t qrow = (size_t)v->dim * (v->enc == ENC_FLOAT32 ? 4 : 1);
+    return batched_call(v, me, [&](const std::vector<BatchReq*>& batch, int total) -> int32_t {
+        if (batch.size() == 1) {
+            BatchReq* r = batch[0];
+            return view_search_host(v, r->queries, r->nq, r->k, r->from, r->size, nullptr, r->sc, r->docs, r->shard,
+                                    r->cnt, r->tot, r->mx);
+        }
+        const int sz = batch[0]->size;
+        std::vector<char> q((size_t)total * qrow);
+        std::vector<float> sc((size_t)total * sz), mx(total);
+        std::vector<int32_t> dc((size_t)total * sz), sh((size_t)total * sz), cnt(total);
+        std::vector<int64_t> tot(total);
+        int off = 0;
+        for (BatchReq* r : batch) {
+            std::memcpy(q.data() + (size_t)off * qrow, r->queries, (size_t)r->nq * qrow);
+            off += r->nq;
+        }
+        const int32_t rc = view_search_host(v, q.data(), total, batch[0]->k, batch[0]->from, sz, nullptr, sc.data(),
+                                            dc.data(), sh.data(), cnt.data(), tot.data(), mx.data());
+        if (rc) return rc;
+        off = 0;
+        for (BatchReq* r : batch) {
+            const size_t o = (size_t)off * sz, n = (size_t)r->nq * sz;
+            std::memcpy(r->sc, sc.data() + o, n * 4);
+            std::memcpy(r->docs, dc.data() + o, n * 4);
+            std::memcpy(r->shard, sh.data() + o, n * 4);
+            std::memcpy(r->cnt, cnt.data() + off, (size_t)r->nq * 4);
+            std::memcpy(r->tot, tot.data() + off, (size_t)r->nq * 8);
+            std::memcpy(r->mx, mx.data() + off, (size_t)r->nq * 4);
+            off += r->nq;
+        }
+        return OSK_OK;
+    });
+    OSK_GUARD_END
+}
+
+// [L] KnnVectorsReader.search on one segment (host buffers, synchronous).
+int32_t osk_seg_search(osk_seg* seg, const void* queries, int32_t n_queries, int32_t k,
+                       const uint64_t* accept_bits, float* out_scores, int32_t* out_docs,
+                       int32_t* out_count, int64_t* out_visited) {
+    OSK_GUARD_BEGIN
+    clear_error();
+    OSK_REQUIRE(seg != nullptr && queries != nullptr, "null argument");
+    if (accept_bits || !g_tuning.host_batching || n_queries < 1 || n_queries > kBatchMaxQueries)
+        return seg_search_host(seg, queries, n_queries, k, accept_bits, out_scores, out_docs, out_count, out_visited);
+    osk_view* root;
+    {
+        std::lock_guard<std::mutex> lk(seg->mu);
+        if (!seg->self_view) {
+            osk_seg* one[1] = {seg};
+            int32_t rc = osk_view_create(one, 1, nullptr, nullptr, 1, nullptr, &seg->self_view);
+            if (rc) return rc;
+            seg->self_view->holds_refs = false;   // owned by the segment: must not keep it alive
+            seg->refs.fetch_sub(1);
+        }
+        root = seg->self_view;
+    }
+    BatchReq me{queries, n_queries, k, 0, k, out_scores, out_docs, nullptr, out_count, nullptr, nullptr, out_visited};
+    const size_t qrow = (size_t)seg->dim * (seg->enc == ENC_FLOAT32 ? 4 : 1);
+    return batched_call(root, me, [&](const std::vector<BatchReq*>& batch, int total) -> int32_t {
+        if (batch.size() == 1) {
+            BatchReq* r = batch[0];
+            return seg_search_host(seg, r->queries, r->nq, r->k, nullptr, r->sc, r->docs, r->cnt, r->visited);
+        }
+        const int kk = batch[0]->k;
+        std::vector<char> q((size_t)total * qrow);
+        std::vector<float> sc((size_t)total * kk);
+        std::vector<int32_t> dc((size_t)total * kk), cnt(total);
+        std::vector<int64_t> vis(total);
+        int off = 0;
+        for (BatchReq* r : batch) {
+            std::memcpy(q.data() + (size_t)off * qrow, r->queries, (size_t)r->nq * qrow);
+            off += r->nq;
+        }
+        const int32_t rc = seg_search_host(seg, q.data(), total, kk, nullptr, sc.data(), dc.data(), cnt.data(), vis.data());
+        if (rc) return rc;
+        off = 0;
+        for (BatchReq* r : batch) {
+            const size_t o = (size_t)off * kk, n = (size_t)r->nq * kk;
+            std::memcpy(r->sc, sc.data() + o, n * 4);
+            std::memcpy(r->docs, dc.data() + o, n * 4);
+            std::memcpy(r->cnt, cnt.data() + off, (size_t)r->nq * 4);
+            if (r->visited) std::memcpy(r->visited, vis.data() + off, (size_t)r->nq * 8);
+            off += r->nq;
+        }
+        return OSK_OK;
+    });
     OSK_GUARD_END
 }
 

@@ -305,6 +305,8 @@ int cfg_index(int units);
 // (every path returns the same exact results).  The fields marked TESTING are settable only in the
 // testing build (libosknn_testing.so, -DOSK_TESTING): they corrupt results or trace internals.
 struct Tuning {
+    std::atomic<int> host_batching{1};       // host entries batch concurrent unfiltered calls (osk_api.hip batched_call)...
+    std::atomic<int> host_batch_leaders{1};  // ...with at most this many batches in flight per view (1: measured best)
     std::atomic<int> scan_nt{1};          // non-temporal corpus loads in scan_f32 (+4% HBM rate, profiles/r01_scan_ab.txt)
     std::atomic<int> tiles_target{0};     // workgroup tiles per view (scan grid size); 0 = whole rounds of the chip's
                               // resident slots (osk_view_create)

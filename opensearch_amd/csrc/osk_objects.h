@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <atomic>
 #include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -222,6 +223,14 @@ struct osk_view {
     std::vector<osk_view*> replicas;          // slots 1.. (created on demand)
     std::vector<hipStream_t> lease_streams;   // one per slot
     std::vector<char> lease_busy;             // per slot
+    // opportunistic batching of concurrent host calls (osk_api.hip batched_call)
+    struct Batcher {
+        std::mutex mu;
+        std::condition_variable cv;
+        std::deque<void*> queue;              // waiting requests (BatchReq*)
+        int leaders = 0;                      // batches in flight
+        int64_t batches = 0, requests = 0;
+    } batcher;
     ~osk_view();
 };
 

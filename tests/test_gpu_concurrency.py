@@ -194,3 +194,49 @@ def test_host_entries_lease_concurrent_workspaces():
     finally:
         ds.close()
         r.close()
+
+
+def test_host_calls_batch_opportunistically():
+    """Concurrent unfiltered host calls on one view are batched while the device is busy (same k /
+    from / size only): some batches carry several requests, and every caller gets
+    exactly its serial result, whatever it was batched with."""
+    rows = O.synth(0, 200000, 256, 220, 3)
+    r = LU.GpuFlatVectorsReader("v", rows, COS)
+    ds = LU.DeviceShardSet([[LU.LeafReaderContext(0, 0, r)]], [0])
+    pool = O.synth(0, 48, 256, 221, 3)
+    shapes = [(10, 0, 10), (5, 0, 5), (10, 2, 8)]
+    want = {(i, sh): ds.search(pool[i:i + 1], sh[0], sh[1], sh[2]) for i in range(48) for sh in shapes}
+    want_seg = {i: r.search_batch(pool[i:i + 2], 7) for i in range(0, 46, 2)}
+    b0, q0 = ds.counter("host_batches"), ds.counter("host_batched_requests")
+    errors, barrier = [], threading.Barrier(8)
+
+    def worker(t):
+        try:
+            barrier.wait()
+            for rep in range(60):
+                i = (t * 5 + rep * 3) % 48
+                if t == 7:   # a segment-level caller with 2 queries per call
+                    j = (i // 2) * 2
+                    if j > 44:
+                        j = 44
+                    if not same(r.search_batch(pool[j:j + 2], 7), want_seg[j]):
+                        errors.append(("seg", t, rep))
+                    continue
+                sh = shapes[(t + rep) % 3]
+                if not same(ds.search(pool[i:i + 1], sh[0], sh[1], sh[2]), want[(i, sh)]):
+                    errors.append(("view", t, rep, sh))
+        except Exception as e:   # noqa: BLE001
+            errors.append(repr(e))
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    try:
+        assert not errors, errors[:5]
+        nb, nq = ds.counter("host_batches") - b0, ds.counter("host_batched_requests") - q0
+        assert nq == 7 * 60 and nb < nq   # every view call went through the batcher; some were merged
+    finally:
+        ds.close()
+        r.close()

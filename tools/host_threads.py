@@ -31,8 +31,14 @@ def main():
     ap.add_argument("--dim", type=int, default=768)
     ap.add_argument("--threads", default="1,2,4,8")
     ap.add_argument("--calls", type=int, default=200, help="calls per thread")
+    ap.add_argument("--batching", type=int, default=1, help="osk_tune host_batching (opportunistic batching of "
+                    "concurrent calls; 0 = each call alone)")
+    ap.add_argument("--leaders", type=int, default=0, help="osk_tune host_batch_leaders (0 = library default)")
     a = ap.parse_args()
     L = lib()
+    _lib.tune("host_batching", a.batching)
+    if a.leaders:
+        _lib.tune("host_batch_leaders", a.leaders)
     segs = []
     for s in range(a.shards):
         h = C.c_void_p()
@@ -73,11 +79,15 @@ def main():
             th.join()
         dt = time.perf_counter() - t0
         assert all(c == 10 for o in outs for c in o)
-        slots = C.c_int64()
+        slots, nb, nr = C.c_int64(), C.c_int64(), C.c_int64()
         check(L.osk_view_counter(view, b"host_slots", C.byref(slots)))
+        check(L.osk_view_counter(view, b"host_batches", C.byref(nb)))
+        check(L.osk_view_counter(view, b"host_batched_requests", C.byref(nr)))
         n = T * a.calls
         print(json.dumps({"threads": T, "calls": n, "qps": n / dt, "latency_ms": dt / a.calls * 1e3,
-                          "host_slots": slots.value, "rows": a.rows_per_shard * a.shards, "dim": a.dim}), flush=True)
+                          "host_slots": slots.value, "batching": a.batching, "leaders": a.leaders,
+                          "requests_per_batch_so_far": nr.value / max(1, nb.value),
+                          "rows": a.rows_per_shard * a.shards, "dim": a.dim}), flush=True)
     L.osk_view_release(view)
     for h in segs:
         L.osk_seg_release(C.c_void_p(h))
