@@ -755,12 +755,28 @@ __global__ __launch_bounds__(kBlock, QB == 1 || (NS && KS == 2) ? 4 : (NS ? 2 : 
     const float QW = __double2float_ru((double)p.gam * (1.0 + 0x1p-18));
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb) {
-        const double r = 1.0 + 0x1p-18;
-        QY[qb] = __double2float_ru(((double)qc[qb].y + 0x1p-18 * (double)qc[qb].z) * r);
-        QZ[qb] = __double2float_ru((double)qc[qb].z * r);
-        Q0[qb] = __double2float_ru((double)p.gam * (double)qc[qb].w * r);
+        if constexpr (SIM == SIM_EUCLIDEAN) {
+            // EUCLIDEAN: a lower bound of sq8_bounds' d² lower bound (before its ·(1 − g2)), with the
+            // slack m = 2^-17 in place of its 2^-20 and |I·s_x·s_b| ≤ s_x|q_x|·(s_b|q_b| + |δ_b|):
+            //   lq = |x|²(1 − m) + Q0 − 2·I·s_x·s_b − |x|_q·QY − |δ_x|·QZ,
+            //   QY = (2 + 2m)·s_b|δ_b| + 2m·(s_b|q_b| + |δ_b|) ↑, QZ = (2 + 2m)(s_b|q_b| + |δ_b|) ↑,
+            //   Q0 = |b|²(1 − m) ↓.
+            // The extra 3·2^-20 of (|x|² + |b|² + 2|approx| + 2·eq) exceeds every rounding of both
+            // computations, so lq·(1 − g2) never exceeds the precise side: a pair the precise test
+            // passes (d² lower bound ≤ threshold) passes here.
+            const double m = 0x1p-17;
+            QY[qb] = __double2float_ru((2.0 + 2.0 * m) * (double)qc[qb].y + 2.0 * m * (double)qc[qb].z);
+            QZ[qb] = __double2float_ru((2.0 + 2.0 * m) * (double)qc[qb].z);
+            Q0[qb] = __double2float_rd((double)qc[qb].w * (1.0 - m));
+        } else {
+            const double r = 1.0 + 0x1p-18;
+            QY[qb] = __double2float_ru(((double)qc[qb].y + 0x1p-18 * (double)qc[qb].z) * r);
+            QZ[qb] = __double2float_ru((double)qc[qb].z * r);
+            Q0[qb] = __double2float_ru((double)p.gam * (double)qc[qb].w * r);
+        }
         qvm[qb] = __ballot(qv[qb]);
     }
+    const float g2m = 1.0f - p.g2;   // sq8_bounds' EUCLIDEAN factor, the same float expression
 #ifdef OSK_TESTING
     const int ablate = p.ablate;
 #else
@@ -834,13 +850,13 @@ __global__ __launch_bounds__(kBlock, QB == 1 || (NS && KS == 2) ? 4 : (NS ? 2 : 
             return;
         }
         uint64_t pm[QB][4];   // lanes whose (row i, query) pair passes the quick test (lane masks; rows
-                              // past a partial group's end may be set: insertions re-check vo)
+                              // past a partial group's end may be set: masked when folding, vo re-checked)
         uint32_t qm = 0u;     // queries with a passing lane (wave-uniform)
         // both bounds of a pair, for the rare list insertions and the pilot (the quick test reads one)
         auto bounds = [&](int qb, int i, float& lo, float& hi) {
             sq8_bounds(sim, (float)acc[qb][i], aq.row(i), qc[qb], p.gam, p.g2, lo, hi);
         };
-        if constexpr (SIM == SIM_EUCLIDEAN || QB == 1) {
+        if constexpr (QB == 1) {
             // (one query block: the register-capped 4-workgroup instances keep the precise side)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -862,6 +878,18 @@ __global__ __launch_bounds__(kBlock, QB == 1 || (NS && KS == 2) ? 4 : (NS ? 2 : 
 #pragma unroll
                 for (int qb = 0; qb < QB; ++qb) {
                     const f32x2 I2 = {(float)acc[qb][2 * h], (float)acc[qb][2 * h + 1]};
+                    if constexpr (SIM == SIM_EUCLIDEAN) {
+                        const f32x2 E = __builtin_elementwise_fma(
+                            aq.z[h], f32x2{-QZ[qb], -QZ[qb]},
+                            __builtin_elementwise_fma(aq.y[h], f32x2{-QY[qb], -QY[qb]},
+                                                      __builtin_elementwise_fma(aq.w[h], f32x2{1.0f - 0x1p-17f, 1.0f - 0x1p-17f},
+                                                                                f32x2{Q0[qb], Q0[qb]})));
+                        const f32x2 lq = __builtin_elementwise_fma(I2, aq.x[h] * f32x2{-2.0f * qc[qb].x, -2.0f * qc[qb].x}, E) *
+                                         f32x2{g2m, g2m};
+                        pm[qb][2 * h] = __ballot(!(lq.x > tq[qb]));
+                        pm[qb][2 * h + 1] = __ballot(!(lq.y > tq[qb]));
+                        continue;
+                    }
                     const f32x2 E = __builtin_elementwise_fma(
                         aq.y[h], f32x2{QY[qb], QY[qb]},
                         __builtin_elementwise_fma(aq.z[h], f32x2{QZ[qb], QZ[qb]},
@@ -874,9 +902,15 @@ __global__ __launch_bounds__(kBlock, QB == 1 || (NS && KS == 2) ? 4 : (NS ? 2 : 
             }
         }
         if (!pilot) {
+            // rows past a partial group's end hold stale slot data: mask them here, or every wave's
+            // last group would run the insertion loop for every query (C2: +0.08 ms per launch)
+            uint64_t vm[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) vm[i] = __ballot(vo[i]);
 #pragma unroll
             for (int qb = 0; qb < QB; ++qb) {
-                const uint64_t bl = (pm[qb][0] | pm[qb][1] | pm[qb][2] | pm[qb][3]) & qvm[qb];
+                const uint64_t bl =
+                    ((pm[qb][0] & vm[0]) | (pm[qb][1] & vm[1]) | (pm[qb][2] & vm[2]) | (pm[qb][3] & vm[3])) & qvm[qb];
                 qm |= (uint32_t)((bl | (bl >> 16) | (bl >> 32) | (bl >> 48)) & 0xFFFFull) << (16 * qb);
             }
         }

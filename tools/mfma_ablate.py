@@ -13,11 +13,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from opensearch_amd import _lib, distributed as D  # noqa: E402
 from opensearch_amd._lib import check, lib  # noqa: E402
 
-# argv: [C3|C4] [batch]  (C3: 8 × 1.25M × 768 COSINE; C4: 8 × 12.5M × 96 DOT_PRODUCT)
+# argv: [C3|C4|C2] [batch]  (C3: 8 × 1.25M × 768 COSINE; C4: 8 × 12.5M × 96 DOT_PRODUCT; C2: 8 × 125k × 128 L2)
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C3"
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 K = 10
-RPS, DIM, SIM = (1_250_000, 768, _lib.COSINE) if cfg == "C3" else (12_500_000, 96, _lib.DOT_PRODUCT)
+RPS, DIM, SIM = {"C3": (1_250_000, 768, _lib.COSINE), "C4": (12_500_000, 96, _lib.DOT_PRODUCT),
+                 "C2": (125_000, 128, _lib.EUCLIDEAN)}[cfg]
 # TUNE="key=value,..." sets library knobs (osk_tune_set) before staging
 for kv in filter(None, os.environ.get("TUNE", "").split(",")):
     _lib.tune(kv.split("=")[0], int(kv.split("=")[1]))
