@@ -1397,20 +1397,23 @@ int32_t lease_view(osk_view* root, ViewLease& out) {
                 break;
             }
         if (slot < 0 && (int)root->lease_busy.size() < osk_view::kMaxLeases) {
-            osk_view* v = root;
+            hipStream_t st = nullptr;
+            OSK_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
             if (!root->lease_busy.empty()) {   // slots 1..: a replica over the same segments
                 std::vector<osk_seg*> segs = root->segs;
+                osk_view* v = nullptr;
                 int32_t rc = osk_view_create(segs.data(), (int32_t)segs.size(), root->seg_shard.data(),
                                              root->seg_doc_base.data(), root->n_shards, root->shard_index.data(), &v);
-                if (rc) return rc;
+                if (rc) {
+                    (void)hipStreamDestroy(st);
+                    return rc;
+                }
                 if (!root->holds_refs) {   // a segment's self view: its replicas must not keep it alive
                     v->holds_refs = false;
                     for (osk_seg* sg : segs) sg->refs.fetch_sub(1);
                 }
                 root->replicas.push_back(v);
             }
-            hipStream_t st = nullptr;
-            OSK_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
             root->lease_streams.push_back(st);
             root->lease_busy.push_back(0);
             slot = (int)root->lease_busy.size() - 1;
@@ -1921,7 +1924,16 @@ int32_t batched_call(osk_view* root, BatchReq& me, Fn&& fn) {
             }
             ++B.leaders;
             lk.unlock();
-            const int32_t rc = fn(batch, total);
+            int32_t rc;
+            try {   // the batch's requests must always be completed, whatever happens
+                rc = fn(batch, total);
+            } catch (const std::bad_alloc&) {
+                set_error("host allocation failed");
+                rc = OSK_ERR_OOM;
+            } catch (...) {
+                set_error("batched search failed");
+                rc = OSK_ERR_INVALID;
+            }
             const std::string err = rc ? std::string(osk_last_error()) : std::string();
             lk.lock();
             for (BatchReq* r : batch) {
