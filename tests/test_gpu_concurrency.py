@@ -240,3 +240,43 @@ def test_host_calls_batch_opportunistically():
     finally:
         ds.close()
         r.close()
+
+
+def test_batched_host_call_errors_stay_with_their_caller():
+    """A request that fails (here k = 0) fails alone: the batcher groups by (k, from, size), so the
+    valid concurrent calls still get their exact results, and the failing caller gets the error code
+    and its own message."""
+    rows = O.synth(0, 50000, 128, 230, 3)
+    r = LU.GpuFlatVectorsReader("v", rows, COS)
+    ds = LU.DeviceShardSet([[LU.LeafReaderContext(0, 0, r)]], [0])
+    pool = O.synth(0, 16, 128, 231, 3)
+    want = [ds.search(pool[i:i + 1], 10, 0, 10) for i in range(16)]
+    results, barrier = {}, threading.Barrier(6)
+
+    def worker(t):
+        barrier.wait()
+        for rep in range(20):
+            i = (t + rep) % 16
+            try:
+                if t == 0:
+                    ds.search(pool[i:i + 1], 0, 0, 10)
+                    results[(t, rep)] = "no error"
+                else:
+                    results[(t, rep)] = same(ds.search(pool[i:i + 1], 10, 0, 10), want[i])
+            except _lib.OskError as e:
+                results[(t, rep)] = ("error", str(e))
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(6)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    try:
+        for (t, rep), v in results.items():
+            if t == 0:
+                assert isinstance(v, tuple) and v[0] == "error" and "k must be" in v[1], v
+            else:
+                assert v is True, (t, rep, v)
+    finally:
+        ds.close()
+        r.close()
