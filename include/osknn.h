@@ -266,7 +266,8 @@ int32_t osk_view_stats(osk_view* view, int64_t* batched_calls, int64_t* fallback
  * "sq8_calls" (prefiltered searches), "sq8_fallback_queries" (queries where some tile's candidate
  * list overflowed past the certificate and the tile was re-scanned exactly), "sq8_exact_tiles"
  * (such tiles), "sq8_rescored_rows" (rows re-scored exactly, all calls), "select_calls" (searches
- * on the select path, k > 12). */
+ * on the select path, k > 12), "host_slots" (workspace slots the host entries have leased: 1 + replicas),
+ * "host_batches" / "host_batched_requests" (opportunistic batching of concurrent host calls). */
 int32_t osk_view_counter(osk_view* view, const char* name, int64_t* value);
 /* Testing build only (the shipped library returns OSK_ERR_UNSUPPORTED): copy `bytes` of an internal
  * buffer of the view's last search ("akeys", "cand_a", "flags", "qsplit", "qnorm", "sq8cand", "sq8lb",
