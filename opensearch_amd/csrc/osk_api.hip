@@ -543,7 +543,7 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
     const int R = 64 / kL[v->cfg];
     int64_t total = 0;
     for (int i = 0; i < n_segs; ++i) total += segs[i]->n_rows;
-    const int64_t min_rows = std::max<int64_t>(4LL * R * 8, (int)g_tuning.tile_min_rows);
+    int64_t min_rows = std::max<int64_t>(4LL * R * 8, (int)g_tuning.tile_min_rows);
     int64_t target = g_tuning.tiles_target;
     if (target <= 0) {
         int cus = 0;
@@ -560,6 +560,10 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
         // 7.2 -> 6.5 ms, C3 b1 within 1%).
         const int64_t large = (int64_t)cus * g_tuning.tile_large_slots;
         if (g_tuning.tile_large_slots > 0 && total >= large * min_rows) target = large;
+        // views smaller than one round at tile_min_rows (C1: 100k rows): latency-bound, so spread them
+        // over more of the chip with tiles down to 8 row groups per wave (≥ 256 rows): C1's scan
+        // 34 -> 16 µs (profiles/r02o/tile_min_rows.txt); a full round is unaffected (C2: 1024 tiles)
+        if (total < slots * min_rows) min_rows = std::max<int64_t>(4LL * R * 8, 256);
     }
     // split the target over segments in proportion to their rows (largest remainder), each segment's
     // share capped so its tiles keep ≥ min_rows rows
