@@ -185,6 +185,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_bounds(SelParams p) {
         bool in[U], valid[U];
         int4 xv[U][V];
         float4 ax[U];
+        uint32_t lbv[U], ubv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             row[u] = r0 + u * R + g;
@@ -230,10 +231,27 @@ __global__ __launch_bounds__(kSelThreads) void sel_bounds(SelParams p) {
                 lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qnd, xnd);
             }
             nvis += __popcll(__ballot(t == 0 && valid[u]));
-            if (in[u] && t == 0) {   // every real score is ≥ 0, whose sortable form is ≥ 2^31: 0 = no row
-                p.lb[vbase + row[u]] = valid[u] ? float_to_sortable(lb) : 0u;
-                p.ub[vbase + row[u]] = valid[u] ? float_to_sortable(ub) : 0u;
+            // every real score is ≥ 0, whose sortable form is ≥ 2^31: 0 = no row
+            lbv[u] = valid[u] ? float_to_sortable(lb) : 0u;
+            ubv[u] = valid[u] ? float_to_sortable(ub) : 0u;
+        }
+        // the iteration's U·R rows are contiguous (r0 + u·R + g): lane j < U·R gathers row r0 + j's values
+        // from the lane holding them (t = 0 of group g = j mod R) and the wave stores them as one
+        // contiguous run per array (one store instruction each instead of U partial ones)
+        const int j = lane;
+        const int src = (j % R) * L;
+        uint32_t lbo = 0u, ubo = 0u;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t a = (uint32_t)__shfl((int)lbv[u], src), b = (uint32_t)__shfl((int)ubv[u], src);
+            if (j / R == u) {
+                lbo = a;
+                ubo = b;
             }
+        }
+        if (j < U * R && r0 + j < we) {
+            p.lb[vbase + r0 + j] = lbo;
+            p.ub[vbase + r0 + j] = ubo;
         }
     }
     if (p.visited && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
