@@ -270,7 +270,10 @@ int32_t osk_comm_init_rank(int32_t device, int32_t rank, int32_t world, const ui
     std::memcpy(&u, id, sizeof(u));
     OSK_NCCL(R->CommInitRank(&c->comms[0], world, u, rank));
     rc = make_xstreams(c.get());
-    if (rc) return rc;
+    if (rc) {
+        (void)R->CommDestroy(c->comms[0]);
+        return rc;
+    }
     *out = c.release();
     return OSK_OK;
     OSK_GUARD_END
@@ -295,7 +298,13 @@ int32_t osk_comm_init_all(const int32_t* devices, int32_t n, osk_comm** out) {
     c->comms.assign(n, nullptr);
     OSK_NCCL(R->CommInitAll(c->comms.data(), n, devices));
     int32_t rc = make_xstreams(c.get());
-    if (rc) return rc;
+    if (rc) {
+        for (int i = 0; i < n; ++i) {
+            (void)hipSetDevice(devices[i]);
+            (void)R->CommDestroy(c->comms[i]);
+        }
+        return rc;
+    }
     *out = c.release();
     return OSK_OK;
     OSK_GUARD_END
