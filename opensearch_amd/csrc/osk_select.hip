@@ -87,7 +87,10 @@ __global__ __launch_bounds__(kSelThreads) void sel_keys_f32(SelParams p) {
     if (p.visited && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
 }
 
-template <int L, int V>
+// Byte vectors, exact keys: byte-unit lane configs (L lanes × V 16-B units ≥ the row's units, sq8_scan's),
+// U row groups loaded (unconditional, clamped, masked) before any is reduced, and each iteration's U·R
+// contiguous rows' keys stored by one instruction (lane j ← row r0 + j).
+template <int L, int V, int U>
 __global__ __launch_bounds__(kSelThreads) void sel_keys_i8(SelParams p) {
     constexpr int R = 64 / L;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform: scalar loop control
@@ -96,11 +99,15 @@ __global__ __launch_bounds__(kSelThreads) void sel_keys_i8(SelParams p) {
     const SegDev seg = p.segs[tile.seg];
     const uint64_t* abits = p.accept ? p.accept[tile.seg] : nullptr;
     const int4* __restrict__ Q = static_cast<const int4*>(p.q);
+    const int units = p.units;
     int4 qf[V];
     int qn = 0;   // Σq², exact (scan_i8's)
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-        qf[j] = Q[t + j * L];
+        const int f = t + j * L;
+        const int m = f < units ? -1 : 0;
+        const int4 v = Q[f < units ? f : 0];
+        qf[j] = make_int4(v.x & m, v.y & m, v.z & m, v.w & m);
         qn = __builtin_amdgcn_sdot4(qf[j].x, qf[j].x, qn, false);
         qn = __builtin_amdgcn_sdot4(qf[j].y, qf[j].y, qn, false);
         qn = __builtin_amdgcn_sdot4(qf[j].z, qf[j].z, qn, false);
@@ -113,29 +120,55 @@ __global__ __launch_bounds__(kSelThreads) void sel_keys_i8(SelParams p) {
     int64_t wb, we;
     wave_rows<R>(tile, wave, wb, we);
     uint32_t nvis = 0;
-    for (int64_t r0 = wb; r0 < we; r0 += R) {
-        const int64_t row = r0 + g;
-        const bool in = row < we;
-        int32_t doc = 0;
-        const bool valid = in && row_accepted(abits, seg, row, doc);
-        const int4* xr = X + (in ? row : 0) * p.units;
-        int acc = 0;
+    for (int64_t r0 = wb; r0 < we; r0 += R * U) {
+        int4 xv[U][V];
+        int32_t xn[U], doc[U];
+        bool valid[U];
 #pragma unroll
-        for (int j = 0; j < V; ++j) {
-            const int f = t + j * L;
-            const int4 x = (valid && f < p.units) ? xr[f] : make_int4(0, 0, 0, 0);
-            acc = __builtin_amdgcn_sdot4(x.x, qf[j].x, acc, false);
-            acc = __builtin_amdgcn_sdot4(x.y, qf[j].y, acc, false);
-            acc = __builtin_amdgcn_sdot4(x.z, qf[j].z, acc, false);
-            acc = __builtin_amdgcn_sdot4(x.w, qf[j].w, acc, false);
+        for (int u = 0; u < U; ++u) {
+            const int64_t row = r0 + u * R + g;
+            const bool in = row < we;
+            doc[u] = 0;
+            valid[u] = in && row_accepted(abits, seg, row, doc[u]);
+            const int64_t rc = in ? row : wb;
+            const int4* xr = X + rc * units;
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                const int f = t + j * L;
+                const int4 x = load_i4_nt(xr + (f < units ? f : 0));
+                const int m = (valid[u] && f < units) ? -1 : 0;
+                xv[u][j] = make_int4(x.x & m, x.y & m, x.z & m, x.w & m);
+            }
+            xn[u] = seg.xnorm_i[rc];
         }
+        uint64_t kv[U];
 #pragma unroll
-        for (int m = 1; m < L; m <<= 1) acc += __shfl_xor(acc, m);
-        const int32_t xn = valid ? seg.xnorm_i[row] : 0;
-        const int32_t s = p.sim == SIM_EUCLIDEAN ? qn + xn - 2 * acc : acc;
-        const float sc = score_i8(p.sim, s, qn, xn, p.dim);
-        nvis += __popcll(__ballot(t == 0 && valid));
-        if (in && t == 0) p.keys[vbase + row] = valid ? make_key(sc, (uint32_t)(seg.doc_base + doc)) : 0ull;
+        for (int u = 0; u < U; ++u) {
+            int acc = 0;
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                acc = __builtin_amdgcn_sdot4(xv[u][j].x, qf[j].x, acc, false);
+                acc = __builtin_amdgcn_sdot4(xv[u][j].y, qf[j].y, acc, false);
+                acc = __builtin_amdgcn_sdot4(xv[u][j].z, qf[j].z, acc, false);
+                acc = __builtin_amdgcn_sdot4(xv[u][j].w, qf[j].w, acc, false);
+            }
+#pragma unroll
+            for (int m = 1; m < L; m <<= 1) acc += __shfl_xor(acc, m);
+            const int32_t x2 = valid[u] ? xn[u] : 0;
+            const int32_t sv = p.sim == SIM_EUCLIDEAN ? qn + x2 - 2 * acc : acc;
+            const float sc = score_i8(p.sim, sv, qn, x2, p.dim);
+            nvis += __popcll(__ballot(t == 0 && valid[u]));
+            kv[u] = valid[u] ? make_key(sc, (uint32_t)(seg.doc_base + doc[u])) : 0ull;
+        }
+        const int src = (lane % R) * L;
+        uint64_t ko = 0ull;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)kv[u], src);
+            const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(kv[u] >> 32), src);
+            if (lane / R == u) ko = ((uint64_t)hi << 32) | lo;
+        }
+        if (lane < U * R && r0 + lane < we) p.keys[vbase + r0 + lane] = ko;
     }
     if (p.visited && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
 }
@@ -743,9 +776,10 @@ using SelFn = void (*)(SelParams);
 static const SelFn kSelKeysF32[9][2] = {OSK_SEL_F32(4, 2),  OSK_SEL_F32(8, 2),  OSK_SEL_F32(8, 4),
                                         OSK_SEL_F32(16, 4), OSK_SEL_F32(16, 8), OSK_SEL_F32(16, 12),
                                         OSK_SEL_F32(32, 8), OSK_SEL_F32(64, 8), OSK_SEL_F32(64, 16)};
-static const SelFn kSelKeysI8[9] = {sel_keys_i8<4, 2>,  sel_keys_i8<8, 2>,  sel_keys_i8<8, 4>,
-                                    sel_keys_i8<16, 4>, sel_keys_i8<16, 8>, sel_keys_i8<16, 12>,
-                                    sel_keys_i8<32, 8>, sel_keys_i8<64, 8>, sel_keys_i8<64, 16>};
+// byte-unit configs (sel_bounds_cfg of the row's 16-B units), 4 row groups per iteration
+static const SelFn kSelKeysI8[8] = {sel_keys_i8<4, 1, 4>,  sel_keys_i8<8, 1, 4>,  sel_keys_i8<16, 1, 4>,
+                                    sel_keys_i8<16, 2, 4>, sel_keys_i8<16, 3, 4>, sel_keys_i8<16, 4, 4>,
+                                    sel_keys_i8<32, 4, 4>, sel_keys_i8<64, 4, 4>};
 #define OSK_SEL_RS(L, V) {sel_rescore<L, V, false>, sel_rescore<L, V, true>}
 static const SelFn kSelRescore[9][2] = {OSK_SEL_RS(4, 2),  OSK_SEL_RS(8, 2),  OSK_SEL_RS(8, 4),
                                         OSK_SEL_RS(16, 4), OSK_SEL_RS(16, 8), OSK_SEL_RS(16, 12),
@@ -770,7 +804,8 @@ hipError_t launch_select_one(const SelParams& p, int cfg, hipStream_t s, hipEven
     const dim3 tg(p.n_tiles), tb(kSelThreads);
     hipLaunchKernelGGL(sel_init, dim3(p.n_shards * kSelRep), dim3(256), 0, s, p);
     // the writer (stamped by the profile events when given)
-    SelFn writer = p.exact ? (p.enc == ENC_BYTE ? kSelKeysI8[cfg] : kSelKeysF32[cfg][p.sim == SIM_EUCLIDEAN ? 1 : 0])
+    SelFn writer = p.exact ? (p.enc == ENC_BYTE ? kSelKeysI8[sel_bounds_cfg(p.units)]
+                                                : kSelKeysF32[cfg][p.sim == SIM_EUCLIDEAN ? 1 : 0])
                            : kSelBounds[sel_bounds_cfg(p.units8)][p.writer & 3][p.accept ? 1 : 0];
     if (ev_start || ev_stop)
         hipExtLaunchKernelGGL(writer, tg, tb, 0, s, ev_start, ev_stop, 0, p);

@@ -189,6 +189,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--c4-batches", default="1,1024")
     ap.add_argument("--c2-batches", default="1,256")
+    ap.add_argument("--c5i-k", default="10", help="C5i k values (k > 12: the select path's exact mode)")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE")
     ap.add_argument("--c5f-sel", default="0.01,0.1,0.5", help="C5f selectivities")
     ap.add_argument("--outlier", default="0:1,8:10,8:30,32:10", help="C3o corpora dims:scale, comma-separated")
@@ -284,8 +285,9 @@ def main():
     if "C5i" in only:
         v = View(8, 1_250_000, 768, _lib.EUCLIDEAN, _lib.BYTE, _lib.DIST_INT8)
         q = torch.from_numpy(synth_host(0, 64, 768, 43, _lib.DIST_INT8)).cuda()
-        ms, km = run(v, q, 1, st, wu)
-        emit("C5i", v, 1, ms, km, 10_000_000 * 768)
+        for kk in [int(x) for x in a.c5i_k.split(",")]:
+            ms, km = run(v, q, 1, st, wu, k=kk)
+            emit("C5i", v, 1, ms, km, 10_000_000 * 768, {"k": kk})
         v.close()
 
 
