@@ -166,3 +166,28 @@ def test_batched_multi_shard_filters_sparse():
         for leaves in shard_leaves:
             for lf in leaves:
                 lf.reader.close()
+
+
+@pytest.mark.parametrize("offset", [0.0, 1000.0, -3.0e4])
+def test_batched_euclidean_threshold_bound_magnitudes(offset):
+    """EUCLIDEAN's candidate pass filters accumulators with a dot-product bound derived from the
+    running threshold (2d ≥ |x|² + |q|² − (1/t − 1), loosened).  Large |x|² (offset rows), scores near
+    1 (queries that are perturbed rows) and far-away queries must all keep every true candidate: the
+    batched answers equal the streaming scan's and the oracle's, and the certificate holds."""
+    sim = LU.VectorSimilarityFunction.EUCLIDEAN
+    dim = 128
+    rows = corpus(40000, dim, sim, 31) + np.float32(offset)
+    rng = np.random.default_rng(5)
+    near = rows[rng.choice(len(rows), 24, replace=False)] + rng.normal(0, 0.05, (24, dim)).astype(np.float32)
+    far = corpus(24, dim, sim, 32) + np.float32(offset)
+    queries = np.ascontiguousarray(np.concatenate([near, far]), np.float32)
+    r = LU.GpuFlatVectorsReader("v", rows, sim)
+    try:
+        s, d, c, v = r.search_batch(queries, 10)
+        s2, d2, c2, v2 = streaming(r, lambda: r.search_batch(queries, 10))
+        assert np.array_equal(d, d2) and np.array_equal(bits(s), bits(s2))
+        for i in [0, 11, 23, 24, 47]:
+            os_, od, _ = O.exact_search(rows, queries[i], 10, int(sim))
+            assert np.array_equal(d[i], od) and np.array_equal(bits(s[i]), bits(os_))
+    finally:
+        r.close()
