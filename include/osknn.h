@@ -234,7 +234,8 @@ int32_t osk_view_scan_time(osk_view* view, double* total_ms, int64_t* calls);
  *   "sq8_cost_pct"    ...when its 256-query blocks cost no more than the int8 prefilter's launches for
  *                     the same queries, by a per-row cost model of both measured on MI355X with the
  *                     prefilter's side scaled by this / 100 (default 100)
- *   "mfma_units"      workgroup units of the MFMA candidate pass per view (default 512)
+ *   "mfma_units"      workgroup units of the MFMA candidate pass per view (default 0: 256 below
+ *                     16384 tiles of 128 rows, else 512)
  *   "sq8"             0|1 certified int8 prefilter for float32 searches with k ≤ 12 that do not take
  *                     the bf16×3 path (default 1; results are bit-identical either way)
  *   "sq8_mfma_min"    prefilter batches of at least this many queries scan on int8 MFMA (sq8_mfma,

@@ -246,7 +246,7 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         {"tile_min_rows", &g_tuning.tile_min_rows, 1, 1 << 24, false},
         {"mfma_min_batch", &g_tuning.mfma_min_batch, 0, 1 << 30, false},
         {"sq8_cost_pct", &g_tuning.sq8_cost_pct, 0, 100000, false},
-        {"mfma_units", &g_tuning.mfma_units, 1, 32768, false},
+        {"mfma_units", &g_tuning.mfma_units, 0, 32768, false},
         {"sq8", &g_tuning.sq8, 0, 1, false},
         {"filter_gather", &g_tuning.filter_gather, 0, 1, false},
         {"select_mid_k", &g_tuning.select_mid_k, 0, 1, false},
@@ -822,7 +822,10 @@ int32_t ensure_mfma(osk_view* v, hipStream_t st) {
         const std::vector<SegDev> sd = seg_devs(v);
         OSK_HIP(hipMemcpyAsync(v->d_segs.p, sd.data(), sizeof(SegDev) * sd.size(), hipMemcpyHostToDevice, st));
     }
-    const int64_t target = std::max(1, (int)g_tuning.mfma_units);
+    // auto: one workgroup per CU (1 per CU fits: 255 VGPRs, 143 KiB LDS) in 1 round below 16k tiles
+    // (C2 b256: 0.74 → 0.65 ms, fewer pilot tiles), else 2 rounds (C3 b256: 11.6 ms against 11.7;
+    // 384 units, 1.5 rounds, lose 30 %; profiles/r02q/mfma_units.txt)
+    const int64_t target = g_tuning.mfma_units > 0 ? (int64_t)g_tuning.mfma_units : (total_tiles < 16384 ? 256 : 512);
     const int64_t per = std::max<int64_t>(1, (total_tiles + target - 1) / target);
     std::vector<MfmaUnit> units;
     std::vector<int32_t> shard_list_begin(v->n_shards + 1, 0);

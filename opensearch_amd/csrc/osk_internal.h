@@ -319,7 +319,7 @@ struct Tuning {
     std::atomic<int> sq8_cost_pct{100};   // ...when its blocks cost no more than the int8 prefilter's launches (a
                               // per-row cost model of both, view_search_device), the prefilter's side scaled
                               // by this / 100; else the int8 prefilter
-    std::atomic<int> mfma_units{512};     // workgroup units of the MFMA candidate pass per view
+    std::atomic<int> mfma_units{0};       // workgroup units of the MFMA candidate pass per view (0: auto)
     std::atomic<int> sq8{1};              // certified int8 prefilter for float32 batches below mfma_min_batch
     std::atomic<int> gather_min{0};       // ...at most one gather tile per this many accepted rows (0 = every gather
                                           // tile; fewer, longer tiles were slower: profiles/r02c/gather_min_ab.jsonl)
