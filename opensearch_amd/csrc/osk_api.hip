@@ -1485,18 +1485,20 @@ int32_t view_search_device(osk_view* v, const void* d_queries, int nq, int k,
     OSK_HIP(v->ws_cand.reserve(sizeof(uint64_t) * (size_t)nq * v->n_tiles * k));
     OSK_HIP(v->ws_q.reserve((size_t)nq_pad * UP * 16));
     OSK_HIP(v->ws_qnorm.reserve(sizeof(float) * nq_pad));
-    // Path cost model, measured on MI355X, in µs for this view's rows R:
+    // Path cost model, measured end to end on MI355X, in µs for this view's rows R:
     //   int8 prefilter, per launch of ≤ 32 queries: R·(int8 row + 16-B bound terms) at ≈ 4.3 TB/s + ≈ 165 µs
-    //     (pilot, pilot merge, settle: C3 1.82 ms, C4 2.67 ms, C2 0.20 ms per launch);
-    //   bf16×3, per block of ≤ 256 queries: R·(0.144 + 0.00132·dim) ns + ≈ 480 µs (C3 11.6, C4 27.1, C2 0.79 ms).
-    // 96-dim rows stay on the prefilter at any batch, 768-dim rows move to bf16×3 blocks from about 200
+    //     + 0.28 µs per dim (pilot, pilot merge, settle and re-score: C3 2.2 ms, C4 2.7 ms, C2 0.20 ms per launch);
+    //   bf16×3, per block of ≤ 256 queries: R·(0.153 + 0.00119·dim) ns + ≈ 325 µs (C3 11.0, C4 27.1, C2 0.63 ms;
+    //     fitted to those three, profiles/r02q/c2_batches_*.jsonl, c3_batches_*.jsonl).
+    // 96-dim rows stay on the prefilter at any batch, 768-dim rows move to bf16×3 blocks from about 160
     // queries, and small views (C2) from about 128.  sq8_cost_pct scales the prefilter's side (100 = the model).
     const bool sq8_on = v->enc == ENC_FLOAT32 && g_tuning.sq8;
     const bool sq8_ok = sq8_on && k <= kKQ - 4;
     double R = 0.0;
     for (const osk_seg* sg : v->segs) R += (double)sg->n_rows;
-    const double sq8_us = (double)((nq + 31) / 32) * (R * (16.0 * ((v->dim + 15) / 16) + 16.0) / 4.3e6 + 165.0);
-    const double bf_us = (double)((nq + 255) / 256) * (R * (0.144 + 0.00132 * v->dim) * 1e-3 + 480.0);
+    const double sq8_us =
+        (double)((nq + 31) / 32) * (R * (16.0 * ((v->dim + 15) / 16) + 16.0) / 4.3e6 + 165.0 + 0.28 * v->dim);
+    const double bf_us = (double)((nq + 255) / 256) * (R * (0.153 + 0.00119 * v->dim) * 1e-3 + 325.0);
     const bool blocks_cheaper = bf_us * 100.0 <= sq8_us * (double)g_tuning.sq8_cost_pct;
     const bool batched = v->enc == ENC_FLOAT32 && g_tuning.mfma_min_batch > 0 &&
                          nq >= g_tuning.mfma_min_batch && k <= kKC - 4 && (!sq8_ok || blocks_cheaper);

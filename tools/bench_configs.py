@@ -189,6 +189,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--c4-batches", default="1,1024")
     ap.add_argument("--c2-batches", default="1,256")
+    ap.add_argument("--c3-batches", default="1,256")
     ap.add_argument("--c5i-k", default="10", help="C5i k values (k > 12: the select path's exact mode)")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE")
     ap.add_argument("--c5f-sel", default="0.01,0.1,0.5", help="C5f selectivities")
@@ -228,10 +229,9 @@ def main():
         v = View(8, 1_250_000, 768, _lib.COSINE, _lib.FLOAT32, _lib.DIST_NORMALISH_UNIT)
         q = qpool(512, 768, _lib.DIST_NORMALISH_UNIT)
         if "C3" in only:
-            ms, km = run(v, q, 1, st, wu)
-            emit("C3", v, 1, ms, km, 10_000_000 * 768 * 4)
-            ms, km = run(v, q, 256, st, wu)
-            emit("C3", v, 256, ms, km, 10_000_000 * 768 * 4)
+            for b in [int(x) for x in a.c3_batches.split(",")]:
+                ms, km = run(v, q, b, st, wu)
+                emit("C3", v, b, ms, km, 10_000_000 * 768 * 4)
         if "C5f" in only:
             rng = np.random.default_rng(44)
             for sel in [float(x) for x in a.c5f_sel.split(",")]:
