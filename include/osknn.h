@@ -9,11 +9,12 @@
  * failure (S/search/query/QueryPhase.java:307-309) — the library never brings the node down.
  *
  * Concurrency:
- *   - host entries (osk_seg_search, osk_view_search, osk_shards_search_merge's per-view work): every
- *     concurrent call leases a workspace slot of the view (the view itself, or a replica view over
- *     the same segments, created on demand, at most 8) together with that slot's own stream, so
- *     concurrent synchronous searches of one segment or shard set run concurrently on the device;
- *     a call waits only when all 8 slots are busy.  Concurrent unfiltered calls with the same k /
+ *   - host entries (osk_seg_search, osk_view_search): every concurrent call leases a workspace slot of
+ *     the view (the view itself, or a replica view over the same segments, created on demand, at most
+ *     8) together with that slot's own stream, so concurrent synchronous searches of one segment or
+ *     shard set run concurrently on the device; a call waits only when all 8 slots are busy.
+ *     osk_shards_search_merge instead takes each view's own workspace under its mutex, on the library's
+ *     stream (one collective sequence per communicator serialises those calls anyway).  Concurrent unfiltered calls with the same k /
  *     from / size are moreover batched opportunistically: while a batch runs, the calls that arrive
  *     queue up and the next batch takes them all (≤ 32 queries, one corpus pass for all of them;
  *     results identical to unbatched calls; tune "host_batching", "host_batch_leaders");
@@ -253,6 +254,7 @@ int32_t osk_view_scan_time(osk_view* view, double* total_ms, int64_t* calls);
  *   "gather_min"      accepted rows per gather tile at least (default 0 = every tile of the segment)
  *   "select_mid_k"    0|1 float32 searches with 12 < k ≤ 64 take the select path over int8 bounds
  *                     (default 1) instead of the fp32 streaming scan; k > 64 always takes it
+ *   "call_timing"     0|1 host entries time each call on the device (osk_last_call_device_ns; default 0)
  *   "sel_writer"      select path bounds writer: 0 = 4 row groups in flight + Java's transform,
  *                     1 = 4 groups + fp32 COSINE bounds, 2 = 2 groups (default), 3 = 1 group (fast bounds)
  * The testing build (libosknn_testing.so) also accepts "sq8_mfma_ablate", "mfma_ablate" (A/B timing,
@@ -268,12 +270,25 @@ int32_t osk_view_stats(osk_view* view, int64_t* batched_calls, int64_t* fallback
  * list overflowed past the certificate and the tile was re-scanned exactly), "sq8_exact_tiles"
  * (such tiles), "sq8_rescored_rows" (rows re-scored exactly, all calls), "select_calls" (searches
  * on the select path, k > 12), "host_slots" (workspace slots the host entries have leased: 1 + replicas),
- * "host_batches" / "host_batched_requests" (opportunistic batching of concurrent host calls). */
+ * "host_batches" / "host_batched_requests" (opportunistic batching of concurrent host calls).  The
+ * search counters sum over the view and the replica slots its host entries leased.  osk_view_profile /
+ * osk_view_scan_time time the device-entry calls on this view object only (per-call host timing:
+ * osk_last_call_device_ns). */
 int32_t osk_view_counter(osk_view* view, const char* name, int64_t* value);
 /* Testing build only (the shipped library returns OSK_ERR_UNSUPPORTED): copy `bytes` of an internal
  * buffer of the view's last search ("akeys", "cand_a", "flags", "qsplit", "qnorm", "sq8cand", "sq8lb",
  * "qc", "settle_trace") to host memory. */
 int32_t osk_view_debug_copy(osk_view* view, const char* name, void* host, int64_t bytes);
+
+/* Device time of this thread's last synchronous host search (osk_seg_search / osk_view_search), for a
+ * plugin's query-profile metrics: k-NN work shows up in the shard profile's rewrite time
+ * (S/search/internal/ContextIndexSearcher.java:207-216) and a plugin adds its own timers through
+ * SearchPlugin.getQueryProfileMetricsProvider (S/plugins/SearchPlugin.java:108).  Needs the
+ * "call_timing" knob (osk_tune_set, off by default: two events per call).  *device_ns = nanoseconds from
+ * the call's first to its last device operation on its stream (−1: timing off, or no host search on this
+ * thread yet); *shared_by (optional) = how many concurrent host requests that launch chain served
+ * (opportunistic batching: the time is shared by them). */
+int32_t osk_last_call_device_ns(int64_t* device_ns, int32_t* shared_by);
 
 /* Host-buffer convenience: shard search + coordinator merge on one device, synchronous.
  * accept: NULL or n_segs host pointers (each NULL or a host bitset). */
@@ -337,21 +352,42 @@ int32_t osk_comm_info(const osk_comm* comm, int32_t* rank, int32_t* world, int32
 /* Raw all-gather of `bytes` per rank (device buffers; one-device-per-process communicators). */
 int32_t osk_comm_all_gather(osk_comm* comm, const void* d_send, void* d_recv, int64_t bytes, void* stream);
 
+/* Every rank must issue the same searches in the same order (one collective sequence per communicator,
+ * like the coordinator's one request per shard copy).  Each call's exchange block carries a header — call
+ * sequence number, batch, k, from/size, shards per rank, dim/encoding and a fingerprint of the query
+ * bytes — and the shard indices of the rank's lists, which the device reduce compares across ranks.
+ * Ranks whose calls differ get count = −1 (and total hits −1) for every query of that call, and the
+ * communicator becomes poisoned: every later call returns OSK_ERR_INVALID (release and re-create it).
+ * osk_comm_status reports it (OSK_ERR_INVALID + message) without synchronising: synchronise the call's
+ * stream first.  info (optional, 4 values): [flag, rank 0's call number, first differing rank, its call
+ * number].  (A rank that never issues its call leaves the others blocked inside RCCL, as the
+ * coordinator would wait on a shard that never answers.) */
+int32_t osk_comm_status(const osk_comm* comm, int64_t* info);
+/* Testing build only (libosknn_testing.so; the shipped library returns OSK_ERR_UNSUPPORTED): a
+ * communicator of `world` processes that may share ONE device (RCCL refuses that), whose all-gather
+ * goes through the POSIX shared-memory segment named by id (a NUL-terminated "/name"), at most
+ * slot_bytes per rank and call.  It drives exactly the world > 1 code of the entries below on a
+ * one-GPU machine; a peer missing for 120 s is an error, not a hang. */
+int32_t osk_comm_init_loopback(int32_t device, int32_t rank, int32_t world, const uint8_t* id, int64_t slot_bytes,
+                               osk_comm** out);
+
 /* The whole multi-GPU query, host buffers, synchronous: every local view (views[i] on the
  * communicator's local device i) scans its shards, the per-shard top-k lists of every rank are
  * all-gathered once, and the coordinator reduce (from, size) runs on the device.  Every rank gets the
  * merged result.  shardIndex of a hit = the shard_index its view was created with (use the global
  * rank of the shard in sorted ShardId order).  accept: NULL or one host bitset pointer per segment
- * of every view, view 0's segments first.  All ranks must hold the same number of shards per rank
- * (the largest view's), or use the device entry below. */
+ * of every view, view 0's segments first.  Ranks may hold different numbers of shards (8 shards over 3
+ * GPUs): the list slots per rank are agreed on every call (a small all-gather that overlaps the scans). */
 int32_t osk_shards_search_merge(osk_comm* comm, osk_view* const* views, int32_t n_views, const void* queries,
                                 int32_t n_queries, int32_t k, const uint64_t* const* accept, int32_t from,
                                 int32_t size, float* out_scores, int32_t* out_docs, int32_t* out_shard_index,
                                 int32_t* out_count, int64_t* out_total_hits, float* out_max_score);
 /* The same for one GPU per process with device buffers, asynchronous on `stream`: d_queries
  * n_queries × dim on the view's device, d_accept as osk_view_search_device, shards_per_rank the
- * (common) number of list slots per rank (≥ the view's shards; slots past them are empty), outputs as
- * osk_merge_device. */
+ * number of list slots per rank (≥ the view's shards; slots past them are empty), outputs as
+ * osk_merge_device.  shards_per_rank must be the same on every rank (the caller knows the shard
+ * layout, e.g. the largest shard count of any rank): it sizes the all-gather, and RCCL cannot pair
+ * gathers of different sizes. */
 int32_t osk_shards_search_merge_device(osk_comm* comm, osk_view* view, const void* d_queries, int32_t n_queries,
                                        int32_t k, const uint64_t* const* d_accept, int32_t shards_per_rank,
                                        int32_t from, int32_t size, float* d_scores, int32_t* d_docs,

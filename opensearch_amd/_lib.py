@@ -75,6 +75,8 @@ SIGNATURES = {
     "osk_comm_release": (_I32, [_P]),
     "osk_comm_info": (_I32, [_P, _PI32, _PI32, _PI32]),
     "osk_comm_all_gather": (_I32, [_P, _P, _P, _I64, _P]),
+    "osk_comm_status": (_I32, [_P, _PI64]),
+    "osk_comm_init_loopback": (_I32, [_I32, _I32, _I32, _P, _I64, C.POINTER(_P)]),
     "osk_shards_search_merge": (_I32, [_P, _P, _I32, _P, _I32, _I32, _P, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     "osk_shards_search_merge_device": (_I32, [_P, _P, _P, _I32, _I32, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P,
                                               _P]),
@@ -97,6 +99,7 @@ SIGNATURES = {
     "osk_view_counter": (_I32, [_P, C.c_char_p, _PI64]),
     "osk_view_debug_copy": (_I32, [_P, C.c_char_p, _P, _I64]),
     "osk_view_scan_time": (_I32, [_P, C.POINTER(C.c_double), _PI64]),
+    "osk_last_call_device_ns": (_I32, [_PI64, _PI32]),
 }
 
 
@@ -174,6 +177,13 @@ def ptr(a) -> int | None:
 def tune(key: str, value: int) -> None:
     """Process-wide tuning knob (osk_tune_set): scan_nt, tiles_target, mfma_min_batch, mfma_units."""
     check(lib().osk_tune_set(key.encode(), int(value)))
+
+
+def last_call_device_ns() -> tuple[int, int]:
+    """(device ns, requests sharing it) of this thread's last host search (tune("call_timing", 1))."""
+    ns, shared = C.c_int64(), C.c_int32()
+    check(lib().osk_last_call_device_ns(C.byref(ns), C.byref(shared)))
+    return ns.value, shared.value
 
 
 def device_count() -> int:

@@ -24,8 +24,9 @@ CSRC = PKG / "csrc"
 INCLUDE = ROOT / "include"
 LIB = PKG / "libosknn.so"
 LIB_TESTING = PKG / "libosknn_testing.so"
-# the sources whose objects differ in the testing build (the C-ABI's test knobs; sq8_mfma's A/B ablations)
-TESTING_VARIANTS = ("osk_api.hip", "osk_sq8.hip")
+# the sources whose objects differ in the testing build (the C-ABI's test knobs; sq8_mfma's A/B ablations;
+# the loopback transport of the multi-rank exchange)
+TESTING_VARIANTS = ("osk_api.hip", "osk_sq8.hip", "osk_comm.hip")
 OBJDIR = ROOT / "build" / "osknn"
 
 SOURCES = ["osk_kernels.hip", "osk_mfma.hip", "osk_sq8.hip", "osk_filter.hip", "osk_select.hip", "osk_api.hip", "osk_comm.hip", "osk_host.cpp"]

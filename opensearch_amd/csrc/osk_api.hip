@@ -26,6 +26,40 @@ namespace {
 std::mutex g_dev_mu;
 std::vector<hipStream_t> g_streams;
 int g_ndev = -1;
+// Per-call device time of this thread's last synchronous host search (osk_last_call_device_ns):
+// nanoseconds between the call's first and last device operation on its stream, and how many host
+// requests shared that launch chain (opportunistic batching).  −1 / 0: timing off or no call yet.
+thread_local int64_t t_call_ns = -1;
+thread_local int32_t t_call_shared = 0;
+
+// Call timing of a host search (tune "call_timing"): events bracket the call's work on its stream.
+struct CallTimer {
+    osk_view* v = nullptr;
+    hipStream_t st = nullptr;
+    int32_t begin(osk_view* view, hipStream_t stream) {
+        t_call_ns = -1;
+        t_call_shared = 0;
+        if (!g_tuning.call_timing) return OSK_OK;
+        for (hipEvent_t& e : view->ev_call)
+            if (!e) OSK_HIP(hipEventCreate(&e));
+        v = view;
+        st = stream;
+        OSK_HIP(hipEventRecord(v->ev_call[0], st));
+        return OSK_OK;
+    }
+    int32_t end() {   // before the call's final stream synchronisation
+        if (v) OSK_HIP(hipEventRecord(v->ev_call[1], st));
+        return OSK_OK;
+    }
+    int32_t publish() {   // after it
+        if (!v) return OSK_OK;
+        float ms = 0.f;
+        OSK_HIP(hipEventElapsedTime(&ms, v->ev_call[0], v->ev_call[1]));
+        t_call_ns = (int64_t)((double)ms * 1e6);
+        t_call_shared = 1;
+        return OSK_OK;
+    }
+};
 }  // namespace
 
 namespace osk {
@@ -134,6 +168,8 @@ osk_view::~osk_view() {
     for (hipStream_t st : lease_streams)
         if (st) (void)hipStreamDestroy(st);
     if (xs_event) (void)hipEventDestroy(xs_event);
+    for (hipEvent_t e : ev_call)
+        if (e) (void)hipEventDestroy(e);
     for (int i = 0; i < kEvRing; ++i) {
         if (ev_start[i]) (void)hipEventDestroy(ev_start[i]);
         if (ev_stop[i]) (void)hipEventDestroy(ev_stop[i]);
@@ -257,6 +293,7 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         {"sq8_mfma_min", &g_tuning.sq8_mfma_min, 0, 1 << 20, false},
         {"sq8_mfma_ring", &g_tuning.sq8_mfma_ring, -1, 8, false},
         {"i8_stream", &g_tuning.i8_stream, 0, 1, false},
+        {"call_timing", &g_tuning.call_timing, 0, 1, false},
         {"sq8_mfma_ablate", &g_tuning.sq8_mfma_ablate, 0, 3, true},
         {"sq8_force_fallback", &g_tuning.sq8_force_fallback, 0, 1, true},
         {"settle_trace", &g_tuning.settle_trace, 0, 1, true},
@@ -1482,7 +1519,6 @@ int32_t view_search_device(osk_view* v, const void* d_queries, int nq, int k,
         if (d_visited) OSK_HIP(hipMemsetAsync(d_visited, 0, sizeof(int64_t) * v->segs.size(), st));
         return OSK_OK;
     }
-    OSK_HIP(v->ws_cand.reserve(sizeof(uint64_t) * (size_t)nq * v->n_tiles * k));
     OSK_HIP(v->ws_q.reserve((size_t)nq_pad * UP * 16));
     OSK_HIP(v->ws_qnorm.reserve(sizeof(float) * nq_pad));
     // Path cost model, measured end to end on MI355X, in µs for this view's rows R:
@@ -1649,12 +1685,23 @@ int32_t osk_view_debug_copy(osk_view* v, const char* name, void* host, int64_t b
     OSK_GUARD_END
 }
 
+// The view and every replica its host entries leased (slots): counters are summed over them.
+static std::vector<osk_view*> slot_views(osk_view* v) {
+    std::lock_guard<std::mutex> lk(v->lease_mu);
+    std::vector<osk_view*> out{v};
+    out.insert(out.end(), v->replicas.begin(), v->replicas.end());
+    return out;
+}
+
 int32_t osk_view_stats(osk_view* v, int64_t* batched_calls, int64_t* fallback_queries) {
     OSK_GUARD_BEGIN
     OSK_REQUIRE(v != nullptr && batched_calls && fallback_queries, "null argument");
-    std::lock_guard<std::mutex> lk(v->mu);
-    *batched_calls = v->mfma_calls;
-    *fallback_queries = v->mfma_fallback_queries;
+    *batched_calls = *fallback_queries = 0;
+    for (osk_view* s : slot_views(v)) {
+        std::lock_guard<std::mutex> lk(s->mu);
+        *batched_calls += s->mfma_calls;
+        *fallback_queries += s->mfma_fallback_queries;
+    }
     return OSK_OK;
     OSK_GUARD_END
 }
@@ -1675,21 +1722,30 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
         *value = n == "host_batches" ? v->batcher.batches : v->batcher.requests;
         return OSK_OK;
     }
-    std::lock_guard<std::mutex> lk(v->mu);
-    if (n == "mfma_calls") *value = v->mfma_calls;
-    else if (n == "mfma_fallback_queries") *value = v->mfma_fallback_queries;
-    else if (n == "sq8_calls") *value = v->sq8_calls;
-    else if (n == "select_calls") *value = v->sel_calls;
-    else if (n == "sq8_slices")
+    if (n == "sq8_slices") {
+        std::lock_guard<std::mutex> lk(v->mu);
         *value = v->n_slices;
-    else if (n == "sq8_fallback_queries" || n == "sq8_rescored_rows" || n == "sq8_exact_tiles") {
-        unsigned long long c[4];
-        OSK_HIP(hipMemcpy(c, v->d_counters.p, sizeof(c), hipMemcpyDeviceToHost));
-        *value = (int64_t)(n == "sq8_fallback_queries" ? c[0] : n == "sq8_rescored_rows" ? c[1] : c[2]);
-    } else {
-        set_error("unknown counter: " + n);
-        return OSK_ERR_INVALID;
+        return OSK_OK;
     }
+    const bool dev = n == "sq8_fallback_queries" || n == "sq8_rescored_rows" || n == "sq8_exact_tiles";
+    OSK_REQUIRE(dev || n == "mfma_calls" || n == "mfma_fallback_queries" || n == "sq8_calls" || n == "select_calls",
+                "unknown counter: " + n);
+    // summed over the view and the replicas its host entries leased
+    int64_t sum = 0;
+    for (osk_view* s : slot_views(v)) {
+        std::lock_guard<std::mutex> lk(s->mu);
+        if (dev) {
+            if (!s->d_counters.p) continue;
+            unsigned long long c[4];
+            OSK_HIP(hipDeviceSynchronize());   // the last search may be on any stream
+            OSK_HIP(hipMemcpy(c, s->d_counters.p, sizeof(c), hipMemcpyDeviceToHost));
+            sum += (int64_t)(n == "sq8_fallback_queries" ? c[0] : n == "sq8_rescored_rows" ? c[1] : c[2]);
+        } else {
+            sum += n == "mfma_calls" ? s->mfma_calls : n == "mfma_fallback_queries" ? s->mfma_fallback_queries
+                 : n == "sq8_calls" ? s->sq8_calls : s->sel_calls;
+        }
+    }
+    *value = sum;
     return OSK_OK;
     OSK_GUARD_END
 }
@@ -1735,6 +1791,8 @@ static int32_t view_search_host(osk_view* v, const void* queries, int32_t n_quer
     const int nq = n_queries, S = v->n_shards, ns = (int)v->segs.size();
     const int64_t elem = v->enc == ENC_FLOAT32 ? 4 : 1;
     const size_t qbytes = (size_t)nq * v->dim * elem;
+    CallTimer timer;
+    if ((rc = timer.begin(v, st)) != OSK_OK) return rc;
 
     // accept bitsets → device
     const uint64_t* const* d_acc = nullptr;
@@ -1746,9 +1804,13 @@ static int32_t view_search_host(osk_view* v, const void* queries, int32_t n_quer
             if (accept[i]) words += (size_t)(v->segs[i]->max_doc + 63) / 64;
         OSK_HIP(v->ws_accept.reserve(std::max<size_t>(8, words * 8)));
         OSK_HIP(v->ws_accept_ptrs.reserve(sizeof(void*) * ns));
-        std::vector<const uint64_t*> ptrs(ns, nullptr);
+        // the pointer table is staged in the view's pinned buffer: it is the source of an async copy and
+        // must outlive it (the stream is synchronised only at the end of the call)
+        OSK_HIP(v->h_accept_tab.reserve(sizeof(void*) * ns));
+        const uint64_t** ptrs = static_cast<const uint64_t**>(v->h_accept_tab.p);
         size_t off = 0;
         for (int i = 0; i < ns; ++i) {
+            ptrs[i] = nullptr;
             if (!accept[i]) continue;
             const size_t w = (size_t)(v->segs[i]->max_doc + 63) / 64;
             ptrs[i] = v->ws_accept.as<uint64_t>() + off;
@@ -1756,8 +1818,7 @@ static int32_t view_search_host(osk_view* v, const void* queries, int32_t n_quer
                                    hipMemcpyHostToDevice, st));
             off += w;
         }
-        OSK_HIP(hipMemcpyAsync(v->ws_accept_ptrs.p, ptrs.data(), sizeof(void*) * ns,
-                               hipMemcpyHostToDevice, st));
+        OSK_HIP(hipMemcpyAsync(v->ws_accept_ptrs.p, ptrs, sizeof(void*) * ns, hipMemcpyHostToDevice, st));
         d_acc = v->ws_accept_ptrs.as<const uint64_t*>();
     }
     OSK_HIP(v->ws_qin.reserve(std::max<size_t>(16, qbytes)));
@@ -1784,7 +1845,9 @@ static int32_t view_search_host(osk_view* v, const void* queries, int32_t n_quer
                                st));
     OSK_HIP(v->h_stage.reserve(total_b));
     OSK_HIP(hipMemcpyAsync(v->h_stage.p, ob, total_b, hipMemcpyDeviceToHost, st));
+    if ((rc = timer.end()) != OSK_OK) return rc;
     OSK_HIP(hipStreamSynchronize(st));
+    if ((rc = timer.publish()) != OSK_OK) return rc;
     const char* hb = static_cast<const char*>(v->h_stage.p);
     std::memcpy(out_scores, hb + o_sc, b_sc);
     std::memcpy(out_docs, hb + o_doc, b_doc);
@@ -1832,6 +1895,8 @@ static int32_t seg_search_host(osk_seg* seg, const void* queries, int32_t n_quer
     const int nq = n_queries;
     const int64_t elem = seg->enc == ENC_FLOAT32 ? 4 : 1;
     const size_t qbytes = (size_t)nq * seg->dim * elem;
+    CallTimer timer;
+    if ((rc = timer.begin(v, st)) != OSK_OK) return rc;
     const uint64_t* const* d_acc = nullptr;
     if (accept_bits) {
         const size_t w = (size_t)(seg->max_doc + 63) / 64;
@@ -1857,7 +1922,9 @@ static int32_t seg_search_host(osk_seg* seg, const void* queries, int32_t n_quer
     OSK_HIP(hipMemcpyAsync(hb, v->ws_keys.p, kb, hipMemcpyDeviceToHost, st));
     OSK_HIP(hipMemcpyAsync(hb + kb, v->ws_counts.p, cb, hipMemcpyDeviceToHost, st));
     OSK_HIP(hipMemcpyAsync(hb + kb + cb, v->ws_visited.p, 8, hipMemcpyDeviceToHost, st));
+    if ((rc = timer.end()) != OSK_OK) return rc;
     OSK_HIP(hipStreamSynchronize(st));
+    if ((rc = timer.publish()) != OSK_OK) return rc;
     const uint64_t* keys = reinterpret_cast<const uint64_t*>(hb);
     const int32_t* cnt = reinterpret_cast<const int32_t*>(hb + kb);
     int64_t visited;
@@ -1908,6 +1975,8 @@ struct BatchReq {
     int32_t rc = OSK_OK;
     std::string err;
     bool done = false;
+    int64_t device_ns = -1;   // the serving launch chain's device time (call_timing) ...
+    int32_t shared = 0;       // ... and how many requests it served
 };
 
 // run `fn(batch, total_queries)` as a leader whenever possible until `me` is done
@@ -1934,6 +2003,7 @@ int32_t batched_call(osk_view* root, BatchReq& me, Fn&& fn) {
             ++B.leaders;
             lk.unlock();
             int32_t rc;
+            t_call_ns = -1;
             try {   // the batch's requests must always be completed, whatever happens
                 rc = fn(batch, total);
             } catch (const std::bad_alloc&) {
@@ -1948,6 +2018,8 @@ int32_t batched_call(osk_view* root, BatchReq& me, Fn&& fn) {
             for (BatchReq* r : batch) {
                 r->rc = rc;
                 r->err = err;
+                r->device_ns = t_call_ns;
+                r->shared = t_call_ns >= 0 ? (int32_t)batch.size() : 0;
                 r->done = true;
             }
             --B.leaders;
@@ -1958,6 +2030,8 @@ int32_t batched_call(osk_view* root, BatchReq& me, Fn&& fn) {
             B.cv.wait(lk);
         }
     }
+    t_call_ns = me.device_ns;
+    t_call_shared = me.shared;
     if (me.rc) set_error("batched search: " + me.err);
     return me.rc;
 }
@@ -2067,6 +2141,15 @@ int32_t osk_seg_search(osk_seg* seg, const void* queries, int32_t n_queries, int
         }
         return OSK_OK;
     });
+    OSK_GUARD_END
+}
+
+int32_t osk_last_call_device_ns(int64_t* device_ns, int32_t* shared_by) {
+    OSK_GUARD_BEGIN
+    OSK_REQUIRE(device_ns != nullptr, "null argument");
+    *device_ns = t_call_ns;
+    if (shared_by) *shared_by = t_call_shared;
+    return OSK_OK;
     OSK_GUARD_END
 }
 

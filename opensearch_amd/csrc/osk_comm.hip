@@ -14,18 +14,25 @@
 // hit keys [nq][shards_per_rank][k] (key 0 = empty); one ncclAllGather moves them to every GPU
 // (8·k·nq bytes per shard: latency-bound, µs next to a ms scan); merge_coord then runs straight over
 // the gathered rank-major image.  A list's hit count is its number of non-zero keys, so counts are not
-// exchanged.  The shardIndex of every gathered slot is exchanged once per (communicator, view).
+// exchanged.  Each rank's block also carries its shard indices and a call header (sequence number,
+// batch shape, query fingerprint) that the reduce checks across ranks, so ranks that issued different
+// calls get an error instead of a merge of unrelated lists (see "the exchange block" below).
 //
 // RCCL is loaded at run time (dlopen of librccl.so.1, preferring a copy the process already loaded,
 // e.g. PyTorch's), so the library itself has no link-time dependency on it and every other entry point
 // works where RCCL is absent; the communicator entry points then fail with OSK_ERR_UNSUPPORTED.
 #include <dlfcn.h>
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstring>
+#include <thread>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -48,7 +55,15 @@ struct osk_comm {
     // reused by every call: calls are serialised by `mu`, and a stream wait binds the record before it
     std::vector<hipEvent_t> ev_in, ev_out;
     std::mutex mu;                       // one collective sequence at a time
+    uint64_t seq = 0;                    // calls issued (the exchange header's sequence number)
+    // [mismatch flag, rank 0's sequence number, first mismatching rank, its sequence number], written by
+    // the reduce kernel (pinned host memory); a set flag makes the communicator refuse further calls
+    osk::HostPinned h_err;
+    osk::HostPinned h_spr;               // the host entry's shards-per-rank agreement (agree_spr)
+    void* lb = nullptr;                  // testing build: loopback transport instead of RCCL
+    void (*lb_free)(void*) = nullptr;
     ~osk_comm() {
+        if (lb_free) lb_free(lb);
         for (size_t i = 0; i < devices.size(); ++i) {
             (void)hipSetDevice(devices[i]);
             if (i < xstreams.size() && xstreams[i]) (void)hipStreamDestroy(xstreams[i]);
@@ -136,6 +151,8 @@ int32_t make_xstreams(osk_comm* c) {
         OSK_HIP(hipEventCreateWithFlags(&c->ev_in[i], hipEventDisableTiming));
         OSK_HIP(hipEventCreateWithFlags(&c->ev_out[i], hipEventDisableTiming));
     }
+    OSK_HIP(c->h_err.reserve(4 * sizeof(int64_t)));
+    std::memset(c->h_err.p, 0, 4 * sizeof(int64_t));
     return OSK_OK;
 }
 
@@ -152,6 +169,15 @@ hipError_t leave_xstream(osk_comm* c, size_t i, hipStream_t st) {
 }
 
 // The per-shard lists of one view, padded to `spr` shards per rank: ws_xkeys [nq][spr][k].
+// ws_keys [nq][n_shards][k] → ws_xkeys [nq][spr][k], the pad slots zero (empty lists).
+int32_t pad_lists(osk_view* v, int nq, int k, int spr, hipStream_t st) {
+    uint64_t* xk = v->ws_xkeys.as<uint64_t>();
+    OSK_HIP(hipMemsetAsync(xk, 0, sizeof(uint64_t) * nq * spr * k, st));
+    OSK_HIP(hipMemcpy2DAsync(xk, sizeof(uint64_t) * spr * k, v->ws_keys.p, sizeof(uint64_t) * v->n_shards * k,
+                             sizeof(uint64_t) * v->n_shards * k, nq, hipMemcpyDeviceToDevice, st));
+    return OSK_OK;
+}
+
 int32_t search_padded(osk_view* v, const void* d_queries, int nq, int k, const uint64_t* const* d_accept, int spr,
                       hipStream_t st) {
     const size_t per = (size_t)nq * spr * k;
@@ -164,60 +190,200 @@ int32_t search_padded(osk_view* v, const void* d_queries, int nq, int k, const u
     int32_t rc = view_search_device(v, d_queries, nq, k, d_accept, v->ws_keys.as<uint64_t>(),
                                     v->ws_counts.as<int32_t>(), nullptr, st);
     if (rc) return rc;
-    // rows of n_shards·k keys → rows of spr·k keys, the pad slots zero (empty lists)
-    OSK_HIP(hipMemsetAsync(xk, 0, sizeof(uint64_t) * per, st));
-    OSK_HIP(hipMemcpy2DAsync(xk, sizeof(uint64_t) * spr * k, v->ws_keys.p, sizeof(uint64_t) * v->n_shards * k,
-                             sizeof(uint64_t) * v->n_shards * k, nq, hipMemcpyDeviceToDevice, st));
-    return OSK_OK;
+    return pad_lists(v, nq, k, spr, st);
 }
 
-// The shardIndex of every gathered slot (rank r's slot j ↔ its view's shard_index[j]; pads INT32_MAX),
-// exchanged once per (comm, spr) and kept in every local view's d_xsi.
-int32_t exchange_shard_index(osk_comm* c, osk_view* const* views, int spr) {
-    const hipStream_t* sts = c->xstreams.data();   // synchronous: behind every earlier collective
-    bool fresh = true;
-    for (size_t i = 0; i < c->devices.size(); ++i)
-        fresh &= views[i]->xsi_comm == c->id && views[i]->xsi_spr == spr;
-    if (fresh) return OSK_OK;
-    const Rccl* R = &g_rccl;
-    for (size_t i = 0; i < c->devices.size(); ++i) {
-        osk_view* v = views[i];
-        OSK_HIP(hipSetDevice(v->device));
-        OSK_HIP(hipDeviceSynchronize());   // one-time: no earlier reduce still reads d_xsi
-        std::vector<int32_t> mine(spr, 0x7FFFFFFF);
-        for (int j = 0; j < v->n_shards; ++j) mine[j] = v->shard_index[j];
-        OSK_HIP(v->d_xsi.reserve(sizeof(int32_t) * (size_t)spr * (c->world + 1)));
-        int32_t* own = v->d_xsi.as<int32_t>() + (size_t)spr * c->world;   // the local part, after the image
-        OSK_HIP(hipMemcpyAsync(own, mine.data(), sizeof(int32_t) * spr, hipMemcpyHostToDevice, sts[i]));
-        OSK_HIP(hipStreamSynchronize(sts[i]));
-    }
-    OSK_NCCL(R->GroupStart());
-    for (size_t i = 0; i < c->devices.size(); ++i) {
-        osk_view* v = views[i];
-        int32_t* own = v->d_xsi.as<int32_t>() + (size_t)spr * c->world;
-        OSK_NCCL(R->AllGather(own, v->d_xsi.p, (size_t)spr, ncclInt32, c->comms[i], sts[i]));
-    }
-    OSK_NCCL(R->GroupEnd());
-    for (size_t i = 0; i < c->devices.size(); ++i) {
-        OSK_HIP(hipSetDevice(views[i]->device));
-        OSK_HIP(hipStreamSynchronize(sts[i]));
-        views[i]->xsi_comm = c->id;
-        views[i]->xsi_spr = spr;
-    }
-    return OSK_OK;
+// ---- the exchange block ------------------------------------------------------------------------
+// Rank block (u64 words): [keys nq·spr·k][header kXHdrWords][shard indices spr int32, padded to words].
+// Every call gathers whole blocks, so each call carries its own shardIndex (no cached exchange state a
+// rank could disagree about) and a header the reduce compares across ranks (osk_device.h
+// xchg_header_check): call sequence number, batch, k, from/size, shards per rank, dim/encoding and a
+// fingerprint of the query bytes.  Ranks that issued different calls get count −1 on every query and
+// a sticky error on the communicator instead of merging keys of different queries.
+struct Block {
+    size_t keys, words;
+};
+Block block_of(int nq, int k, int spr) {
+    const size_t keys = (size_t)nq * spr * k;
+    return {keys, keys + kXHdrWords + (size_t)(spr + 1) / 2};
 }
 
-// One all-gather of every local view's ws_xkeys into its ws_xgath (grouped over local devices).
-int32_t gather_keys(osk_comm* c, osk_view* const* views, int nq, int k, int spr, const hipStream_t* sts) {
-    const size_t per = (size_t)nq * spr * k;
+constexpr uint64_t kXMagic = 0x4F534B5800000001ull;   // "OSKX", block format 1
+
+// Header words of this call (w[5], the query fingerprint, is computed on the device).
+void header_words(uint64_t (&w)[kXHdrWords], uint64_t seq, int nq, int k, int from, int size, int spr, int dim,
+                  int enc, int world) {
+    w[0] = kXMagic;
+    w[1] = seq;
+    w[2] = (uint32_t)nq | ((uint64_t)(uint32_t)k << 32);
+    w[3] = (uint32_t)from | ((uint64_t)(uint32_t)size << 32);
+    w[4] = (uint32_t)spr | ((uint64_t)(uint32_t)(dim | enc << 16) << 32);
+    w[5] = 0;
+    w[6] = (uint64_t)world;
+    w[7] = 0;
+}
+
+int32_t poisoned(const osk_comm* c) {
+    const int64_t* e = static_cast<const int64_t*>(c->h_err.p);
+    if (!e || !e[0]) return OSK_OK;
+    set_error("communicator poisoned: the ranks issued different calls (rank 0 at call " + std::to_string(e[1]) +
+              ", rank " + std::to_string(e[2]) + " at call " + std::to_string(e[3]) +
+              "); every rank must issue the same searches in the same order — release and re-create it");
+    return OSK_ERR_INVALID;
+}
+
+#ifdef OSK_TESTING
+// ---- loopback transport (testing build only) -----------------------------------------------------
+// Lets one GPU host several ranks (RCCL refuses two ranks on one device), so the world > 1 code of
+// this file runs on a one-GPU box: the all-gather goes through a POSIX shared-memory segment.  Per
+// call g every rank copies its block into slot [g & 1][rank], publishes gen[rank] = g, waits for every
+// rank's gen ≥ g, copies all slots into its receive buffer and publishes read[rank] = g; a slot is
+// rewritten (call g + 2) only once every rank has read call g.  A peer that does not arrive within
+// kLoopbackTimeoutS is an error, not a hang.
+struct Loopback {
+    static constexpr int kMaxWorld = 64;
+    static constexpr double kTimeoutS = 120.0;
+    struct Ctrl {
+        std::atomic<int64_t> joined;
+        std::atomic<int64_t> gen[kMaxWorld];
+        std::atomic<int64_t> read[kMaxWorld];
+        std::atomic<int64_t> bytes[2][kMaxWorld];
+    };
+    int rank = 0, world = 1;
+    size_t slot_bytes = 0, map_bytes = 0;
+    void* base = nullptr;
+    int fd = -1;
+    std::string name;
+    int64_t gen = 0;
+    Ctrl* ctrl() const { return static_cast<Ctrl*>(base); }
+    char* slot(int par, int r) const {
+        return static_cast<char*>(base) + 4096 + ((size_t)par * world + r) * slot_bytes;
+    }
+    ~Loopback() {
+        if (base) munmap(base, map_bytes);
+        if (fd >= 0) close(fd);
+        if (rank == 0 && !name.empty()) shm_unlink(name.c_str());
+    }
+    // every rank's counter ≥ want (false: timed out)
+    bool wait_all(std::atomic<int64_t>* a, int64_t want) const {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int r = 0; r < world; ++r)
+            while (a[r].load(std::memory_order_acquire) < want) {
+                if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kTimeoutS)
+                    return false;
+                std::this_thread::sleep_for(std::chrono::microseconds(20));
+            }
+        return true;
+    }
+};
+
+int32_t lb_allgather(Loopback* L, const void* d_send, void* d_recv, size_t bytes, hipStream_t st) {
+    OSK_REQUIRE(bytes <= L->slot_bytes, "loopback all-gather: the block is larger than the slot");
+    Loopback::Ctrl* c = L->ctrl();
+    const int64_t g = ++L->gen;
+    const int par = (int)(g & 1);
+    if (!L->wait_all(c->read, g - 2)) {   // slot [par][rank] is free once every rank has read call g − 2
+        set_error("loopback all-gather: a peer never finished reading call " + std::to_string(g - 2));
+        return OSK_ERR_DEVICE;
+    }
+    OSK_HIP(hipMemcpyAsync(L->slot(par, L->rank), d_send, bytes, hipMemcpyDeviceToHost, st));
+    OSK_HIP(hipStreamSynchronize(st));
+    c->bytes[par][L->rank].store((int64_t)bytes, std::memory_order_relaxed);
+    c->gen[L->rank].store(g, std::memory_order_release);
+    if (!L->wait_all(c->gen, g)) {
+        set_error("loopback all-gather: a peer never issued call " + std::to_string(g));
+        return OSK_ERR_DEVICE;
+    }
+    bool same = true;
+    for (int r = 0; r < L->world; ++r) same &= c->bytes[par][r].load(std::memory_order_relaxed) == (int64_t)bytes;
+    for (int r = 0; same && r < L->world; ++r)
+        OSK_HIP(hipMemcpyAsync(static_cast<char*>(d_recv) + (size_t)r * bytes, L->slot(par, r), bytes,
+                               hipMemcpyHostToDevice, st));
+    OSK_HIP(hipStreamSynchronize(st));
+    c->read[L->rank].store(g, std::memory_order_release);
+    OSK_REQUIRE(same, "loopback all-gather: the ranks passed blocks of different sizes");
+    return OSK_OK;
+}
+#endif
+
+// One all-gather of every local view's block (ws_xkeys, `words` u64) into its ws_xgath, on the
+// communicator's exchange streams (grouped over local devices).
+int32_t gather_blocks(osk_comm* c, osk_view* const* views, size_t words, const hipStream_t* sts) {
     for (size_t i = 0; i < c->devices.size(); ++i) {
         OSK_HIP(hipSetDevice(views[i]->device));
-        OSK_HIP(views[i]->ws_xgath.reserve(sizeof(uint64_t) * per * c->world));
+        OSK_HIP(views[i]->ws_xgath.reserve(sizeof(uint64_t) * words * c->world));
     }
+#ifdef OSK_TESTING
+    if (c->lb) return lb_allgather(static_cast<Loopback*>(c->lb), views[0]->ws_xkeys.p, views[0]->ws_xgath.p,
+                                   words * 8, sts[0]);
+#endif
     OSK_NCCL(g_rccl.GroupStart());
     for (size_t i = 0; i < c->devices.size(); ++i)
-        OSK_NCCL(g_rccl.AllGather(views[i]->ws_xkeys.p, views[i]->ws_xgath.p, per, ncclUint64, c->comms[i], sts[i]));
+        OSK_NCCL(g_rccl.AllGather(views[i]->ws_xkeys.p, views[i]->ws_xgath.p, words, ncclUint64, c->comms[i], sts[i]));
     OSK_NCCL(g_rccl.GroupEnd());
+    return OSK_OK;
+}
+
+// This rank's block of one view: the trailer (header + shard indices) and the per-shard lists padded to
+// spr shards.
+int32_t fill_block(osk_view* v, const void* d_queries, int nq, int k, const uint64_t* const* d_accept, int spr,
+                   const uint64_t (&hw)[kXHdrWords], hipStream_t st) {
+    const Block B = block_of(nq, k, spr);
+    OSK_HIP(v->ws_xkeys.reserve(sizeof(uint64_t) * B.words));
+    const int64_t qbytes = (int64_t)nq * v->dim * (v->enc == ENC_FLOAT32 ? 4 : 1);
+    OSK_HIP(launch_xhdr_fill(v->ws_xkeys.as<uint64_t>() + B.keys, hw, d_queries, qbytes,
+                             v->d_shard_index.as<int32_t>(), v->n_shards, spr, st));
+    return search_padded(v, d_queries, nq, k, d_accept, spr, st);
+}
+
+// The reduce's view of a gathered (or, world 1, local) image of blocks.
+XLayout image_layout(const osk_comm* c, const uint64_t* image, const Block& B, const int32_t** shard_index) {
+    XLayout x;
+    x.rank_words = B.words;
+    x.si_stride = (int)(2 * B.words);
+    x.hdr = image + B.keys;
+    x.err = static_cast<int64_t*>(c->h_err.p);
+    *shard_index = reinterpret_cast<const int32_t*>(image + B.keys + kXHdrWords);
+    return x;
+}
+
+// The largest shard count over every view of every rank (host entry).  Each local device sends its
+// view's count through the exchange stream; the host waits for the tiny gather (the scans already run).
+int32_t agree_spr(osk_comm* c, osk_view* const* views, int* spr) {
+    const size_t nl = c->devices.size(), W = (size_t)c->world;
+    OSK_HIP(c->h_spr.reserve(sizeof(int64_t) * nl * (W + 1)));
+    int64_t* h = static_cast<int64_t*>(c->h_spr.p);   // [nl] send values, then [nl][W] received
+    for (size_t i = 0; i < nl; ++i) {
+        osk_view* v = views[i];
+        OSK_HIP(hipSetDevice(v->device));
+        OSK_HIP(v->ws_xspr.reserve(sizeof(int64_t) * (W + 1)));
+        h[i] = v->n_shards;
+        OSK_HIP(hipMemcpyAsync(v->ws_xspr.as<int64_t>() + W, h + i, 8, hipMemcpyHostToDevice, c->xstreams[i]));
+    }
+#ifdef OSK_TESTING
+    if (c->lb) {
+        int32_t rc = lb_allgather(static_cast<Loopback*>(c->lb), views[0]->ws_xspr.as<int64_t>() + W,
+                                  views[0]->ws_xspr.p, 8, c->xstreams[0]);
+        if (rc) return rc;
+    } else
+#endif
+    {
+        OSK_NCCL(g_rccl.GroupStart());
+        for (size_t i = 0; i < nl; ++i)
+            OSK_NCCL(g_rccl.AllGather(views[i]->ws_xspr.as<int64_t>() + W, views[i]->ws_xspr.p, 1, ncclInt64,
+                                      c->comms[i], c->xstreams[i]));
+        OSK_NCCL(g_rccl.GroupEnd());
+    }
+    int64_t* recv = h + nl;
+    OSK_HIP(hipSetDevice(views[0]->device));
+    OSK_HIP(hipMemcpyAsync(recv, views[0]->ws_xspr.p, 8 * W, hipMemcpyDeviceToHost, c->xstreams[0]));
+    for (size_t i = 0; i < nl; ++i) {
+        OSK_HIP(hipSetDevice(views[i]->device));
+        OSK_HIP(hipStreamSynchronize(c->xstreams[i]));
+    }
+    int m = 1;
+    for (size_t r = 0; r < W; ++r) m = std::max<int>(m, (int)recv[r]);
+    *spr = m;
     return OSK_OK;
 }
 
@@ -343,9 +509,84 @@ int32_t osk_comm_all_gather(osk_comm* comm, const void* d_send, void* d_recv, in
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : device_stream(comm->devices[0]);
     std::lock_guard<std::mutex> lk(comm->mu);
     OSK_HIP(enter_xstream(comm, 0, st));
-    OSK_NCCL(g_rccl.AllGather(d_send, d_recv, (size_t)bytes, ncclUint8, comm->comms[0], comm->xstreams[0]));
+#ifdef OSK_TESTING
+    if (comm->lb) {
+        rc = lb_allgather(static_cast<Loopback*>(comm->lb), d_send, d_recv, (size_t)bytes, comm->xstreams[0]);
+        if (rc) return rc;
+    } else
+#endif
+        OSK_NCCL(g_rccl.AllGather(d_send, d_recv, (size_t)bytes, ncclUint8, comm->comms[0], comm->xstreams[0]));
     OSK_HIP(leave_xstream(comm, 0, st));
     return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_comm_status(const osk_comm* comm, int64_t* info) {
+    OSK_GUARD_BEGIN
+    clear_error();
+    OSK_REQUIRE(comm != nullptr, "comm is null");
+    const int64_t* e = static_cast<const int64_t*>(comm->h_err.p);
+    if (info)
+        for (int i = 0; i < 4; ++i) info[i] = e ? e[i] : 0;
+    return poisoned(comm);
+    OSK_GUARD_END
+}
+
+int32_t osk_comm_init_loopback(int32_t device, int32_t rank, int32_t world, const uint8_t* id, int64_t slot_bytes,
+                               osk_comm** out) {
+    OSK_GUARD_BEGIN
+    clear_error();
+#ifndef OSK_TESTING
+    (void)device; (void)rank; (void)world; (void)id; (void)slot_bytes; (void)out;
+    set_error("osk_comm_init_loopback exists only in the testing build (libosknn_testing.so)");
+    return OSK_ERR_UNSUPPORTED;
+#else
+    OSK_REQUIRE(out != nullptr && id != nullptr, "null argument");
+    OSK_REQUIRE(world >= 1 && world <= Loopback::kMaxWorld && rank >= 0 && rank < world, "need 0 <= rank < world <= 64");
+    OSK_REQUIRE(slot_bytes >= 4096 && slot_bytes <= (int64_t)1 << 30, "slot_bytes must be in [4 KiB, 1 GiB]");
+    const size_t n = strnlen(reinterpret_cast<const char*>(id), OSK_COMM_ID_BYTES);
+    OSK_REQUIRE(n > 1 && n < OSK_COMM_ID_BYTES && id[0] == '/', "loopback id: a NUL-terminated name \"/...\"");
+    int32_t rc = check_device(device);
+    if (rc) return rc;
+    auto L = std::make_unique<Loopback>();
+    L->rank = rank;
+    L->world = world;
+    L->slot_bytes = ((size_t)slot_bytes + 4095) & ~(size_t)4095;
+    L->map_bytes = 4096 + 2 * (size_t)world * L->slot_bytes;
+    L->name.assign(reinterpret_cast<const char*>(id), n);
+    static_assert(sizeof(Loopback::Ctrl) <= 4096, "loopback control block");
+    L->fd = shm_open(L->name.c_str(), O_CREAT | O_RDWR, 0600);
+    OSK_REQUIRE(L->fd >= 0, "loopback: shm_open failed: " + std::string(strerror(errno)));
+    OSK_REQUIRE(ftruncate(L->fd, (off_t)L->map_bytes) == 0, "loopback: ftruncate failed");
+    L->base = mmap(nullptr, L->map_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, L->fd, 0);
+    if (L->base == MAP_FAILED) {
+        L->base = nullptr;
+        set_error("loopback: mmap failed");
+        return OSK_ERR_OOM;
+    }
+    // (a fresh segment is zero-filled; every rank joins before the first call)
+    L->ctrl()->joined.fetch_add(1);
+    const auto t0 = std::chrono::steady_clock::now();
+    while (L->ctrl()->joined.load() < world) {
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > Loopback::kTimeoutS) {
+            set_error("loopback: not every rank joined");
+            return OSK_ERR_DEVICE;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+    auto c = std::make_unique<osk_comm>();
+    c->id = ++g_comm_ids;
+    c->rank = rank;
+    c->world = world;
+    c->devices = {device};
+    c->comms.assign(1, nullptr);
+    rc = make_xstreams(c.get());
+    if (rc) return rc;
+    c->lb = L.release();
+    c->lb_free = [](void* p) { delete static_cast<Loopback*>(p); };
+    *out = c.release();
+    return OSK_OK;
+#endif
     OSK_GUARD_END
 }
 
@@ -367,37 +608,32 @@ int32_t osk_shards_search_merge_device(osk_comm* comm, osk_view* view, const voi
     if (rc) return rc;
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : device_stream(view->device);
     std::lock_guard<std::mutex> lc(comm->mu);
+    rc = poisoned(comm);
+    if (rc) return rc;
     std::lock_guard<std::mutex> lv(view->mu);
     rc = order_after_last(view, st);
     if (rc) return rc;
-    osk_view* const vs[1] = {view};
-    if (comm->world > 1) {
-        rc = exchange_shard_index(comm, vs, shards_per_rank);
-        if (rc) return rc;
-    } else if (view->xsi_comm != comm->id || view->xsi_spr != shards_per_rank) {
-        std::vector<int32_t> mine(shards_per_rank, 0x7FFFFFFF);
-        for (int j = 0; j < view->n_shards; ++j) mine[j] = view->shard_index[j];
-        OSK_HIP(view->d_xsi.reserve(sizeof(int32_t) * shards_per_rank));
-        OSK_HIP(hipMemcpyAsync(view->d_xsi.p, mine.data(), sizeof(int32_t) * shards_per_rank, hipMemcpyHostToDevice, st));
-        OSK_HIP(hipStreamSynchronize(st));
-        view->xsi_comm = comm->id;
-        view->xsi_spr = shards_per_rank;
-    }
-    rc = search_padded(view, d_queries, n_queries, k, d_accept, shards_per_rank, st);
+    const Block B = block_of(n_queries, k, shards_per_rank);
+    uint64_t hw[kXHdrWords];
+    header_words(hw, ++comm->seq, n_queries, k, from, size, shards_per_rank, view->dim, view->enc, comm->world);
+    rc = fill_block(view, d_queries, n_queries, k, d_accept, shards_per_rank, hw, st);
     if (rc) return rc;
+    osk_view* const vs[1] = {view};
     const uint64_t* image = view->ws_xkeys.as<uint64_t>();
-    if (comm->world > 1) {   // world 1: the local lists are the whole image
-        // lists ready on st → the all-gather on the communicator's exchange stream → the reduce on st.
+    if (comm->world > 1) {   // world 1: the local block is the whole image
+        // block ready on st → the all-gather on the communicator's exchange stream → the reduce on st.
         // The view's next search (same view, any stream) is ordered after this call's reduce on st
         // (order_after_last), which waits for this gather, so ws_xkeys / ws_xgath are never raced.
         OSK_HIP(enter_xstream(comm, 0, st));
-        rc = gather_keys(comm, vs, n_queries, k, shards_per_rank, comm->xstreams.data());
+        rc = gather_blocks(comm, vs, B.words, comm->xstreams.data());
         if (rc) return rc;
         OSK_HIP(leave_xstream(comm, 0, st));
         image = view->ws_xgath.as<uint64_t>();
     }
-    OSK_HIP(launch_coord_reduce(image, nullptr, view->d_xsi.as<int32_t>(), n_queries, comm->world, shards_per_rank, k,
-                               from, size, d_scores, d_docs, d_shard_out, d_count, d_total_hits, d_max_score, st));
+    const int32_t* sidx = nullptr;
+    const XLayout x = image_layout(comm, image, B, &sidx);
+    OSK_HIP(launch_coord_reduce(image, nullptr, sidx, n_queries, comm->world, shards_per_rank, k, from, size, d_scores,
+                               d_docs, d_shard_out, d_count, d_total_hits, d_max_score, st, x));
     return OSK_OK;
     OSK_GUARD_END
 }
@@ -420,12 +656,11 @@ int32_t osk_shards_search_merge(osk_comm* comm, osk_view* const* views, int32_t 
                     "all views must share dim and encoding");
         spr = std::max(spr, views[i]->n_shards);
     }
-    // every rank must use the same shards_per_rank: in one-process mode it is the max over the views;
-    // across processes the caller must stage the same number of shards on every rank (or use the
-    // device entry, which takes shards_per_rank explicitly)
     int32_t rc = check_merge_args(comm, n_queries, k, from, size, spr);
     if (rc) return rc;
     std::lock_guard<std::mutex> lc(comm->mu);
+    rc = poisoned(comm);
+    if (rc) return rc;
     std::vector<std::unique_lock<std::mutex>> locks;
     std::vector<hipStream_t> sts(n_views);
     const int64_t elem = views[0]->enc == ENC_FLOAT32 ? 4 : 1;
@@ -442,12 +677,6 @@ int32_t osk_shards_search_merge(osk_comm* comm, osk_view* const* views, int32_t 
         // queries and accept bitsets → this device
         OSK_HIP(v->ws_qin.reserve(std::max<size_t>(16, qbytes)));
         OSK_HIP(hipMemcpyAsync(v->ws_qin.p, queries, qbytes, hipMemcpyHostToDevice, sts[i]));
-    }
-    rc = exchange_shard_index(comm, views, spr);
-    if (rc) return rc;
-    for (int i = 0; i < n_views; ++i) {
-        osk_view* v = views[i];
-        OSK_HIP(hipSetDevice(v->device));
         const int ns = (int)v->segs.size();
         const uint64_t* const* d_acc = nullptr;
         bool any = false;
@@ -474,7 +703,29 @@ int32_t osk_shards_search_merge(osk_comm* comm, osk_view* const* views, int32_t 
             d_acc = v->ws_accept_ptrs.as<const uint64_t*>();
         }
         seg_off += ns;
-        rc = search_padded(v, v->ws_qin.p, n_queries, k, d_acc, spr, sts[i]);
+        OSK_HIP(v->ws_keys.reserve(sizeof(uint64_t) * (size_t)n_queries * v->n_shards * k));
+        OSK_HIP(v->ws_counts.reserve(sizeof(int32_t) * (size_t)n_queries * v->n_shards));
+        rc = view_search_device(v, v->ws_qin.p, n_queries, k, d_acc, v->ws_keys.as<uint64_t>(),
+                                v->ws_counts.as<int32_t>(), nullptr, sts[i]);
+        if (rc) return rc;
+    }
+    // Shards per rank = the largest view of any rank.  Ranks may hold different numbers of shards (8 shards
+    // over 3 GPUs), so it is agreed on every call — a small all-gather on the exchange streams while the
+    // scans run — rather than cached (a cache would let ranks disagree on whether to exchange).
+    if (comm->world > 1) {
+        rc = agree_spr(comm, views, &spr);
+        if (rc) return rc;
+    }
+    const Block B = block_of(n_queries, k, spr);
+    uint64_t hw[kXHdrWords];
+    header_words(hw, ++comm->seq, n_queries, k, from, size, spr, views[0]->dim, views[0]->enc, comm->world);
+    for (int i = 0; i < n_views; ++i) {
+        osk_view* v = views[i];
+        OSK_HIP(hipSetDevice(v->device));
+        OSK_HIP(v->ws_xkeys.reserve(sizeof(uint64_t) * B.words));
+        OSK_HIP(launch_xhdr_fill(v->ws_xkeys.as<uint64_t>() + B.keys, hw, v->ws_qin.p, (int64_t)qbytes,
+                                 v->d_shard_index.as<int32_t>(), v->n_shards, spr, sts[i]));
+        rc = pad_lists(v, n_queries, k, spr, sts[i]);
         if (rc) return rc;
     }
     const uint64_t* image = views[0]->ws_xkeys.as<uint64_t>();
@@ -483,7 +734,7 @@ int32_t osk_shards_search_merge(osk_comm* comm, osk_view* const* views, int32_t 
             OSK_HIP(hipSetDevice(views[i]->device));
             OSK_HIP(enter_xstream(comm, i, sts[i]));
         }
-        rc = gather_keys(comm, views, n_queries, k, spr, comm->xstreams.data());
+        rc = gather_blocks(comm, views, B.words, comm->xstreams.data());
         if (rc) return rc;
         for (int i = 0; i < n_views; ++i) {   // every view's next search reuses its ws_xkeys / ws_xgath
             OSK_HIP(hipSetDevice(views[i]->device));
@@ -501,16 +752,20 @@ int32_t osk_shards_search_merge(osk_comm* comm, osk_view* const* views, int32_t 
                  o_tot = (o_cnt + b_cnt + 7) / 8 * 8, o_max = o_tot + b_tot, total_b = o_max + b_max;
     OSK_HIP(v0->ws_xout.reserve(total_b));
     char* ob = v0->ws_xout.as<char>();
-    OSK_HIP(launch_coord_reduce(image, nullptr, v0->d_xsi.as<int32_t>(), n_queries, comm->world, spr, k, from, size,
+    const int32_t* sidx = nullptr;
+    const XLayout x = image_layout(comm, image, B, &sidx);
+    OSK_HIP(launch_coord_reduce(image, nullptr, sidx, n_queries, comm->world, spr, k, from, size,
                                reinterpret_cast<float*>(ob + o_sc), reinterpret_cast<int32_t*>(ob + o_doc),
                                reinterpret_cast<int32_t*>(ob + o_sh), reinterpret_cast<int32_t*>(ob + o_cnt),
-                               reinterpret_cast<int64_t*>(ob + o_tot), reinterpret_cast<float*>(ob + o_max), sts[0]));
+                               reinterpret_cast<int64_t*>(ob + o_tot), reinterpret_cast<float*>(ob + o_max), sts[0], x));
     OSK_HIP(v0->h_stage.reserve(total_b));
     OSK_HIP(hipMemcpyAsync(v0->h_stage.p, ob, total_b, hipMemcpyDeviceToHost, sts[0]));
     for (int i = 0; i < n_views; ++i) {
         OSK_HIP(hipSetDevice(views[i]->device));
         OSK_HIP(hipStreamSynchronize(sts[i]));
     }
+    rc = poisoned(comm);   // the ranks issued different calls: no result
+    if (rc) return rc;
     const char* hb = static_cast<const char*>(v0->h_stage.p);
     std::memcpy(out_scores, hb + o_sc, b_sc);
     std::memcpy(out_docs, hb + o_doc, b_doc);

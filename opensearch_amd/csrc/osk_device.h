@@ -107,4 +107,28 @@ __device__ __forceinline__ float settle_exact(const float4* xr, bool valid, int 
     else return score_f32(sim, sum, qn, xn);
 }
 
+// The exchange header check of the coordinator reduce (one wave, lane = 0..63): 1 when some rank's
+// header words differ from rank 0's — the ranks did not issue the same call (osk_comm.hip).  The first
+// mismatch is recorded in x.err: [1, rank 0's call sequence number, the rank, its sequence number].
+__device__ __forceinline__ int xchg_header_check(const XLayout& x, int n_ranks, size_t rank_words, int lane) {
+    const int pairs = (n_ranks - 1) * kXHdrWords;
+    int bad_pair = 0x7FFFFFFF;
+    for (int e = lane; e < pairs; e += 64) {
+        const int r = 1 + e / kXHdrWords, w = e % kXHdrWords;
+        if (x.hdr[(size_t)r * rank_words + w] != x.hdr[w]) bad_pair = min(bad_pair, e);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) bad_pair = min(bad_pair, __shfl_xor(bad_pair, o));
+    if (bad_pair == 0x7FFFFFFF) return 0;
+    if (lane == 0 && x.err) {
+        const int r = 1 + bad_pair / kXHdrWords;
+        x.err[1] = (int64_t)x.hdr[1];
+        x.err[2] = r;
+        x.err[3] = (int64_t)x.hdr[(size_t)r * rank_words + 1];
+        __threadfence_system();
+        x.err[0] = 1;
+    }
+    return 1;
+}
+
 }  // namespace osk

@@ -264,17 +264,37 @@ struct SelParams {
 // one query: writer → radix select → collect → (re-score) → sort; cfg = the view's fp32/byte lane cfg
 hipError_t launch_select_one(const SelParams& p, int cfg, hipStream_t s, hipEvent_t ev_start = nullptr,
                              hipEvent_t ev_stop = nullptr);
+// Layout of a gathered multi-rank image (osk_comm.hip).  Default: rank r's lists [nq][sl][k] at
+// r·nq·sl·k words, shardIndex of slot (r, j) at shard_index[r·sl + j], no header.  The exchange gathers
+// one block per rank instead — [keys nq·sl·k][header kXHdrWords][shard indices sl int32] — so every
+// call carries its own shardIndex and a header that the reduce compares across ranks: a rank whose
+// header differs (another call sequence number, batch, k, from/size, shards per rank or query
+// fingerprint) makes every query's count −1 and records the mismatch in `err` (host memory).
+constexpr int kXHdrWords = 8;
+struct XHdrWords {
+    uint64_t w[kXHdrWords];
+};
+struct XLayout {
+    size_t rank_words = 0;            // u64 words per rank block (0 = nq·sl·k, no header)
+    int si_stride = 0;                // int32 between ranks' shard index arrays (0 = sl)
+    const uint64_t* hdr = nullptr;    // rank 0's header (rank r's at hdr + r·rank_words); null = none
+    int64_t* err = nullptr;           // [flag, rank-0 seq, first mismatching rank, its seq]
+};
 // The coordinator reduce: merge_coord (one workgroup per query, ≤ kCoordMax = 4096 hits ranked in LDS)
 // or, for more hits per query, merge_rank (launch_merge_rank); same layout, same outputs.
 hipError_t launch_coord_reduce(const uint64_t* shard_keys, const int32_t* shard_counts, const int32_t* shard_index,
                                int nq, int n_ranks, int sl, int k, int from, int size, float* scores, int32_t* docs,
                                int32_t* shard_out, int32_t* count, int64_t* total_hits, float* max_score,
-                               hipStream_t s);
+                               hipStream_t s, const XLayout& x = XLayout{});
 // coordinator reduce for lists of any length (merge_coord's layout and outputs; no 4096-hit limit)
 hipError_t launch_merge_rank(const uint64_t* keys, const int32_t* counts, const int32_t* shard_index, int nq,
                              int n_ranks, int sl, int k, int from, int size, float* scores, int32_t* docs,
                              int32_t* shard_out, int32_t* count, int64_t* total_hits, float* max_score,
-                             hipStream_t s);
+                             hipStream_t s, const XLayout& x = XLayout{});
+// The exchange block's trailer of this rank: header words w[0..kXHdrWords) with w[5] replaced by a
+// fingerprint of the query bytes, then the shard indices (sl slots: the view's n_shards, pads INT32_MAX).
+hipError_t launch_xhdr_fill(uint64_t* hdr, const uint64_t* w, const void* queries, int64_t query_bytes,
+                            const int32_t* shard_index, int n_shards, int sl, hipStream_t s);
 
 hipError_t launch_sq8_quantize(const float4* x, int64_t n, int units, int pitch, int units8, void* out8,
                                float4* aux, int mode, hipStream_t s);
@@ -331,6 +351,7 @@ struct Tuning {
                                           // first and scan them (osk_filter.hip); 0 = walk the bitset windows
     std::atomic<int> sq8_mfma_nt{1};      // A/B: non-temporal row loads in sq8_mfma
     std::atomic<int> i8_stream{1};        // byte fields, one query, no filter: scan_i8_stream (0 = scan_i8)
+    std::atomic<int> call_timing{0};      // host entries time each call on the device (osk_last_call_device_ns)
     std::atomic<int> sq8_mfma_ring{-1};   // sq8_mfma LDS-DMA ring slots per wave (≤ 256 dims, unfiltered):
                                           // -1 = as many as fit 2 workgroups per CU, 0 = off (register loads)
     std::atomic<int> sq8_mfma_queries{32};    // queries per sq8_mfma launch: 16 or 32 (two MFMA chains per row operand)
@@ -363,6 +384,6 @@ hipError_t launch_merge_coord(const uint64_t* shard_keys, const int32_t* shard_c
                               const int32_t* shard_index, int nq, int n_ranks, int sl, int k, int from,
                               int size, float* scores, int32_t* docs, int32_t* shard_out,
                               int32_t* count, int64_t* total_hits, float* max_score,
-                              hipStream_t s);
+                              hipStream_t s, const XLayout& x = XLayout{});
 
 }  // namespace osk

@@ -666,7 +666,7 @@ __global__ __launch_bounds__(kBlock) void merge_coord(const uint64_t* __restrict
                                                       int32_t* __restrict__ shard_out,
                                                       int32_t* __restrict__ count,
                                                       int64_t* __restrict__ total_hits,
-                                                      float* __restrict__ max_score) {
+                                                      float* __restrict__ max_score, XLayout x) {
     // empty slot = (su 0, shardIndex INT32_MAX, doc INT32_MAX): it never ranks above a hit
     __shared__ __attribute__((aligned(16))) uint32_t s_su[kCoordMax];
     __shared__ __attribute__((aligned(16))) int32_t s_sidx[kCoordMax];
@@ -675,15 +675,43 @@ __global__ __launch_bounds__(kBlock) void merge_coord(const uint64_t* __restrict
     // kernel 10 µs instead of 3.7 µs — tools/mc_micro.hip)
     __shared__ int s_red_n[kBlock / 64], s_red_total[kBlock / 64];
     __shared__ uint32_t s_red_max[kBlock / 64];
+    __shared__ int s_bad;
     const int b = blockIdx.x, tid = threadIdx.x, nq = gridDim.x;
     const int n_shards = n_ranks * sl;
     const int topn = min(k, from + size);
     const int n_slots = n_shards * topn;
     const int n4 = (n_slots + 3) & ~3;   // ≤ kCoordMax (the host checks n_slots ≤ 4096)
+    const size_t rw = x.rank_words ? x.rank_words : (size_t)nq * sl * k;
+    const int sis = x.si_stride ? x.si_stride : sl;
+    // list s = (rank r, local shard j): its count index (r·nq + b)·sl + j (counts exist only for
+    // contiguous images), its keys at r·rw + (b·sl + j)·k, its shardIndex at r·sis + j
     auto list = [&](int s) -> size_t {
         const int r = s / sl, j = s - r * sl;
         return ((size_t)(r * nq + b) * sl + j);
     };
+    auto keys_of = [&](int s) -> const uint64_t* {
+        const int r = s / sl, j = s - r * sl;
+        return shard_keys + (size_t)r * rw + ((size_t)b * sl + j) * k;
+    };
+    auto sidx_of = [&](int s) -> int32_t {
+        const int r = s / sl, j = s - r * sl;
+        return shard_index[r * sis + j];
+    };
+    if (x.hdr) {   // every rank's block must come from the same call (xchg_header_check)
+        if (tid < 64) {
+            const int bad = xchg_header_check(x, n_ranks, rw, tid);
+            if (tid == 0) s_bad = bad;
+        }
+        __syncthreads();
+        if (s_bad) {
+            if (tid == 0) {
+                count[b] = -1;
+                total_hits[b] = -1;
+                max_score[b] = __builtin_nanf("");
+            }
+            return;
+        }
+    }
     // stats (TopDocsStats): Σ hits over the shards, max of their top scores
     int part_total = 0;
     uint32_t part_max = 0u;
@@ -691,14 +719,14 @@ __global__ __launch_bounds__(kBlock) void merge_coord(const uint64_t* __restrict
         for (int s = tid; s < n_shards; s += kBlock) {
             const size_t o = list(s);
             const int c = shard_counts[o];
-            const uint64_t top = shard_keys[o * k];
+            const uint64_t top = keys_of(s)[0];
             part_total += c;
             if (c > 0) part_max = max(part_max, (uint32_t)(top >> 32));
         }
     } else if (topn < k) {   // (topn == k: the slot loop below sees every list entry)
         for (int e = tid; e < n_shards * k; e += kBlock) {
             const int s = e / k, i = e - s * k;
-            const uint64_t key = shard_keys[list(s) * k + i];
+            const uint64_t key = keys_of(s)[i];
             part_total += key != 0ull;
             if (i == 0 && key) part_max = max(part_max, (uint32_t)(key >> 32));
         }
@@ -708,10 +736,9 @@ __global__ __launch_bounds__(kBlock) void merge_coord(const uint64_t* __restrict
     for (int slot = tid; slot < n4; slot += kBlock) {
         const int s = slot / topn, i = slot - s * topn;
         const bool real = slot < n_slots;
-        const size_t o = real ? list(s) : 0;
-        const uint64_t key = real ? shard_keys[o * k + i] : 0ull;
-        const int c = real && shard_counts ? shard_counts[o] : 0;
-        const int32_t si = real ? shard_index[s] : 0;
+        const uint64_t key = real ? keys_of(s)[i] : 0ull;
+        const int c = real && shard_counts ? shard_counts[list(s)] : 0;
+        const int32_t si = real ? sidx_of(s) : 0;
         const bool hit = real && (shard_counts ? i < c : key != 0ull);
         s_su[slot] = hit ? (uint32_t)(key >> 32) : 0u;
         s_doc[slot] = hit ? key_doc(key) : INT32_MAX;
@@ -783,10 +810,60 @@ hipError_t launch_merge_coord(const uint64_t* shard_keys, const int32_t* shard_c
                               const int32_t* shard_index, int nq, int n_ranks, int sl, int k, int from,
                               int size, float* scores, int32_t* docs, int32_t* shard_out,
                               int32_t* count, int64_t* total_hits, float* max_score,
-                              hipStream_t s) {
+                              hipStream_t s, const XLayout& x) {
     hipLaunchKernelGGL(merge_coord, dim3(nq), dim3(kBlock), 0, s, shard_keys, shard_counts,
                        shard_index, n_ranks, sl, k, from, size, scores, docs, shard_out, count,
-                       total_hits, max_score);
+                       total_hits, max_score, x);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// multi-rank exchange trailer (osk_comm.hip): header + fingerprint of the query bytes + shard indices
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {   // splitmix64 finaliser
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// One workgroup.  The fingerprint is Σ mix64(word_i + i·φ) over the query's 32-bit words (a strided
+// sample of at most 16384 of them for large batches, plus the tail bytes and the byte count):
+// order-independent across threads, so identical bytes give identical fingerprints on every rank.
+__global__ __launch_bounds__(256) void xhdr_fill(uint64_t* __restrict__ hdr, XHdrWords w,
+                                                 const uint8_t* __restrict__ q, int64_t qbytes,
+                                                 const int32_t* __restrict__ shard_index, int n_shards, int sl) {
+    __shared__ uint64_t s_part[4];
+    const int tid = threadIdx.x;
+    const int64_t n32 = qbytes >> 2;
+    const int64_t n_sample = n32 < 16384 ? n32 : 16384;
+    const int64_t stride = n_sample ? n32 / n_sample : 1;
+    uint64_t h = 0;
+    for (int64_t i = tid; i < n_sample; i += 256) {
+        const int64_t e = i * stride;
+        uint32_t v;
+        __builtin_memcpy(&v, q + e * 4, 4);
+        h += mix64((uint64_t)v + (uint64_t)e * 0x9E3779B97F4A7C15ull);
+    }
+    if (tid < (int)(qbytes & 3)) h += mix64((uint64_t)q[n32 * 4 + tid] + 0xA5A5ull * (uint64_t)(tid + 1));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o);
+    if ((tid & 63) == 0) s_part[tid >> 6] = h;
+    __syncthreads();
+    if (tid < kXHdrWords) {
+        uint64_t v = w.w[tid];
+        if (tid == 5) v = mix64(s_part[0] + s_part[1] + s_part[2] + s_part[3] + (uint64_t)qbytes);
+        hdr[tid] = v;
+    }
+    int32_t* si = reinterpret_cast<int32_t*>(hdr + kXHdrWords);
+    for (int j = tid; j < sl; j += 256) si[j] = j < n_shards ? shard_index[j] : 0x7FFFFFFF;
+}
+
+hipError_t launch_xhdr_fill(uint64_t* hdr, const uint64_t* w, const void* queries, int64_t query_bytes,
+                            const int32_t* shard_index, int n_shards, int sl, hipStream_t s) {
+    XHdrWords hw;
+    for (int i = 0; i < kXHdrWords; ++i) hw.w[i] = w[i];
+    hipLaunchKernelGGL(xhdr_fill, dim3(1), dim3(256), 0, s, hdr, hw, static_cast<const uint8_t*>(queries),
+                       query_bytes, shard_index, n_shards, sl);
     return hipGetLastError();
 }
 

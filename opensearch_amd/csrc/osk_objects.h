@@ -158,6 +158,7 @@ struct osk_view {
     osk::DevBuf ws_cand, ws_q, ws_qnorm, ws_qin, ws_keys, ws_counts, ws_accept_ptrs, ws_accept,
         ws_out, ws_visited;
     osk::HostPinned h_stage;
+    osk::HostPinned h_accept_tab;     // osk_view_search's accept pointer table (source of an async copy)
     // batched MFMA path
     bool mfma_ready = false;
     int n_munits = 0;
@@ -191,11 +192,9 @@ struct osk_view {
     int n_gtiles = 0, n_gslices = 0;
     osk::DevBuf d_gtiles, d_gslices, d_gshard_slice_begin, d_seg_tiles;
     osk::DevBuf ws_tcnt, ws_scnt, ws_comp;
-    // multi-GPU exchange (osk_comm.hip): this rank's lists padded to the comm's shards per rank, the
-    // gathered image of every rank, and the shardIndex of every gathered slot (exchanged once per comm)
-    osk::DevBuf ws_xkeys, ws_xgath, d_xsi, ws_xout;
-    uint64_t xsi_comm = 0;            // id of the comm d_xsi was exchanged on (0 = none)
-    int xsi_spr = 0;                  // ...and its shards per rank
+    // multi-GPU exchange (osk_comm.hip): this rank's block (lists padded to the call's shards per rank,
+    // header, shard indices), the gathered blocks of every rank, the host entry's reduce outputs
+    osk::DevBuf ws_xkeys, ws_xgath, ws_xout, ws_xspr;
     std::mutex mu;
     // scan-kernel timing (osk_view_profile): a ring of (start, stop) event pairs, one per search call,
     // folded into scan_ms when a slot is reused (kEvRing calls later: long complete, no host wait) or
@@ -206,6 +205,7 @@ struct osk_view {
     bool ev_pending[kEvRing] = {};
     int64_t ev_next = 0;                  // calls started since enabling
     hipEvent_t ev0 = nullptr, ev1 = nullptr;   // the current call's pair
+    hipEvent_t ev_call[2] = {};                 // host entries' per-call device time (tune call_timing)
     double scan_ms = 0.0;
     int64_t scan_calls = 0;
     const uint64_t* h_accept_ptr = nullptr;   // source of osk_seg_search's one-pointer accept table copy

@@ -663,11 +663,19 @@ struct MergeArgs {
     int32_t* count;
     int64_t* total_hits;
     float* max_score;
+    XLayout x;
+    size_t rw;                  // u64 words per rank block
+    int sis;                    // int32 between ranks' shard index arrays
 };
 
+// keys of list s = (rank r, local shard j) of query b
 __device__ __forceinline__ size_t merge_list(const MergeArgs& a, int b, int s) {
     const int r = s / a.sl, j = s - r * a.sl;
-    return ((size_t)(r * a.nq + b) * a.sl + j) * a.k;
+    return (size_t)r * a.rw + ((size_t)b * a.sl + j) * a.k;
+}
+__device__ __forceinline__ int32_t merge_sidx(const MergeArgs& a, int s) {
+    const int r = s / a.sl, j = s - r * a.sl;
+    return a.shard_index[r * a.sis + j];
 }
 
 // hits of list s (not cut): the count, or the number of non-zero keys (binary search)
@@ -697,6 +705,12 @@ __device__ __forceinline__ int count_better(const uint64_t* l, int n, uint32_t s
 }
 
 __global__ __launch_bounds__(kSelThreads) void merge_rank(MergeArgs a) {
+    if (a.x.hdr) {   // mismatched exchange blocks: merge_stats writes count −1, nothing to rank
+        bool bad = false;
+        for (int e = 0; e < (a.n_ranks - 1) * kXHdrWords && !bad; ++e)
+            bad = a.x.hdr[(size_t)(1 + e / kXHdrWords) * a.rw + e % kXHdrWords] != a.x.hdr[e % kXHdrWords];
+        if (bad) return;
+    }
     const int b = blockIdx.y;
     const int topn = min(a.k, a.from + a.size);
     const int S = a.n_ranks * a.sl;
@@ -707,14 +721,14 @@ __global__ __launch_bounds__(kSelThreads) void merge_rank(MergeArgs a) {
     if (i >= cs) return;
     const uint64_t key = a.keys[merge_list(a, b, s) + i];
     const uint32_t su = (uint32_t)(key >> 32);
-    const int32_t si = a.shard_index[s];
+    const int32_t si = merge_sidx(a, s);
     int64_t rank = i;
     for (int s2 = 0; s2 < S && rank < a.from + a.size; ++s2) {
         if (s2 == s) continue;
         const int c2 = min(merge_hits(a, b, s2), topn);
         // another shard's hit ranks before this one on a higher score, or an equal score with a
         // lower shardIndex ([L] TopDocs.merge tie-break; shard indices are distinct)
-        rank += count_better(a.keys + merge_list(a, b, s2), c2, su, a.shard_index[s2] < si);
+        rank += count_better(a.keys + merge_list(a, b, s2), c2, su, merge_sidx(a, s2) < si);
     }
     if (rank >= a.from && rank < a.from + a.size) {
         const size_t o = (size_t)b * a.size + (rank - a.from);
@@ -728,7 +742,23 @@ __global__ __launch_bounds__(kSelThreads) void merge_rank(MergeArgs a) {
 __global__ __launch_bounds__(kSelThreads) void merge_stats(MergeArgs a) {
     __shared__ int64_t s_tot[kSelThreads / 64], s_cut[kSelThreads / 64];
     __shared__ uint32_t s_max[kSelThreads / 64];
+    __shared__ int s_bad;
     const int b = blockIdx.x, tid = threadIdx.x;
+    if (a.x.hdr) {
+        if (tid < 64) {
+            const int bad = xchg_header_check(a.x, a.n_ranks, a.rw, tid);
+            if (tid == 0) s_bad = bad;
+        }
+        __syncthreads();
+        if (s_bad) {
+            if (tid == 0) {
+                a.count[b] = -1;
+                a.total_hits[b] = -1;
+                a.max_score[b] = __builtin_nanf("");
+            }
+            return;
+        }
+    }
     const int topn = min(a.k, a.from + a.size);
     const int S = a.n_ranks * a.sl;
     int64_t tot = 0, cut = 0;
@@ -826,9 +856,10 @@ hipError_t launch_select_one(const SelParams& p, int cfg, hipStream_t s, hipEven
 hipError_t launch_merge_rank(const uint64_t* keys, const int32_t* counts, const int32_t* shard_index, int nq,
                              int n_ranks, int sl, int k, int from, int size, float* scores, int32_t* docs,
                              int32_t* shard_out, int32_t* count, int64_t* total_hits, float* max_score,
-                             hipStream_t s) {
+                             hipStream_t s, const XLayout& x) {
     MergeArgs a{keys, counts, shard_index, n_ranks, sl, k, from, size, nq, scores, docs, shard_out, count,
-                total_hits, max_score};
+                total_hits, max_score, x, x.rank_words ? x.rank_words : (size_t)nq * sl * k,
+                x.si_stride ? x.si_stride : sl};
     const int topn = std::min(k, from + size);
     const int64_t n = (int64_t)n_ranks * sl * topn;
     hipLaunchKernelGGL(merge_stats, dim3(nq), dim3(kSelThreads), 0, s, a);
@@ -841,15 +872,15 @@ hipError_t launch_merge_rank(const uint64_t* keys, const int32_t* counts, const 
 hipError_t launch_coord_reduce(const uint64_t* shard_keys, const int32_t* shard_counts, const int32_t* shard_index,
                                int nq, int n_ranks, int sl, int k, int from, int size, float* scores, int32_t* docs,
                                int32_t* shard_out, int32_t* count, int64_t* total_hits, float* max_score,
-                               hipStream_t s) {
+                               hipStream_t s, const XLayout& x) {
     // merge_coord ranks every hit against every other in one workgroup: best for few hits (k = 10:
     // 80 per query); beyond a few hundred the parallel binary-search ranking wins (k = 100, 8 shards:
     // 105 µs → ≈10 µs)
     if ((int64_t)n_ranks * sl * std::min(k, from + size) <= 256)
         return launch_merge_coord(shard_keys, shard_counts, shard_index, nq, n_ranks, sl, k, from, size, scores, docs,
-                                  shard_out, count, total_hits, max_score, s);
+                                  shard_out, count, total_hits, max_score, s, x);
     return launch_merge_rank(shard_keys, shard_counts, shard_index, nq, n_ranks, sl, k, from, size, scores, docs,
-                             shard_out, count, total_hits, max_score, s);
+                             shard_out, count, total_hits, max_score, s, x);
 }
 
 }  // namespace osk

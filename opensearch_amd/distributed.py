@@ -61,6 +61,26 @@ class DeviceComm:
         return cls(h.value)
 
     @classmethod
+    def init_loopback(cls, device: int, rank: int, world: int, name: str, slot_bytes: int = 1 << 22) -> "DeviceComm":
+        """Testing build only (inside `_lib.testing()`): `world` processes that may share one GPU, the
+        all-gather through the POSIX shared-memory segment `name` ("/..."), so the world > 1 exchange
+        runs on a one-GPU box."""
+        raw = name.encode() + b"\0"
+        if len(raw) > _lib.OSK_COMM_ID_BYTES or not name.startswith("/"):
+            raise ValueError("loopback name: '/...' of at most 127 bytes")
+        buf = (C.c_uint8 * _lib.OSK_COMM_ID_BYTES).from_buffer_copy(raw.ljust(_lib.OSK_COMM_ID_BYTES, b"\0"))
+        h = C.c_void_p()
+        check(lib().osk_comm_init_loopback(device, rank, world, buf, slot_bytes, C.byref(h)))
+        return cls(h.value)
+
+    def status(self) -> tuple[int, list[int]]:
+        """(return code of osk_comm_status, [flag, rank 0's call number, differing rank, its call number]).
+        Synchronise the calls' streams first."""
+        info = (C.c_int64 * 4)()
+        rc = lib().osk_comm_status(self._h, info)
+        return rc, list(info)
+
+    @classmethod
     def from_process_group(cls, device: int, group=None) -> "DeviceComm":
         """Rank 0 makes the id; torch.distributed (any backend) hands it to the other ranks."""
         rank, world = dist.get_rank(group), dist.get_world_size(group)

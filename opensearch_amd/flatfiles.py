@@ -154,29 +154,35 @@ class _In:
         return self._take(self.vint()).decode()
 
 
-def _write_header(o: _Out, codec: str, segment_id: bytes, suffix: str):
+def _write_header(o: _Out, codec: str, segment_id: bytes, suffix: str, version: int = VERSION):
+    """[L] CodecUtil.writeIndexHeader: BE magic, codec name (vInt length + bytes), BE version, the
+    16-byte segment id, suffix (one length byte + bytes)."""
     o.be_int(CODEC_MAGIC)
     o.string(codec)
-    o.be_int(VERSION)
+    o.be_int(version)
     o.raw(segment_id)
     raw = suffix.encode()
     o.b.append(len(raw))
     o.raw(raw)
 
 
-def _check_header(i: _In, codec: str, segment_id: bytes, suffix: str):
+def _check_header(i: _In, codec: str, segment_id: bytes, suffix: str, min_version: int = VERSION,
+                  max_version: int = VERSION) -> int:
+    """[L] CodecUtil.checkIndexHeader; returns the version."""
     if i.be_int() != CODEC_MAGIC:
         raise CorruptIndexError("codec header mismatch")
     name = i.string()
     if name != codec:
         raise CorruptIndexError(f"codec mismatch: expected {codec!r}, got {name!r}")
-    if i.be_int() != VERSION:
-        raise CorruptIndexError("unsupported version")
+    version = i.be_int()
+    if not min_version <= version <= max_version:
+        raise CorruptIndexError(f"unsupported version {version}")
     if i._take(16) != segment_id:
         raise CorruptIndexError("segment id mismatch")
     n = i._take(1)[0]
     if i._take(n).decode() != suffix:
         raise CorruptIndexError("segment suffix mismatch")
+    return version
 
 
 def _write_footer(o: _Out):

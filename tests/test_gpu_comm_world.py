@@ -1,0 +1,205 @@
+"""The multi-rank exchange of osk_comm.hip at world 2, 3 and 8, on ONE GPU.
+
+RCCL refuses two ranks on one device, so the testing build's loopback transport
+(`osk_comm_init_loopback`, libosknn_testing.so) stands in for ncclAllGather: every rank is its own
+process, stages its shards on the box's one GPU and runs exactly the world > 1 code of
+`osk_shards_search_merge_device` / `osk_shards_search_merge` — per-call exchange blocks (lists padded
+to shards-per-rank, header, shard indices), the gather on the communicator's exchange stream, and the
+device coordinator reduce with the cross-rank header check.  Only the byte transport differs from the
+8-GPU node.
+
+* parity: the merged hits of every rank equal the N = 1 oracle merge (per-shard exactSearch +
+  TopDocs.merge with shardIndex = global shard number) bit for bit, for both entries, from/size cuts
+  and a k = 100 call that takes the merge_rank reduce;
+* a rank that recreates its view between calls (a refresh on one node only) still merges correctly —
+  the shard indices travel with every call, nothing is cached per (communicator, view);
+* ranks that issue different calls (queries in another order, another from) get count −1 and a
+  poisoned communicator (OSK_ERR_INVALID), not a merge of unrelated lists.
+
+Reference semantics: S/action/search/SearchPhaseController.java:224-253 (mergeTopDocs, setShardIndex),
+S/action/search/AbstractSearchAsyncAction.java:262-268 (one request per shard copy, loop index =
+shardIndex).
+"""
+import multiprocessing as mp
+import os
+import traceback
+import uuid
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+N_SHARDS = 8
+DIM, SIM, SEED, DIST = 100, 2, 77, 3   # COSINE over L2-normalised Irwin–Hall rows
+SIZES = [2500 + 611 * s for s in range(N_SHARDS)]
+ROW0 = np.concatenate([[0], np.cumsum(SIZES)]).astype(np.int64)
+# (n_queries, k, from, size, entry, query seed)
+CALLS = [(1, 10, 0, 10, "device", 5), (3, 10, 2, 8, "device", 6), (2, 30, 5, 20, "device", 7),
+         (4, 10, 0, 10, "host", 8), (1, 100, 0, 100, "device", 9), (2, 12, 0, 12, "host", 10)]
+
+
+def _queries(nq, qseed):
+    return O.synth(0, nq, DIM, 1000 + qseed, DIST)
+
+
+def _worker(rank, world, name, mode, out_q):
+    try:
+        import ctypes as C
+
+        import torch
+
+        from opensearch_amd import _lib, distributed as D
+        from opensearch_amd._lib import check, ptr
+        with _lib.testing():
+            L = _lib.lib()
+            shards = D.owned_shards(rank, N_SHARDS, world)
+            spr = D.max_shards_per_rank(N_SHARDS, world)
+            segs = []
+            for s in shards:
+                h = C.c_void_p()
+                check(L.osk_seg_synth(0, SIZES[s], DIM, _lib.FLOAT32, SIM, SEED, DIST, int(ROW0[s]), C.byref(h)))
+                segs.append(h.value)
+
+            def make_view():
+                arr = (C.c_void_p * len(segs))(*segs)
+                seg_shard = np.arange(len(segs), dtype=np.int32)
+                base = np.zeros(len(segs), np.int32)
+                sidx = np.asarray(shards, np.int32)
+                v = C.c_void_p()
+                check(L.osk_view_create(arr, len(segs), ptr(seg_shard), ptr(base), len(segs), ptr(sidx), C.byref(v)))
+                return v
+
+            view = make_view()
+            comm = D.DeviceComm.init_loopback(0, rank, world, name)
+            stream = torch.cuda.Stream()
+
+            def device_call(nq, k, from_, size, qs):
+                dq = torch.from_numpy(_queries(nq, qs)).cuda()
+                torch.cuda.synchronize()
+                step = D.ShardSearchMerge(comm, view, spr, nq, k, from_, size, device=0)
+                res = step(dq.data_ptr(), stream.cuda_stream)
+                stream.synchronize()
+                return [t.cpu().numpy().copy() for t in res]
+
+            results = []
+            if mode in ("parity", "recreate"):
+                for i, (nq, k, from_, size, entry, qs) in enumerate(CALLS):
+                    if mode == "recreate" and rank == 1 and i % 2 == 1:   # this rank alone refreshes
+                        check(L.osk_view_release(view))
+                        view = make_view()
+                    if entry == "device":
+                        results.append(device_call(nq, k, from_, size, qs))
+                    else:
+                        results.append(list(D.shards_search_merge(comm, [view], _queries(nq, qs), k, from_, size)))
+            elif mode == "misorder":
+                # rank 0 issues query A then B, rank 1 B then A: the first call's blocks differ
+                order = (5, 6) if rank == 0 else (6, 5)
+                first = device_call(1, 10, 0, 10, order[0])
+                rc, info = comm.status()
+                try:
+                    device_call(1, 10, 0, 10, order[1])
+                    second = None
+                except _lib.OskError as e:
+                    second = e.code
+                results = [int(first[3][0]), int(first[4][0]), rc, info, second]
+            elif mode == "misfrom":
+                # host entry, same block size, another `from` on rank 1
+                from_ = 0 if rank == 0 else 2
+                try:
+                    D.shards_search_merge(comm, [view], _queries(2, 5), 10, from_, 8)
+                    results = ["no error"]
+                except _lib.OskError as e:
+                    results = [e.code, str(e)]
+            comm.close()
+            check(L.osk_view_release(view))
+            for h in segs:
+                check(L.osk_seg_release(C.c_void_p(h)))
+        out_q.put((rank, results))
+    except BaseException:
+        out_q.put((rank, "ERROR " + traceback.format_exc()))
+
+
+def _run(world, mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    name = f"/osk_lb_{os.getpid()}_{uuid.uuid4().hex[:10]}"
+    procs = [ctx.Process(target=_worker, args=(r, world, name, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            r, res = q.get(timeout=240)
+            out[r] = res
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+        try:
+            os.unlink("/dev/shm" + name)
+        except OSError:
+            pass
+    for r in range(world):
+        assert not (isinstance(out[r], str) and out[r].startswith("ERROR")), out[r]
+    return out
+
+
+def _oracle(nq, k, from_, size, qs):
+    queries = _queries(nq, qs)
+    want = []
+    for i in range(nq):
+        lists = []
+        for s in range(N_SHARDS):
+            rows = O.synth(int(ROW0[s]), SIZES[s], DIM, SEED, DIST)
+            lists.append(O.exact_search(rows, queries[i], k, SIM)[:2])   # totalHits counts all k per shard
+        want.append(O.topdocs_merge(lists, from_, size, list(range(N_SHARDS))))
+    return want
+
+
+@pytest.fixture(scope="module")
+def expected():
+    return [_oracle(nq, k, f, sz, qs) for (nq, k, f, sz, _, qs) in CALLS]
+
+
+def _check(results, expected):
+    for (nq, k, from_, size, entry, _), got, want in zip(CALLS, results, expected):
+        sc, dc, sh, cnt, tot, mx = got
+        for i in range(nq):
+            es, ed, esh, et, em = want[i]
+            n = int(cnt[i])
+            assert n == len(ed), (entry, k, i)
+            assert np.array_equal(dc[i, :n], ed) and np.array_equal(sh[i, :n], esh), (entry, k, i)
+            assert np.array_equal(sc[i, :n].view(np.uint32), es.view(np.uint32)), (entry, k, i)
+            assert int(tot[i]) == et and np.float32(mx[i]).view(np.uint32) == np.float32(em).view(np.uint32)
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_world_n_merge_equals_oracle(world, expected):
+    out = _run(world, "parity")
+    for r in range(world):
+        _check(out[r], expected)
+
+
+def test_one_rank_recreates_its_view_between_calls(expected):
+    out = _run(2, "recreate")
+    for r in range(2):
+        _check(out[r], expected)
+
+
+def test_misordered_calls_poison_the_communicator():
+    out = _run(2, "misorder")
+    for r in range(2):
+        count, total, rc, info, second = out[r]
+        assert count == -1 and total == -1
+        assert rc == -1 and info[0] == 1 and info[1] == 1 and info[2] == 1 and info[3] == 1
+        assert second == -1   # OSK_ERR_INVALID: refused, no collective issued
+
+
+def test_mismatched_from_fails_the_host_entry():
+    out = _run(2, "misfrom")
+    for r in range(2):
+        assert out[r][0] == -1 and "poisoned" in out[r][1], out[r]

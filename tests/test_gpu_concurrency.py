@@ -280,3 +280,62 @@ def test_batched_host_call_errors_stay_with_their_caller():
     finally:
         ds.close()
         r.close()
+
+
+def test_counters_sum_over_leased_replicas_and_call_timing():
+    """Counters of a view sum over the replica slots its host entries leased (osk_view_counter), and the
+    per-call device time of a host search is exported for the query profiler (osk_last_call_device_ns;
+    SearchPlugin.getQueryProfileMetricsProvider, S/plugins/SearchPlugin.java:108)."""
+    import time
+    rows = O.synth(0, 60000, 256, 240, 3)
+    r = LU.GpuFlatVectorsReader("v", rows, COS)
+    ds = LU.DeviceShardSet([[LU.LeafReaderContext(0, 0, r)]], [0])
+    pool = O.synth(0, 16, 256, 241, 3)
+    _lib.tune("host_batching", 0)
+    try:
+        c0 = ds.counter("sq8_calls")
+        barrier = threading.Barrier(8)
+
+        def worker(t):
+            barrier.wait()
+            for rep in range(10):
+                ds.search(pool[(t + rep) % 16:(t + rep) % 16 + 1], 10, 0, 10)
+
+        threads = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+        for th in threads:
+            th.start()
+        for th in threads:
+            th.join()
+        assert ds.counter("sq8_calls") - c0 == 80   # every call, whichever slot served it
+        assert ds.counter("host_slots") >= 1
+        _lib.tune("call_timing", 0)
+        ds.search(pool[:1], 10, 0, 10)
+        assert _lib.last_call_device_ns() == (-1, 0)
+        _lib.tune("call_timing", 1)
+        t0 = time.perf_counter_ns()
+        want = ds.search(pool[:1], 10, 0, 10)
+        wall = time.perf_counter_ns() - t0
+        ns, shared = _lib.last_call_device_ns()
+        assert shared == 1 and 0 < ns <= wall
+        # the timing knob changes nothing but the timing
+        assert same(ds.search(pool[:1], 10, 0, 10), want)
+        # batched host calls report the shared launch chain's time and how many requests it served
+        _lib.tune("host_batching", 1)
+        got = {}
+
+        def timed(t):
+            barrier.wait()
+            ds.search(pool[t:t + 1], 10, 0, 10)
+            got[t] = _lib.last_call_device_ns()
+
+        threads = [threading.Thread(target=timed, args=(t,)) for t in range(8)]
+        for th in threads:
+            th.start()
+        for th in threads:
+            th.join()
+        assert all(ns > 0 and 1 <= sh <= 8 for ns, sh in got.values()), got
+    finally:
+        _lib.tune("call_timing", 0)
+        _lib.tune("host_batching", 1)
+        ds.close()
+        r.close()
