@@ -41,6 +41,7 @@ import json
 import os
 import sys
 import time
+from pathlib import Path
 
 import numpy as np
 import torch
@@ -108,17 +109,65 @@ def cpu_info() -> tuple[str, str]:
     return model, isa
 
 
-def cpu_baseline(sample_rows: int, n_queries: int, threads: int, passes: int = 9) -> dict:
+def _cpulist(text: str) -> list[int]:
+    out = []
+    for part in text.strip().split(","):
+        if part:
+            a, _, b = part.partition("-")
+            out += list(range(int(a), int(b or a) + 1))
+    return out
+
+
+def numa_cores(threads: int) -> tuple[int, list[int]]:
+    """One NUMA node's CPUs for the baseline's threads: the node with the most CPUs this process may use,
+    one hardware thread per physical core first (SMT siblings only if the node has too few cores)."""
+    allowed = os.sched_getaffinity(0)
+    best = (-1, [])
+    for d in sorted(Path("/sys/devices/system/node").glob("node[0-9]*")):
+        try:
+            cpus = [c for c in _cpulist((d / "cpulist").read_text()) if c in allowed]
+        except OSError:
+            continue
+        if len(cpus) > len(best[1]):
+            best = (int(d.name[4:]), cpus)
+    node, cpus = best
+    if not cpus:
+        return -1, sorted(allowed)[:threads]
+    first, rest = [], []
+    for c in cpus:
+        try:
+            sib = _cpulist(Path(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list").read_text())
+        except OSError:
+            sib = [c]
+        (first if c == min(s for s in sib if s in allowed or s == c) else rest).append(c)
+    return node, (first + rest)[:threads]
+
+
+def cpu_baseline(sample_rows: int, n_queries: int, threads: int, passes: int = 15) -> dict:
     """The oracle's Lucene-equivalent exact search (Panama-512 summation order, one thread per row slice
     like the index_searcher pool's slices) over a bounded C3 sample that is far larger than the host's
-    caches, timed as the median of `passes` passes on `threads` threads (the best pass beside it: the box's
-    host cores are shared, so single passes vary), and again on 1 thread."""
+    caches.  The AVX-512 build of the restatement runs where the host has AVX-512 (Lucene's 16-lane
+    FLOAT_SPECIES there); the threads are pinned to one NUMA node (the sample is first-touched there), and
+    `passes` passes are timed on `threads` threads (median reported; min/max beside it: the box's host is
+    shared), then 3 on 1 thread."""
     from oracle import oracle as O
+    isa = O.use_build("v4")
+    node, cores = numa_cores(threads)
+    prev_aff = os.sched_getaffinity(0)
+    threads = len(cores)
+    os.sched_setaffinity(0, cores)   # this thread, and the threads it creates, on the node's cores
+    try:
+        return _cpu_baseline_pinned(O, sample_rows, n_queries, threads, passes, isa, node, cores)
+    finally:
+        os.sched_setaffinity(0, prev_aff)
+
+
+def _cpu_baseline_pinned(O, sample_rows, n_queries, threads, passes, isa, node, cores) -> dict:
     t0 = time.perf_counter()
     rows = O.synth(0, sample_rows, DIM, 42, 3)
     qs = O.synth(0, n_queries, DIM, 43, 3)
     log(f"cpu_baseline: generated {sample_rows}x{DIM} in {time.perf_counter() - t0:.1f}s")
-    O.knn_batch(rows, qs[:threads], K, 2, O.ORDER_PANAMA512, threads)   # warm-up (pages, threads)
+    O.knn_batch(rows, qs, K, 2, O.ORDER_PANAMA512, threads)   # warm-up pass (pages, threads, clocks)
 
     def median_qps(nq, nthreads, n_passes):
         rates = []
@@ -133,14 +182,17 @@ def cpu_baseline(sample_rows: int, n_queries: int, threads: int, passes: int = 9
     qps_1, rates_1 = median_qps(nq1, 1, 3)
     total_rows = N_SHARDS * ROWS_PER_SHARD
     scale = sample_rows / total_rows
-    model, isa = cpu_info()
+    model, _ = cpu_info()
     return {
         "value": qps_n * scale,
         "unit": "queries/s",
         "cores": threads,
         "kind": "port",
         "value_1thread": qps_1 * scale,
+        "min_max_of_passes": [min(rates_n) * scale, max(rates_n) * scale],
         "host_cpus": os.cpu_count(),
+        "numa_node": node,
+        "pinned_cpus": cores,
         "cpu_model": model,
         "isa": isa,
         "passes_qps_on_sample": [round(r, 2) for r in rates_n],

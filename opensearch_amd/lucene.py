@@ -285,12 +285,74 @@ class _KnnVectorQuery:
 
 
 class KnnFloatVectorQuery(_KnnVectorQuery):
-    """[L] KnnFloatVectorQuery(field, float[] target, k, filter)."""
+    """[L] KnnFloatVectorQuery(field, float[] target, k, filter).
+
+    Its rewrite is Lucene's per-leaf route: one KnnVectorsReader.search per leaf, run as per-leaf tasks
+    on the index_searcher pool under concurrent segment search (S/search/DefaultSearchContext.java:257-267).
+    Real Lucene also never calls the reader for a filtered leaf whose accepted docs number ≤ k: it runs
+    exactSearch on the CPU over FloatVectorValues.scorer (Panama order, within 1e-5 of the device but not
+    bit-identical).  GpuKnnFloatVectorQuery below is the plugin's query that routes both onto the device."""
     encoding = VectorEncoding.FLOAT32
 
 
 class KnnByteVectorQuery(_KnnVectorQuery):
     """[L] KnnByteVectorQuery(field, byte[] target, k, filter)."""
+    encoding = VectorEncoding.BYTE
+
+
+class _GpuKnnVectorQuery:
+    """The plugin's k-NN query (`GpuKnnFloatVectorQuery extends KnnFloatVectorQuery`):
+
+    * rewrite: ONE device call per shard — osk_view_search over a view of all the shard's leaves, cached
+      per point-in-time reader (the leaves' readers and docBases), with each leaf's AcceptDocs
+      (liveDocs ∩ filter) pushed down as a bitset — instead of one KnnVectorsReader.search per leaf.
+      The device merges the leaves ([L] TopDocs.merge(k, perLeaf): score desc, doc asc) in the same call;
+    * every filtered leaf goes to the device whatever its cost, so Lucene's `cost ≤ k` CPU exactSearch
+      branch never runs; `exact_search` (the override of [L] AbstractKnnVectorQuery.exactSearch) serves a
+      caller that still asks for a per-leaf exact search, on the device.
+    Results are identical to the per-leaf route (every device path is exact in the device order)."""
+    _views: dict = {}
+
+    def _shard_view(self, leaves: Sequence[LeafReaderContext]) -> "DeviceShardSet":
+        key = tuple((id(lf.reader), lf.reader.handle, lf.doc_base) for lf in leaves)
+        v = _GpuKnnVectorQuery._views.get(key)
+        if v is None:
+            v = DeviceShardSet([list(leaves)], [0])
+            _GpuKnnVectorQuery._views[key] = v
+        return v
+
+    @classmethod
+    def release_views(cls) -> None:
+        """The reader-closed listener: drop the cached views (the segments stay with their readers)."""
+        for v in cls._views.values():
+            v.close()
+        cls._views = {}
+
+    def rewrite(self, leaves: Iterable[LeafReaderContext]) -> TopDocs:
+        leaves = [lf for lf in leaves if lf.reader.field == self.field]
+        if not leaves:
+            return TopDocs(TotalHits(0), [])
+        view = self._shard_view(leaves)
+        accept = [self._accept(lf) for lf in leaves]
+        if all(a is None for a in accept):
+            accept = None
+        s, d, _, c, _, _ = view.search(self.target, self.k, 0, self.k, accept=accept)
+        n = int(c[0])
+        return TopDocs(TotalHits(n), [ScoreDoc(int(d[0, i]), float(s[0, i])) for i in range(n)])
+
+    def exact_search(self, leaf: LeafReaderContext, accept: np.ndarray | None) -> TopDocs:
+        """[L] AbstractKnnVectorQuery.exactSearch(context, acceptIterator, timeout) on the device."""
+        td = leaf.reader.search(self.field, self.target, self.k, accept)
+        for sd in td.score_docs:
+            sd.doc += leaf.doc_base
+        return td
+
+
+class GpuKnnFloatVectorQuery(_GpuKnnVectorQuery, KnnFloatVectorQuery):
+    encoding = VectorEncoding.FLOAT32
+
+
+class GpuKnnByteVectorQuery(_GpuKnnVectorQuery, KnnByteVectorQuery):
     encoding = VectorEncoding.BYTE
 
 

@@ -103,25 +103,37 @@ static void lane_cfg(int units, int* L, int* V) {
 
 static inline float elem(const float* v, int dim, int i) { return i < dim ? v[i] : 0.0f; }
 
-/* kind 0: Σ a·b, kind 1: Σ (a−b)² — in the device lane layout */
+/* kind 0: Σ a·b, kind 1: Σ (a−b)² — in the device lane layout.  Lane t keeps 4 fma chains over
+ * units t, t+L, t+2L, …; chain e of lane t sees elements 4(t + jL) + e, j = 0..V−1, i.e. position
+ * i = 4t + e of the j-th contiguous block of 4L elements — so the 4L chains are one contiguous fma
+ * sweep per block (vectorisable, same arithmetic).  Then (x+y)+(z+w) per lane and an xor-butterfly
+ * over the L lanes. */
 static float device_sum(const float* a, const float* b, int dim, int kind) {
     int L, V;
     const int units = (dim + 3) / 4;
     lane_cfg(units, &L, &V);
-    float p[64];
-    for (int t = 0; t < L; ++t) {
-        float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        for (int j = 0; j < V; ++j) {
-            const int f = t + j * L;
-            for (int e = 0; e < 4; ++e) {
-                float x = 0.0f, y = 0.0f;
-                if (f < units) { x = elem(a, dim, 4 * f + e); y = elem(b, dim, 4 * f + e); }
-                if (kind == 0) acc[e] = fmaf(x, y, acc[e]);
-                else { const float d = x - y; acc[e] = fmaf(d, d, acc[e]); }
+    const int W = 4 * L;
+    float acc[256];
+    for (int i = 0; i < W; ++i) acc[i] = 0.0f;
+    for (int j = 0; j < V; ++j) {
+        const int base = j * W;
+        if (base + W <= dim) {
+            const float* x = a + base;
+            const float* y = b + base;
+            if (kind == 0)
+                for (int i = 0; i < W; ++i) acc[i] = fmaf(x[i], y[i], acc[i]);
+            else
+                for (int i = 0; i < W; ++i) { const float d = x[i] - y[i]; acc[i] = fmaf(d, d, acc[i]); }
+        } else {   /* the ragged tail block (zeros past dim, as the padded rows) */
+            for (int i = 0; i < W; ++i) {
+                const float x = elem(a, dim, base + i), y = elem(b, dim, base + i);
+                if (kind == 0) acc[i] = fmaf(x, y, acc[i]);
+                else { const float d = x - y; acc[i] = fmaf(d, d, acc[i]); }
             }
         }
-        p[t] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
     }
+    float p[64];
+    for (int t = 0; t < L; ++t) p[t] = (acc[4 * t] + acc[4 * t + 1]) + (acc[4 * t + 2] + acc[4 * t + 3]);
     for (int m = 1; m < L; m <<= 1) {
         float nx[64];
         for (int t = 0; t < L; ++t) nx[t] = p[t] + p[t ^ m];

@@ -23,15 +23,45 @@ ORDER_PANAMA512 = 2
 ORDER_SCALAR_NOFMA = 3      # Lucene's orders where Constants.HAS_FAST_*_FMA is false: multiply, then add
 ORDER_PANAMA512_NOFMA = 4
 
+LIB_V4_PATH = HERE / "liboracle_v4.so"   # same source, x86-64-v4 (AVX-512) build: the CPU baseline's
 _lock = threading.Lock()
 _lib = None
+_variant = "v3"
 
 
 def build(force: bool = False) -> Path:
     src = HERE / "lucene_oracle.c"
-    if force or not LIB_PATH.exists() or LIB_PATH.stat().st_mtime < src.stat().st_mtime:
+    stale = any(not p.exists() or p.stat().st_mtime < src.stat().st_mtime for p in (LIB_PATH, LIB_V4_PATH))
+    if force or stale:
         subprocess.run(["make", "-s", "-B" if force else "-s", "-C", str(HERE)], check=True)
     return LIB_PATH
+
+
+def host_has_avx512() -> bool:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("flags"):
+                    return " avx512f " in line + " "
+    except OSError:
+        pass
+    return False
+
+
+def use_build(variant: str) -> str:
+    """Select the build before the first call: "v4" (AVX-512, only where the host has avx512f) or "v3"
+    (AVX2, the default).  Returns the ISA label of the build that will be loaded."""
+    global _variant
+    with _lock:
+        if _lib is not None:
+            raise RuntimeError("the oracle library is already loaded")
+        _variant = "v4" if variant == "v4" and host_has_avx512() else "v3"
+    return isa()
+
+
+def isa() -> str:
+    return ("AVX-512, x86-64-v4 build (16 fp32 lanes)" if _variant == "v4"
+            else "AVX2, x86-64-v3 build (8 fp32 lanes)")
 
 
 def lib() -> C.CDLL:
@@ -39,7 +69,7 @@ def lib() -> C.CDLL:
     with _lock:
         if _lib is None:
             build()
-            L = C.CDLL(str(LIB_PATH))
+            L = C.CDLL(str(LIB_V4_PATH if _variant == "v4" else LIB_PATH))
             P, I32, I64, U64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64
             L.orc_synth.argtypes = [P, I64, I64, I32, U64, I32]
             L.orc_score_f32.argtypes = [P, P, I32, I32, I32]

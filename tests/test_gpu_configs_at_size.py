@@ -1,0 +1,226 @@
+"""Oracle parity at the benchmarked sizes, in the large-tile regime, for every BASELINE config.
+
+Every view here is at least CUs × 24 × 1,024 rows (≈ 6.29M on an MI355X, the large-tile rule of
+osk_view_create) or is the benchmarked config itself, and each path the bench takes at
+that size is checked against the oracle — docs, shard indices and score bits of the coordinator merge:
+
+* C3-shaped 6.5M × 768 COSINE, 8 shards: batch 1 on the VALU int8 prefilter (sq8_scan), batch 32 on
+  the int8 MFMA prefilter (sq8_mfma, register path at 768 dims), batch 256 on the bf16×3 MFMA
+  candidate path, batches 128 / 160 / 192 on whichever path the library's cost model picks (the
+  test restates the model and asserts the choice), and a 10 %-filtered single query (compacted
+  gather scan);
+* C4-shaped 6.5M × 96, DOT_PRODUCT and MAXIMUM_INNER_PRODUCT: batches 32 and 1024 on the LDS-DMA
+  ring instance of sq8_mfma;
+* C2 1M × 128 EUCLIDEAN (SIFT-like), one shard, batch 256 on bf16×3;
+* C5 int8 6.5M × 768 EUCLIDEAN byte vectors, batch 1 on scan_i8_stream.
+
+Large batches check a sample of their queries (every query of the batch is computed in the same
+launches).  The corpora are generated on the device by the counter generator and shard by shard on
+the host by its twin (O.synth), so host memory stays at one shard.  The oracle is the per-shard
+[L] exactSearch (O.knn_batch, device summation order, multi-threaded) and the coordinator
+TopDocs.merge (SearchPhaseController.java:224-246).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from opensearch_amd import _lib, lucene as LU
+from oracle import oracle as O
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
+
+N_SHARDS = 8
+SHARD_INDEX = [3, 1, 4, 0, 6, 2, 7, 5]      # permuted sorted-ShardId ranks
+THREADS = max(1, min(16, os.cpu_count() or 1))
+SIM = LU.VectorSimilarityFunction
+
+
+def _readers(rows_per_shard, dim, sim, seed, dist, enc=LU.VectorEncoding.FLOAT32):
+    return [LU.GpuFlatVectorsReader.synthetic("v", rows_per_shard, dim, sim, enc, seed=seed, dist=dist,
+                                              row0=s * rows_per_shard) for s in range(N_SHARDS)]
+
+
+def _oracle(rows_per_shard, dim, sim, seed, dist, query_sets, k, n_shards=N_SHARDS, shard_index=SHARD_INDEX,
+            accept=None):
+    """Per query set: the coordinator merge of every query, shard by shard on the host."""
+    lists = [[[] for _ in range(len(q))] for q in query_sets]
+    for s in range(n_shards):
+        rows = O.synth(s * rows_per_shard, rows_per_shard, dim, seed, dist)
+        for qi, qs in enumerate(query_sets):
+            if accept is not None or rows.dtype == np.int8:
+                for i in range(len(qs)):
+                    ab = None if accept is None else O.bits_from_bool(accept[s])
+                    sc, dc, _ = O.exact_search(rows, qs[i], k, int(sim), accept_bits=ab)
+                    lists[qi][i].append((sc, dc))
+            else:
+                sc, dc, cc = O.knn_batch(rows, qs, k, int(sim), O.ORDER_DEVICE, THREADS)
+                for i in range(len(qs)):
+                    lists[qi][i].append((sc[i, :cc[i]], dc[i, :cc[i]]))
+        del rows
+    return [[O.topdocs_merge(ls, 0, k, shard_index) for ls in per_q] for per_q in lists]
+
+
+def _check(out, want, rows_idx, k):
+    s, d, sh, c, t, _ = out
+    for j, i in enumerate(rows_idx):
+        es, ed, esh, et, _ = want[j]
+        assert c[i] == len(ed) == k, (i, c[i], len(ed))
+        assert np.array_equal(d[i], ed), (i, d[i], ed)
+        assert np.array_equal(sh[i], esh), (i, sh[i], esh)
+        assert np.array_equal(np.asarray(s[i], np.float32).view(np.uint32), es.view(np.uint32)), i
+        assert t[i] == et
+
+
+def _sample(n, m, seed):
+    return np.sort(np.random.default_rng(seed).choice(n, size=m, replace=False))
+
+
+# ---- the library's path cost model, restated (osk_api.hip view_search_device) -------
+def _takes_bf16x3(rows, dim, nq, k=10):
+    if nq < 96 or k > 12:
+        return False
+    sq8_us = ((nq + 31) // 32) * (rows * (16.0 * ((dim + 15) // 16) + 16.0) / 4.3e6 + 165.0 + 0.28 * dim)
+    bf_us = ((nq + 255) // 256) * (rows * (0.153 + 0.00119 * dim) * 1e-3 + 325.0)
+    return bf_us <= sq8_us
+
+
+# ---------------------------------------------------------------------------------------------------
+# C3-shaped: 6.5M × 768 COSINE, 8 shards
+# ---------------------------------------------------------------------------------------------------
+C3_RPS, C3_DIM, C3_SEED = 812_500, 768, 4242
+
+
+@pytest.fixture(scope="module")
+def c3():
+    readers = _readers(C3_RPS, C3_DIM, SIM.COSINE, C3_SEED, _lib.DIST_NORMALISH_UNIT)
+    ds = LU.DeviceShardSet([[LU.LeafReaderContext(0, 0, r)] for r in readers], SHARD_INDEX)
+    q = {"b1": O.synth(0, 1, C3_DIM, 501, 3), "b32": O.synth(0, 32, C3_DIM, 502, 3),
+         "b256": O.synth(0, 256, C3_DIM, 503, 3), "b128": O.synth(0, 128, C3_DIM, 504, 3),
+         "b160": O.synth(0, 160, C3_DIM, 505, 3), "b192": O.synth(0, 192, C3_DIM, 506, 3)}
+    samp = {"b1": [0], "b32": list(range(32)), "b256": list(_sample(256, 16, 1)), "b128": list(_sample(128, 8, 2)),
+            "b160": list(_sample(160, 8, 3)), "b192": list(_sample(192, 8, 4))}
+    names = list(q)
+    want = _oracle(C3_RPS, C3_DIM, SIM.COSINE, C3_SEED, 3, [q[n][samp[n]] for n in names], 10)
+    yield ds, q, samp, dict(zip(names, want))
+    ds.close()
+    for r in readers:
+        r.close()
+
+
+def _search_counted(ds, queries, k=10):
+    before = {c: ds.counter(c) for c in ("sq8_calls", "mfma_calls")}
+    out = ds.search(queries, k, 0, k)
+    return out, {c: ds.counter(c) - before[c] for c in before}
+
+
+def test_c3_b1_sq8_scan(c3):
+    ds, q, samp, want = c3
+    out, d = _search_counted(ds, q["b1"])
+    assert d == {"sq8_calls": 1, "mfma_calls": 0}
+    _check(out, want["b1"], samp["b1"], 10)
+
+
+def test_c3_b32_sq8_mfma(c3):
+    ds, q, samp, want = c3
+    out, d = _search_counted(ds, q["b32"])
+    assert d == {"sq8_calls": 1, "mfma_calls": 0}
+    _check(out, want["b32"], samp["b32"], 10)
+
+
+def test_c3_b256_bf16x3(c3):
+    ds, q, samp, want = c3
+    out, d = _search_counted(ds, q["b256"])
+    assert d["mfma_calls"] == 1 and d["sq8_calls"] == 0
+    _check(out, want["b256"], samp["b256"], 10)
+
+
+@pytest.mark.parametrize("b", [128, 160, 192])
+def test_c3_path_choice_follows_the_cost_model(c3, b):
+    ds, q, samp, want = c3
+    rows = N_SHARDS * C3_RPS
+    bf = _takes_bf16x3(rows, C3_DIM, b)
+    assert bf == (b >= 160)   # 768-dim rows switch at about 160 queries
+    out, d = _search_counted(ds, q[f"b{b}"])
+    assert d == ({"sq8_calls": 0, "mfma_calls": 1} if bf else {"sq8_calls": 1, "mfma_calls": 0})
+    _check(out, want[f"b{b}"], samp[f"b{b}"], 10)
+
+
+def test_c3_filtered_10pct_single_query(c3):
+    ds, _, _, _ = c3
+    rng = np.random.default_rng(7)
+    accept = [rng.random(C3_RPS) < 0.10 for _ in range(N_SHARDS)]
+    qs = O.synth(0, 1, C3_DIM, 507, 3)
+    want = _oracle(C3_RPS, C3_DIM, SIM.COSINE, C3_SEED, 3, [qs], 10, accept=accept)[0]
+    out = ds.search(qs, 10, 0, 10, accept=accept)
+    _check(out, want, [0], 10)
+
+
+# ---------------------------------------------------------------------------------------------------
+# C4-shaped: 6.5M × 96, DOT_PRODUCT (unit rows) and MAXIMUM_INNER_PRODUCT (raw rows); the ring sq8_mfma
+# ---------------------------------------------------------------------------------------------------
+C4_RPS, C4_DIM = 812_500, 96
+
+
+@pytest.mark.parametrize("sim,dist", [(SIM.DOT_PRODUCT, _lib.DIST_NORMALISH_UNIT),
+                                      (SIM.MAXIMUM_INNER_PRODUCT, _lib.DIST_NORMALISH)])
+def test_c4_ring_prefilter_b32_and_b1024(sim, dist):
+    seed = 9600 + int(sim)
+    readers = _readers(C4_RPS, C4_DIM, sim, seed, dist)
+    ds = LU.DeviceShardSet([[LU.LeafReaderContext(0, 0, r)] for r in readers], SHARD_INDEX)
+    try:
+        q32 = O.synth(0, 32, C4_DIM, 601, dist)
+        q1024 = O.synth(0, 1024, C4_DIM, 602, dist)
+        s1024 = list(_sample(1024, 32, 5))
+        want32, want1024 = _oracle(C4_RPS, C4_DIM, sim, seed, dist, [q32, q1024[s1024]], 10)
+        assert not _takes_bf16x3(N_SHARDS * C4_RPS, C4_DIM, 1024)   # 96-dim rows stay on the prefilter
+        out, d = _search_counted(ds, q32)
+        assert d == {"sq8_calls": 1, "mfma_calls": 0}
+        _check(out, want32, range(32), 10)
+        out, d = _search_counted(ds, q1024)
+        assert d["mfma_calls"] == 0 and d["sq8_calls"] >= 1
+        _check(out, want1024, s1024, 10)
+    finally:
+        ds.close()
+        for r in readers:
+            r.close()
+
+
+# ---------------------------------------------------------------------------------------------------
+# C2: SIFT-shaped 1M × 128 EUCLIDEAN, one shard, batch 256 on bf16×3
+# ---------------------------------------------------------------------------------------------------
+def test_c2_b256_bf16x3():
+    rows_n, dim, seed = 1_000_000, 128, 1280
+    r = LU.GpuFlatVectorsReader.synthetic("v", rows_n, dim, SIM.EUCLIDEAN, seed=seed, dist=_lib.DIST_UNIFORM01_X128)
+    ds = LU.DeviceShardSet([[LU.LeafReaderContext(0, 0, r)]], [0])
+    try:
+        q = O.synth(0, 256, dim, 701, _lib.DIST_UNIFORM01_X128)
+        samp = list(_sample(256, 16, 6))
+        assert _takes_bf16x3(rows_n, dim, 256)
+        want = _oracle(rows_n, dim, SIM.EUCLIDEAN, seed, _lib.DIST_UNIFORM01_X128, [q[samp]], 10, n_shards=1,
+                       shard_index=[0])[0]
+        out, d = _search_counted(ds, q)
+        assert d == {"sq8_calls": 0, "mfma_calls": 1}
+        _check(out, want, samp, 10)
+    finally:
+        ds.close()
+        r.close()
+
+
+# ---------------------------------------------------------------------------------------------------
+# C5 int8: 6.5M × 768 EUCLIDEAN byte vectors, batch 1 on scan_i8_stream
+# ---------------------------------------------------------------------------------------------------
+def test_c5_int8_stream_b1():
+    rps, dim, seed = 812_500, 768, 5150
+    readers = _readers(rps, dim, SIM.EUCLIDEAN, seed, _lib.DIST_INT8, LU.VectorEncoding.BYTE)
+    ds = LU.DeviceShardSet([[LU.LeafReaderContext(0, 0, r)] for r in readers], SHARD_INDEX)
+    try:
+        q = O.synth(0, 2, dim, 801, _lib.DIST_INT8)
+        want = _oracle(rps, dim, SIM.EUCLIDEAN, seed, _lib.DIST_INT8, [q], 10)[0]
+        for i in range(2):
+            out = ds.search(q[i:i + 1], 10, 0, 10)
+            _check(out, [want[i]], [0], 10)
+    finally:
+        ds.close()
+        for r in readers:
+            r.close()

@@ -1,0 +1,98 @@
+"""The plugin's query routes Lucene-shaped k-NN searches onto the device design.
+
+`GpuKnnFloatVectorQuery.rewrite` (the Python mirror of INTEGRATION.md §3's Java query) makes ONE
+osk_view_search per shard over a view of every leaf — instead of one KnnVectorsReader.search per leaf
+([L] AbstractKnnVectorQuery.rewrite, per-leaf tasks under concurrent segment search,
+S/search/DefaultSearchContext.java:257-267) — and sends every filtered leaf to the device, including
+the leaves whose accepted docs number ≤ k, which Lucene's own query would score on the CPU
+(exactSearch).  On a 20-segment shard with deletions and a filter that leaves some leaves with ≤ k or
+zero accepted docs, the one-call route, the per-leaf route and the oracle (per-leaf exactSearch +
+TopDocs.merge(k, perLeaf), S/search/internal/ContextIndexSearcher.java:203-218) agree on docs and
+score bits.
+"""
+import numpy as np
+import pytest
+
+from opensearch_amd import lucene as LU
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+COS = LU.VectorSimilarityFunction.COSINE
+DIM, K = 96, 10
+
+
+@pytest.fixture(scope="module")
+def shard():
+    rng = np.random.default_rng(11)
+    sizes = [int(x) for x in rng.integers(200, 3000, size=20)]
+    rows = [O.synth(0, n, DIM, 900 + i, 3) for i, n in enumerate(sizes)]
+    readers = [LU.GpuFlatVectorsReader("v", r, COS) for r in rows]
+    base, leaves = 0, []
+    for i, (r, n) in enumerate(zip(readers, sizes)):
+        live = None if i % 3 else rng.random(n) > 0.1          # deletions on every third leaf
+        leaves.append(LU.LeafReaderContext(i, base, r, live))
+        base += n
+    # a filter that leaves leaf 4 with 3 accepted docs (≤ k: Lucene's CPU exactSearch branch), leaf 7
+    # with none, leaf 9 with exactly k, and the others a 30 % sample
+    masks = {}
+    for lf, n in zip(leaves, sizes):
+        m = rng.random(n) < 0.3
+        if lf.ord in (4, 9):
+            m[:] = False
+            m[rng.choice(n, 3 if lf.ord == 4 else K, replace=False)] = True
+        if lf.ord == 7:
+            m[:] = False
+        masks[lf.ord] = m
+    yield leaves, rows, masks
+    LU.GpuKnnFloatVectorQuery.release_views()
+    for r in readers:
+        r.close()
+
+
+def oracle(leaves, rows, q, accept_of):
+    lists = []
+    for lf, r in zip(leaves, rows):
+        acc = accept_of(lf)
+        ab = None if acc is None else O.bits_from_bool(acc)
+        sc, dc, _ = O.exact_search(r, q, K, int(COS), accept_bits=ab)
+        lists.append((sc, dc + lf.doc_base))
+    es, ed, _, _, _ = O.topdocs_merge(lists, 0, K, list(range(len(lists))))
+    return es, ed
+
+
+def hits(td):
+    return (np.array([h.score for h in td.score_docs], np.float32).view(np.uint32),
+            np.array([h.doc for h in td.score_docs], np.int32))
+
+
+@pytest.mark.parametrize("filtered", [False, True])
+def test_one_call_per_shard_equals_per_leaf_and_oracle(shard, filtered):
+    leaves, rows, masks = shard
+    filt = (lambda lf: masks[lf.ord]) if filtered else None
+    for qi in range(4):
+        q = O.synth(0, 1, DIM, 950 + qi, 3)[0]
+        gq = LU.GpuKnnFloatVectorQuery("v", q, K, filt)
+        view = gq._shard_view(leaves)
+        calls = view.counter("sq8_calls") + view.counter("select_calls")
+        one = gq.rewrite(leaves)
+        assert view.counter("sq8_calls") + view.counter("select_calls") == calls + 1   # one device search per shard
+        per_leaf = LU.KnnFloatVectorQuery("v", q, K, filt).rewrite(leaves)
+        es, ed = oracle(leaves, rows, q, gq._accept)
+        for td in (one, per_leaf):
+            s, d = hits(td)
+            assert np.array_equal(d, ed) and np.array_equal(s, es.view(np.uint32)), (filtered, qi)
+
+
+def test_exact_search_override_serves_cost_le_k_leaves_on_the_device(shard):
+    leaves, rows, masks = shard
+    q = O.synth(0, 1, DIM, 960, 3)[0]
+    gq = LU.GpuKnnFloatVectorQuery("v", q, K, lambda lf: masks[lf.ord])
+    for ordinal in (4, 7, 9):
+        lf = leaves[ordinal]
+        acc = gq._accept(lf)
+        td = gq.exact_search(lf, acc)
+        es, ed, _ = O.exact_search(rows[ordinal], q, K, int(COS), accept_bits=O.bits_from_bool(acc))
+        s, d = hits(td)
+        assert len(d) == int(acc.sum()) <= K
+        assert np.array_equal(d, ed + lf.doc_base) and np.array_equal(s, es.view(np.uint32))
