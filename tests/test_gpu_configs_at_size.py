@@ -47,6 +47,7 @@ def _oracle(rows_per_shard, dim, sim, seed, dist, query_sets, k, n_shards=N_SHAR
     lists = [[[] for _ in range(len(q))] for q in query_sets]
     for s in range(n_shards):
         rows = O.synth(s * rows_per_shard, rows_per_shard, dim, seed, dist)
+        print(f"oracle shard {s}/{n_shards} ({rows_per_shard}x{dim})", flush=True)   # progress for long runs
         for qi, qs in enumerate(query_sets):
             if accept is not None or rows.dtype == np.int8:
                 for i in range(len(qs)):
@@ -173,12 +174,21 @@ def test_c4_ring_prefilter_b32_and_b1024(sim, dist):
         q1024 = O.synth(0, 1024, C4_DIM, 602, dist)
         s1024 = list(_sample(1024, 32, 5))
         want32, want1024 = _oracle(C4_RPS, C4_DIM, sim, seed, dist, [q32, q1024[s1024]], 10)
-        assert not _takes_bf16x3(N_SHARDS * C4_RPS, C4_DIM, 1024)   # 96-dim rows stay on the prefilter
         out, d = _search_counted(ds, q32)
         assert d == {"sq8_calls": 1, "mfma_calls": 0}
         _check(out, want32, range(32), 10)
-        out, d = _search_counted(ds, q1024)
+        # b1024 on the ring prefilter (forced: at 6.5M rows the cost model prefers bf16x3 here, at the
+        # 100M rows of C4 itself it keeps the prefilter) and on whichever path the cost model picks
+        _lib.tune("sq8_cost_pct", 1)
+        try:
+            out, d = _search_counted(ds, q1024)
+        finally:
+            _lib.tune("sq8_cost_pct", 100)
         assert d["mfma_calls"] == 0 and d["sq8_calls"] >= 1
+        _check(out, want1024, s1024, 10)
+        assert _takes_bf16x3(N_SHARDS * C4_RPS, C4_DIM, 1024) and not _takes_bf16x3(100_000_000, C4_DIM, 1024)
+        out, d = _search_counted(ds, q1024)
+        assert d == {"sq8_calls": 0, "mfma_calls": 1}
         _check(out, want1024, s1024, 10)
     finally:
         ds.close()
