@@ -63,7 +63,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md; 6.29 TB/s meas
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_traffic_c3_b1.json")
 
 
-def pmc_traffic(rows_local: int, batch: int, prefilter: bool):
+def pmc_traffic(rows_local: int, batch: int, prefilter: bool, six: bool = False):
     """HBM bytes per scan launch from the committed rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes of this
     same command (tools/pmc_traffic.py; gfx950 ×2 FETCH correction applied), scaled to this rank's rows.
     The passes were taken at N=1 (10M rows, batch 1).  None when absent or for another batch size."""
@@ -71,7 +71,7 @@ def pmc_traffic(rows_local: int, batch: int, prefilter: bool):
         return None, None
     data = json.load(open(PMC_SUMMARY))
     # (a prefix: the headline instance is sq8_scan<16, 3, 1, 4, MODE>)
-    want = "sq8_scan<16, 3, 1, 4" if prefilter else "scan_f32<16, 12, 1, false"
+    want = "sq6_scan<3, 3>" if six else "sq8_scan<16, 3, 1, 4" if prefilter else "scan_f32<16, 12, 1, false"
     for name, v in data.items():
         if want in name:
             return v["hbm_bytes"] * rows_local / (N_SHARDS * ROWS_PER_SHARD), os.path.relpath(PMC_SUMMARY, ROOT)
@@ -309,6 +309,12 @@ def main():
         for v in views:
             _lib.check(_lib.lib().osk_view_profile(v, enable))
 
+    # setup: each view's first single queries calibrate the 6-bit tier with synchronous counter reads
+    # (osk_view::sq6_probes); issue them here, with the other one-time builds, not inside the warmup
+    for i in range(4 * F):
+        step(n_pool - 1 - (i % n_pool), F)
+    torch.cuda.synchronize()
+
     def timed(steps, warmup, offset=0, slots=F):
         """W untimed steps, then K steps between barrier + synchronize; returns the max-over-ranks wall
         time, the mean scan-launch duration (HIP events on the launch streams), the GPU event time and
@@ -360,7 +366,7 @@ def main():
 
     _lib.tune("sq8", 0 if a.no_sq8 else 1)
     fb0, rs0, calls0 = counter("sq8_fallback_queries"), counter("sq8_rescored_rows"), counter("sq8_calls")
-    sel0 = counter("select_calls")
+    sel0, six0, rb0 = counter("select_calls"), counter("sq6_calls"), counter("sq6_rebound_rows")
     elapsed_max, ovl_scan_ms, ev_ms, out = timed(a.steps, a.warmup)
     # The same steps one at a time (one query in flight): the per-query latency, and the scan kernel's
     # isolated launch duration — the roofline's denominator.  With F > 1 the launches of neighbouring
@@ -375,6 +381,7 @@ def main():
     # else bf16×3 from batch 96, else fp32)
     prefilter = counter("sq8_calls") > calls0
     select = counter("select_calls") > sel0
+    six = prefilter and counter("sq6_calls") > six0   # single queries on the 6-bit tier
     batched = not prefilter and not select and B >= 96 and K <= 12
     sq8_mfma = prefilter and sq8_mfma_min > 0 and B >= sq8_mfma_min
     # sanity on the last step: every query got `SIZE` hits from the 10M corpus
@@ -393,6 +400,16 @@ def main():
         kernel_name = ("sq8_mfma<KS=12,QB=2> certified int8 prefilter on v_mfma_i32_16x16x64_i8 (bytes = int8 rows "
                        "(tiled copy) + 16-B bound terms per row, once per launch of ≤ 32 queries; time = pilot + "
                        "pilot merge + main pass)")
+    elif six:
+        # the 6-bit codes (3/4 of the int8 row, dims padded to 256 per lane set) + 16-B bound terms of every
+        # row, plus the int8 rows + bound terms the scan re-bounded (counted on the device, per launch)
+        n_six = counter("sq6_calls") - six0
+        rebound = (counter("sq6_rebound_rows") - rb0) / max(1, n_six)
+        passes = B
+        bytes_per_launch = rows_local * (((DIM + 255) // 256) * 192 + 16) + rebound * (u8 * 16 + 16)
+        kernel_name = ("sq6_scan<C=3,U=3> certified 6-bit first tier (bytes = 6-bit codes + 16-B bound terms per "
+                       "row + the int8 rows + terms re-bounded for the rows that pass the 6-bit test; one query "
+                       "per launch)")
     elif prefilter:
         passes = (B + 7) // 8
         bytes_per_launch = rows_local * (u8 * 16 + 16) * passes
@@ -413,6 +430,9 @@ def main():
     if prefilter:
         n_calls = counter("sq8_calls") - calls0
         extra["prefilter"] = {
+            "tier": "6-bit + int8 re-bound" if six else "int8",
+            "int8_rebound_rows_per_query": ((counter("sq6_rebound_rows") - rb0) /
+                                            max(1, counter("sq6_calls") - six0)) if six else None,
             "fallback_queries": counter("sq8_fallback_queries") - fb0,
             "rescored_rows_per_query": (counter("sq8_rescored_rows") - rs0) / max(1, n_calls * B),
             "searches": n_calls,
@@ -453,7 +473,7 @@ def main():
                      shard=np.stack([o[2] for o in outs]), count=np.stack([o[3] for o in outs]),
                      total=np.stack([o[4] for o in outs]), max_score=np.stack([o[5] for o in outs]))
 
-    traffic, traffic_src = pmc_traffic(rows_local, B, prefilter)
+    traffic, traffic_src = pmc_traffic(rows_local, B, prefilter, six)
     ceiling = read_ceiling()
     if rank == 0:
         res = {

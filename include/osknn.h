@@ -141,7 +141,8 @@ int32_t osk_seg_footprint(const osk_seg* seg, int64_t* hbm_bytes);
  * S/index/engine/InternalEngine.java:2409-2432, S/index/IndexWarmer.java:132-135).  Float32 segments
  * get the prefilter copy at staging; the other two are built here or, if never warmed, by the first
  * search that takes their path.  No-op for byte fields. */
-#define OSK_WARM_PREFILTER      1   /* int8 copy + 16-B bound terms per row (¼ + 16 B of the rows)      */
+#define OSK_WARM_PREFILTER      1   /* int8 copy + 16-B bound terms per row (¼ + 16 B of the rows), and
+                                       for dims ≥ 512 the 6-bit tier of single queries (+ ≈3/16 + 16 B)   */
 #define OSK_WARM_PREFILTER_MFMA 2   /* its 16-row tiled twin read by the batched int8 MFMA prefilter    */
 #define OSK_WARM_BATCHED        4   /* bf16 hi/lo split copy of the batched bf16×3 MFMA path (= rows)   */
 #define OSK_WARM_ALL            7
@@ -239,6 +240,10 @@ int32_t osk_view_scan_time(osk_view* view, double* total_ms, int64_t* calls);
  *                     16384 tiles of 128 rows, else 512)
  *   "sq8"             0|1 certified int8 prefilter for float32 searches with k ≤ 12 that do not take
  *                     the bf16×3 path (default 1; results are bit-identical either way)
+ *   "sq6"             0|1 single unfiltered prefiltered queries scan the 6-bit tier where the view has
+ *                     one (dims ≥ 512; default 1) instead of the int8 copy...
+ *   "sq6_probe_pct"   ...unless the view's first 4 such calls re-bound more than this % of the rows from
+ *                     the int8 copy (default 10; the view then keeps the int8 tier)
  *   "sq8_mfma_min"    prefilter batches of at least this many queries scan on int8 MFMA (sq8_mfma,
  *                     default 2; 0 = always the VALU sq8_scan)
  *   "sq8_mfma_queries"  16 | 32 queries per sq8_mfma launch (default 32)
@@ -266,7 +271,9 @@ int32_t osk_tune_set(const char* key, int64_t value);
  * certificate failed and were recomputed by the exact streaming scan. */
 int32_t osk_view_stats(osk_view* view, int64_t* batched_calls, int64_t* fallback_queries);
 /* Named counters of a view: "mfma_calls", "mfma_fallback_queries" (as osk_view_stats),
- * "sq8_calls" (prefiltered searches), "sq8_fallback_queries" (queries where some tile's candidate
+ * "sq8_calls" (prefiltered searches), "sq6_calls" (those whose scan read the 6-bit tier),
+ * "sq6_rebound_rows" (rows the 6-bit scan re-bounded from the int8 copy, all calls),
+ * "sq8_fallback_queries" (queries where some tile's candidate
  * list overflowed past the certificate and the tile was re-scanned exactly), "sq8_exact_tiles"
  * (such tiles), "sq8_rescored_rows" (rows re-scored exactly, all calls), "select_calls" (searches
  * on the select path, k > 12), "host_slots" (workspace slots the host entries have leased: 1 + replicas),

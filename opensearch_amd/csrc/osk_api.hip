@@ -149,6 +149,8 @@ osk_seg::~osk_seg() {
     if (d_q8) (void)hipFree(d_q8);
     if (d_q8aux) (void)hipFree(d_q8aux);
     if (d_q8t) (void)hipFree(d_q8t);
+    if (d_q6) (void)hipFree(d_q6);
+    if (d_q6aux) (void)hipFree(d_q6aux);
 }
 
 int64_t osk_seg::hbm_bytes() const {
@@ -160,6 +162,7 @@ int64_t osk_seg::hbm_bytes() const {
     if (d_split) b += std::max<int64_t>(1, (n_rows + 127) / 128) * 8 * split_KS * 2 * 1024 + n * 4 + 4;
     if (d_q8) b += n * units8 * 16 + n * 16;
     if (d_q8t) b += std::max<int64_t>(1, (n_rows + 15) / 16) * sq8_mfma_ks(units8) * 1024;
+    if (d_q6) b += sq6_bytes(n_rows, dim);
     return b;
 }
 
@@ -284,6 +287,8 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         {"sq8_cost_pct", &g_tuning.sq8_cost_pct, 0, 100000, false},
         {"mfma_units", &g_tuning.mfma_units, 0, 32768, false},
         {"sq8", &g_tuning.sq8, 0, 1, false},
+        {"sq6", &g_tuning.sq6, 0, 1, false},
+        {"sq6_probe_pct", &g_tuning.sq6_probe_pct, 0, 100, false},
         {"filter_gather", &g_tuning.filter_gather, 0, 1, false},
         {"select_mid_k", &g_tuning.select_mid_k, 0, 1, false},
         {"sel_writer", &g_tuning.sel_writer, 0, 3, false},
@@ -294,7 +299,7 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         {"sq8_mfma_ring", &g_tuning.sq8_mfma_ring, -1, 8, false},
         {"i8_stream", &g_tuning.i8_stream, 0, 1, false},
         {"call_timing", &g_tuning.call_timing, 0, 1, false},
-        {"sq8_mfma_ablate", &g_tuning.sq8_mfma_ablate, 0, 3, true},
+        {"sq8_mfma_ablate", &g_tuning.sq8_mfma_ablate, 0, 15, true},   // (also sq6_scan's: 1 no re-bound, 2 no floor)
         {"sq8_force_fallback", &g_tuning.sq8_force_fallback, 0, 1, true},
         {"settle_trace", &g_tuning.settle_trace, 0, 1, true},
         {"mfma_ablate", &g_tuning.mfma_ablate, 0, 31, true},
@@ -652,6 +657,19 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
         }
     }
     OSK_REQUIRE(v->n_tiles < (1 << 24), "too many tiles");
+    // dispatch order of the 6-bit scan: tiles interleaved over shards (shard s's j-th of n_s tiles at
+    // ≈ (j + ½)/n_s of the grid), so every round of resident workgroups scans a slice of every shard and
+    // each shard's floor rises from the first round on (osk_sq6.hip)
+    std::vector<int32_t> tile_order(std::max<size_t>(1, tiles.size()), 0);
+    {
+        std::vector<std::pair<double, int>> key;
+        for (int sh = 0; sh < n_shards; ++sh) {
+            const int t0 = v->shard_tile_begin[sh], n = v->shard_tile_begin[sh + 1] - t0;
+            for (int j = 0; j < n; ++j) key.push_back({(j + 0.5) / n, t0 + j});
+        }
+        std::stable_sort(key.begin(), key.end(), [](auto& a, auto& b) { return a.first < b.first; });
+        for (size_t i = 0; i < key.size(); ++i) tile_order[i] = key[i].second;
+    }
 
     v->seg_doc_base.resize(n_segs);
     for (int i = 0; i < n_segs; ++i) v->seg_doc_base[i] = seg_doc_base ? seg_doc_base[i] : 0;
@@ -669,6 +687,7 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
     OSK_HIP(v->d_shard_tile_begin.reserve(sizeof(int32_t) * (n_shards + 1)));
     OSK_HIP(v->d_shard_index.reserve(sizeof(int32_t) * n_shards));
     OSK_HIP(v->d_tile_coff.reserve(sizeof(int32_t) * tile_coff.size()));
+    OSK_HIP(v->d_tile_order.reserve(sizeof(int32_t) * tile_order.size()));
     OSK_HIP(v->d_seg_vrow.reserve(sizeof(int64_t) * n_segs));
     OSK_HIP(v->d_counters.reserve(sizeof(unsigned long long) * 4));
     OSK_HIP(hipMemsetAsync(v->d_counters.p, 0, sizeof(unsigned long long) * 4, st));
@@ -682,6 +701,8 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
     OSK_HIP(hipMemcpyAsync(v->d_shard_index.p, v->shard_index.data(), sizeof(int32_t) * n_shards,
                            hipMemcpyHostToDevice, st));
     OSK_HIP(hipMemcpyAsync(v->d_tile_coff.p, tile_coff.data(), sizeof(int32_t) * tile_coff.size(),
+                           hipMemcpyHostToDevice, st));
+    OSK_HIP(hipMemcpyAsync(v->d_tile_order.p, tile_order.data(), sizeof(int32_t) * tile_order.size(),
                            hipMemcpyHostToDevice, st));
     OSK_HIP(hipStreamSynchronize(st));
     for (osk_seg* sg : v->segs) sg->refs.fetch_add(1);   // released by ~osk_view
@@ -1031,9 +1052,27 @@ int32_t ensure_sq8_seg(osk_seg* s, hipStream_t st) {
     }
     OSK_HIP(launch_sq8_quantize(static_cast<const float4*>(s->d_rows), s->n_rows, s->units, s->units, u8, q8, aux,
                                 0, st));
+    // the 6-bit tier of single queries, where the dim has one
+    void* q6 = nullptr;
+    float4* aux6 = nullptr;
+    if (sq6_supported(s->dim)) {
+        const int64_t b6 = sq6_bytes(s->n_rows, s->dim), ba = std::max<int64_t>(1, s->n_rows) * 16;
+        e = hipMalloc(&q6, (size_t)(b6 - ba));
+        if (e == hipSuccess) e = hipMalloc(&aux6, (size_t)ba);
+        if (e != hipSuccess) {
+            if (q6) (void)hipFree(q6);
+            (void)hipFree(q8);
+            (void)hipFree(aux);
+            set_error(std::string("hipMalloc of the 6-bit prefilter tier failed: ") + hipGetErrorString(e));
+            return OSK_ERR_OOM;
+        }
+        OSK_HIP(launch_sq6_quantize(static_cast<const float4*>(s->d_rows), s->n_rows, s->units, s->dim, q6, aux6, st));
+    }
     OSK_HIP(hipStreamSynchronize(st));
     s->d_q8 = q8;
     s->d_q8aux = aux;
+    s->d_q6 = q6;
+    s->d_q6aux = aux6;
     s->units8 = u8;
     return OSK_OK;
 }
@@ -1184,7 +1223,23 @@ int32_t ensure_sq8(osk_view* v, hipStream_t st) {
     OSK_HIP(v->d_sq8_aux.reserve(sizeof(void*) * ns));
     OSK_HIP(hipMemcpyAsync(v->d_sq8_rows.p, rows.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
     OSK_HIP(hipMemcpyAsync(v->d_sq8_aux.p, aux.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
+    // the 6-bit tier: used only when every segment has one
+    std::vector<const void*> rows6(ns);
+    std::vector<const float4*> aux6(ns);
+    bool all6 = ns > 0;
+    for (int i = 0; i < ns; ++i) {
+        rows6[i] = v->segs[i]->d_q6;
+        aux6[i] = v->segs[i]->d_q6aux;
+        all6 = all6 && rows6[i] && aux6[i];
+    }
+    if (all6) {
+        OSK_HIP(v->d_sq6_rows.reserve(sizeof(void*) * ns));
+        OSK_HIP(v->d_sq6_aux.reserve(sizeof(void*) * ns));
+        OSK_HIP(hipMemcpyAsync(v->d_sq6_rows.p, rows6.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
+        OSK_HIP(hipMemcpyAsync(v->d_sq6_aux.p, aux6.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
+    }
     OSK_HIP(hipStreamSynchronize(st));
+    v->sq6_ready = all6;
     v->sq8_ready = true;
     return OSK_OK;
 }
@@ -1199,16 +1254,37 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     if (rc) return rc;
     const int u8 = v->units8, S = v->n_shards;
     const int nq_pad = (nq + kMaxNQ - 1) / kMaxNQ * kMaxNQ;
+    // batches of ≥ sq8_mfma_min queries: the int8 MFMA scan, 16 queries per launch; else the VALU
+    // scan, ≤ 8 per launch.  Filtered VALU scans run over the compacted accepted ordinals.  A single
+    // unfiltered query scans the 6-bit tier where the view has one.
+    const bool use_mfma = g_tuning.sq8_mfma_min > 0 && nq >= g_tuning.sq8_mfma_min && sq8_mfma_supported(u8);
+    const bool use6 = nq == 1 && !d_accept && !use_mfma && v->sq6_ready && !v->sq6_off && g_tuning.sq6;
+    const bool probe6 = use6 && v->sq6_probes < kSq6Probes;
+    unsigned long long rb_before = 0;
+    if (probe6) {   // calibration: this call's int8 re-bounds, counted synchronously (first calls only)
+        OSK_HIP(hipStreamSynchronize(st));
+        OSK_HIP(hipMemcpy(&rb_before, v->d_counters.as<unsigned long long>() + 3, sizeof(rb_before),
+                          hipMemcpyDeviceToHost));
+    }
     OSK_HIP(v->ws_q8.reserve((size_t)nq_pad * u8 * 16));
     OSK_HIP(v->ws_qc.reserve(sizeof(float4) * nq_pad));
     OSK_HIP(v->ws_flags.reserve(sizeof(int) * nq));
-    // one launch: padded fp32 queries, |q|² (device order), int8 queries + bound terms, flags = 0
+    Sq6Prep q6{};
+    if (use6) {
+        q6.C = sq6_chunks(v->dim);
+        q6.floor_n = S * kFloorBuckets * kFloorStride;
+        OSK_HIP(v->ws_q6.reserve((size_t)nq_pad * 256 * q6.C));
+        OSK_HIP(v->ws_qc6.reserve(sizeof(float4) * nq_pad));
+        OSK_HIP(v->ws_floor.reserve(sizeof(uint32_t) * (size_t)nq_pad * q6.floor_n));
+        q6.q6 = v->ws_q6.as<uint32_t>();
+        q6.qc6 = v->ws_qc6.as<float4>();
+        q6.floor = v->ws_floor.as<uint32_t>();
+    }
+    // one launch: padded fp32 queries, |q|² (device order), int8 queries + bound terms (and the 6-bit
+    // tier's query form, floor buckets zeroed), flags = 0
     OSK_HIP(launch_sq8_prep(v->cfg, static_cast<const float*>(d_queries), v->dim, nq, nq_pad, UP, u8,
                             v->ws_q.as<float4>(), v->ws_qnorm.as<float>(), v->ws_q8.p, v->ws_qc.as<float4>(),
-                            v->ws_flags.as<int>(), st));
-    // batches of ≥ sq8_mfma_min queries: the int8 MFMA scan, 16 queries per launch; else the VALU
-    // scan, ≤ 8 per launch.  Filtered VALU scans run over the compacted accepted ordinals.
-    const bool use_mfma = g_tuning.sq8_mfma_min > 0 && nq >= g_tuning.sq8_mfma_min && sq8_mfma_supported(u8);
+                            v->ws_flags.as<int>(), st, q6));
     const bool gather = d_accept && !use_mfma && g_tuning.filter_gather;
     if (gather) {
         rc = ensure_gather(v, st);
@@ -1290,6 +1366,23 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             p.thr_keys = v->ws_thr.as<uint64_t>();
             p.thr_counts = v->ws_thr_counts.as<int32_t>();
             OSK_HIP(launch_sq8_mfma(p, st, nullptr, e1));
+        } else if (use6) {
+            p.rows6 = v->d_sq6_rows.as<const void*>();
+            p.aux6 = v->d_sq6_aux.as<const float4*>();
+            p.q6 = v->ws_q6.as<int4>() + (size_t)q0 * 16 * q6.C;
+            p.qc6 = v->ws_qc6.as<float4>() + q0;
+            p.floor = q6.floor;
+            p.k = k;
+            p.n_shards = S;
+            p.counters = v->d_counters.as<unsigned long long>();
+            p.ablate = g_tuning.sq8_mfma_ablate;
+            p.tile_order = v->d_tile_order.as<int32_t>();
+            OSK_HIP(v->ws_cand6.reserve(sizeof(uint32_t) * (size_t)p.n_lists * kSq6Cap));
+            OSK_HIP(v->ws_cnt6.reserve(sizeof(int32_t) * (size_t)nq * p.n_lists));
+            p.cand6 = v->ws_cand6.as<uint32_t>();
+            p.cnt6 = v->ws_cnt6.as<int32_t>();
+            p.cap6 = kSq6Cap;
+            OSK_HIP(launch_sq6_scan(p, v->dim, st, e0, e1));
         } else {
             OSK_HIP(launch_sq8_scan(p.q_count, p, st, e0, e1));
         }
@@ -1321,7 +1414,7 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     sp.flags = v->ws_flags.as<int>();
     sp.counters = v->d_counters.as<unsigned long long>();
     sp.n_lists = 4 * n_scan_tiles;
-    sp.scan_R = use_mfma ? kMfmaScanR : 64 / sq8_lanes(u8);
+    sp.scan_R = use_mfma ? kMfmaScanR : use6 ? kSq6ScanR : 64 / sq8_lanes(u8);
     sp.n_shards = S;
     sp.n_segs = (int)v->segs.size();
     sp.units = v->units;
@@ -1334,6 +1427,20 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     }
     OSK_HIP(launch_sq8_settle(v->cfg, nq, sp, st));
     v->sq8_calls += 1;
+    v->sq6_calls += use6 ? 1 : 0;
+    if (probe6) {
+        unsigned long long rb_after = 0;
+        OSK_HIP(hipStreamSynchronize(st));
+        OSK_HIP(hipMemcpy(&rb_after, v->d_counters.as<unsigned long long>() + 3, sizeof(rb_after),
+                          hipMemcpyDeviceToHost));
+        int64_t rows = 0;
+        for (const osk_seg* sg : v->segs) rows += sg->n_rows;
+        v->sq6_probe_rows += rows;
+        v->sq6_probe_rebound += (int64_t)(rb_after - rb_before);
+        if (++v->sq6_probes == kSq6Probes &&
+            (double)v->sq6_probe_rebound * 100.0 > (double)v->sq6_probe_rows * (double)g_tuning.sq6_probe_pct)
+            v->sq6_off = true;
+    }
     return OSK_OK;
 }
 
@@ -1727,8 +1834,10 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
         *value = v->n_slices;
         return OSK_OK;
     }
-    const bool dev = n == "sq8_fallback_queries" || n == "sq8_rescored_rows" || n == "sq8_exact_tiles";
-    OSK_REQUIRE(dev || n == "mfma_calls" || n == "mfma_fallback_queries" || n == "sq8_calls" || n == "select_calls",
+    const bool dev = n == "sq8_fallback_queries" || n == "sq8_rescored_rows" || n == "sq8_exact_tiles" ||
+                     n == "sq6_rebound_rows";
+    OSK_REQUIRE(dev || n == "mfma_calls" || n == "mfma_fallback_queries" || n == "sq8_calls" || n == "sq6_calls" ||
+                    n == "select_calls",
                 "unknown counter: " + n);
     // summed over the view and the replicas its host entries leased
     int64_t sum = 0;
@@ -1739,10 +1848,11 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
             unsigned long long c[4];
             OSK_HIP(hipDeviceSynchronize());   // the last search may be on any stream
             OSK_HIP(hipMemcpy(c, s->d_counters.p, sizeof(c), hipMemcpyDeviceToHost));
-            sum += (int64_t)(n == "sq8_fallback_queries" ? c[0] : n == "sq8_rescored_rows" ? c[1] : c[2]);
+            sum += (int64_t)(n == "sq8_fallback_queries" ? c[0] : n == "sq8_rescored_rows" ? c[1]
+                             : n == "sq8_exact_tiles" ? c[2] : c[3]);
         } else {
             sum += n == "mfma_calls" ? s->mfma_calls : n == "mfma_fallback_queries" ? s->mfma_fallback_queries
-                 : n == "sq8_calls" ? s->sq8_calls : s->sel_calls;
+                 : n == "sq8_calls" ? s->sq8_calls : n == "sq6_calls" ? s->sq6_calls : s->sel_calls;
         }
     }
     *value = sum;

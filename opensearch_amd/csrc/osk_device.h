@@ -56,6 +56,39 @@ __device__ __forceinline__ float sq8_bound_side(int sim, float I, float4 ax, flo
     return approx + e + sl;
 }
 
+// Quick-reject threshold of a wave list whose worst upper-bound key is `thr` (0 = list not full):
+// a row whose bound fails sq8_pass has upper-bound score ≤ the list's worst score, so it cannot
+// enter the list (the precise test below decides the rest).
+//   EUCLIDEAN: d² threshold; COSINE: dot threshold per |x|; others: dot threshold.
+__device__ __forceinline__ float sq8_quick(int sim, uint64_t thr, float sqn, float cos_slack) {
+    if (thr == 0ull) return sim == SIM_EUCLIDEAN ? __builtin_inff() : -__builtin_inff();
+    const float t = key_score(thr);
+    switch (sim) {
+        case SIM_EUCLIDEAN: {
+            const float tm = t * (1.0f - 0x1p-16f);
+            return tm > 0.0f ? 1.0f / tm - 1.0f : __builtin_inff();
+        }
+        case SIM_MIP: {
+            const float tm = t * (1.0f - 0x1p-16f);
+            if (!(tm > 0.0f)) return -__builtin_inff();
+            return tm >= 1.0f ? tm - 1.0f : 1.0f - 1.0f / tm;
+        }
+        case SIM_DOT_PRODUCT: {
+            const float tm = t - 0x1p-16f * fabsf(t) - 0x1p-20f;
+            return 2.0f * tm - 1.0f;
+        }
+        default: {   // COSINE
+            const float tm = t - 0x1p-16f * fabsf(t) - 0x1p-20f;
+            return (2.0f * tm - 1.0f - cos_slack) * sqn;
+        }
+    }
+}
+__device__ __forceinline__ bool sq8_pass(int sim, float lo, float hi, float tq, float sx) {
+    if (sim == SIM_EUCLIDEAN) return !(lo > tq);
+    if (sim == SIM_COSINE) return !(hi < tq * sx);
+    return !(hi < tq);
+}
+
 // Global-address-space loads (global_load, not flat_load): a flat load also counts in lgkmcnt, so
 // the first LDS read after it would wait for every row load in flight, prefetched ones included.
 __device__ __forceinline__ int4 load_i4_g(const int4* p, bool nt) {

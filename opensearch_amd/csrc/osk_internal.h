@@ -163,6 +163,20 @@ struct Sq8Params {
     const uint32_t* comp;
     const int32_t* scnt;
     int gather_min;                  // at most one gather tile per this many accepted rows of a segment
+    // sq6_scan (osk_sq6.hip): per segment, the 6-bit tiled codes and their bound terms; the query's nibble
+    // split ([8C half-chunks][bh 4 dwords, bl 4 dwords]) and its 6-bit bound terms; the per-(query, shard)
+    // floor buckets [q][n_shards][kFloorBuckets] (sortable lower bounds; rows8 / aux / q8 / qc are the
+    // int8 re-bound of the rows that pass the 6-bit test)
+    const void* const* rows6;
+    const float4* const* aux6;
+    const int4* q6;
+    const float4* qc6;
+    uint32_t* floor;
+    unsigned long long* counters;    // sq6_scan adds its int8 re-bounds to [3] (SettleParams::counters)
+    const int32_t* tile_order;       // sq6_scan: the tile of each workgroup (tiles interleaved over shards)
+    uint32_t* cand6;                 // sq6_scan → sq6_rebound: per list, the rows that passed the 6-bit test
+    int32_t* cnt6;                   // [q][n_lists] their count (> cap6: overflowed)
+    int cap6;
 };
 
 struct SettleParams {
@@ -314,8 +328,29 @@ int sq8_ring_slots(int units8, int qb, int want);   // sq8_mfma LDS-DMA ring dep
 hipError_t launch_sq8_tile(const void* q8, int64_t n_rows, int units8, int ks, void* out, hipStream_t s);
 hipError_t launch_sq8_mfma(const Sq8Params& p, hipStream_t s, hipEvent_t ev_start = nullptr,
                            hipEvent_t ev_stop = nullptr);
+// The 6-bit tier's share of the query prep (C = 0: none): the nibble-split query [nq_pad][64·C dwords],
+// its bound terms, and the floor buckets [nq_pad][floor_n] zeroed
+struct Sq6Prep {
+    uint32_t* q6 = nullptr;
+    float4* qc6 = nullptr;
+    uint32_t* floor = nullptr;
+    int floor_n = 0;
+    int C = 0;
+};
 hipError_t launch_sq8_prep(int cfg, const float* src, int dim, int nq, int nq_pad, int UP, int units8, float4* qpad,
-                           float* qnorm, void* q8, float4* qc, int* flags, hipStream_t s);
+                           float* qnorm, void* q8, float4* qc, int* flags, hipStream_t s, const Sq6Prep& q6 = Sq6Prep{});
+// ---- the 6-bit first tier (osk_sq6.hip): single unfiltered queries over float32 rows of ≥ 512 dims ----
+int sq6_chunks(int dim);                 // C: half-chunks of 32 dims per lane (8 lanes per row)
+int sq6_supported(int dim);
+int64_t sq6_bytes(int64_t n_rows, int dim);   // the tiled codes + bound terms of a segment
+constexpr int kSq6ScanR = 8;             // rows per wave-iteration of sq6_scan (the settle's scan_R)
+constexpr int kFloorBuckets = 64;       // sq6_scan's floor: the k-th best of 64 bucket maxima of lists' best lbs,
+constexpr int kFloorStride = 16;        // one 64-B line per bucket (uint32 units)
+constexpr int kSq6Probes = 4;            // calibration calls of the 6-bit tier per view (osk_view::sq6_probes)
+constexpr int kSq6Cap = 256;             // candidate rows per list between the 6-bit pass and the int8 re-bound
+hipError_t launch_sq6_quantize(const float4* x, int64_t n, int units, int dim, void* out, float4* aux, hipStream_t s);
+hipError_t launch_sq6_scan(const Sq8Params& p, int dim, hipStream_t s, hipEvent_t ev_start = nullptr,
+                           hipEvent_t ev_stop = nullptr);
 hipError_t launch_sq8_settle(int cfg, int nq, const SettleParams& p, hipStream_t s);
 
 int cfg_index(int units);
@@ -341,6 +376,8 @@ struct Tuning {
                               // by this / 100; else the int8 prefilter
     std::atomic<int> mfma_units{0};       // workgroup units of the MFMA candidate pass per view (0: auto)
     std::atomic<int> sq8{1};              // certified int8 prefilter for float32 batches below mfma_min_batch
+    std::atomic<int> sq6{1};              // ...whose single unfiltered queries scan the 6-bit tier where the dim has one,
+    std::atomic<int> sq6_probe_pct{10};   // ...unless its first calls on a view re-bound more than this % of the rows
     std::atomic<int> gather_min{0};       // ...at most one gather tile per this many accepted rows (0 = every gather
                                           // tile; fewer, longer tiles were slower: profiles/r02c/gather_min_ab.jsonl)
     std::atomic<int> sel_writer{2};       // select path bounds writer: 0 U4 + Java transform, 1 U4 fast COSINE

@@ -136,6 +136,8 @@ struct osk_seg {
     void* d_q8 = nullptr;
     float4* d_q8aux = nullptr;
     void* d_q8t = nullptr;    // the int8 rows in sq8_mfma's tiled layout (osk_seg_warm / first batched prefilter)
+    void* d_q6 = nullptr;     // the 6-bit tier (dims with sq6_supported): tiled codes, built with the int8 copy
+    float4* d_q6aux = nullptr;
     int units8 = 0;
     std::mutex mu;
     std::atomic<int> refs{1};          // the reader's reference + one per view that groups the segment
@@ -153,7 +155,7 @@ struct osk_view {
     std::vector<int32_t> shard_index;
     std::vector<int32_t> shard_tile_begin;
     int n_tiles = 0;
-    osk::DevBuf d_segs, d_tiles, d_shard_tile_begin, d_shard_index, d_tile_coff;
+    osk::DevBuf d_segs, d_tiles, d_shard_tile_begin, d_shard_index, d_tile_coff, d_tile_order;
     // workspace
     osk::DevBuf ws_cand, ws_q, ws_qnorm, ws_qin, ws_keys, ws_counts, ws_accept_ptrs, ws_accept,
         ws_out, ws_visited;
@@ -176,6 +178,17 @@ struct osk_view {
     osk::DevBuf d_sq8_rows, d_sq8_aux, d_counters;   // counters: SettleParams::counters
     osk::DevBuf d_sq8_rows_t;                         // per segment: tiled int8 copy (sq8_mfma)
     bool sq8t_ready = false;
+    osk::DevBuf d_sq6_rows, d_sq6_aux;                // per segment: the 6-bit tier (every segment has one or
+    bool sq6_ready = false;                           // the view does not use it)
+    int64_t sq6_calls = 0;
+    osk::DevBuf ws_q6, ws_qc6, ws_floor;              // its query (nibble split, bound terms), floor buckets,
+    osk::DevBuf ws_cand6, ws_cnt6;                    // the streaming pass's candidates per list
+    // the tier's calibration: its first kSq6Probes calls count the rows they re-bound from the int8 copy;
+    // when that exceeds sq6_probe_pct % of the rows scanned the view stops using the tier (data whose
+    // 6-bit bounds do not separate, e.g. uniform EUCLIDEAN rows: DESIGN.md §3f)
+    int sq6_probes = 0;
+    int64_t sq6_probe_rows = 0, sq6_probe_rebound = 0;
+    bool sq6_off = false;
     osk::DevBuf ws_q8, ws_qc, ws_sq8cand, ws_sq8lb, ws_lbmax, ws_trace;
     // settle slices: kSliceLists wave lists each, never spanning shards (an empty shard gets one
     // empty slice so that its result is still written)

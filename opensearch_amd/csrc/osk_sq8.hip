@@ -105,16 +105,19 @@ hipError_t launch_sq8_quantize(const float4* x, int64_t n, int units, int pitch,
 //     slower scan, its extra sdot4 work is not free at the HBM ceiling; so int8 it is)
 //   * flags[r] = 0.
 // ------------------------------------------------------------------------------------------------
-template <int L, int V>
+//   Q6 (single queries of the 6-bit tier, osk_sq6.hip): also its second quantisation of the query, to
+//   [-119, 119] (s6 = max|b|/119), split into signed nibbles b = 16·bh + bl and written in sq6_scan's
+//   layout (64·C dwords per query) with its bound terms, and the query's floor buckets zeroed.
+template <int L, int V, bool Q6>
 __global__ __launch_bounds__(kBlock) void sq8_prep(const float* __restrict__ src, int dim, int nq, int nq_pad,
                                                    int UP, int units8, float4* __restrict__ qpad,
                                                    float* __restrict__ qnorm, uint32_t* __restrict__ q8,
-                                                   float4* __restrict__ qc, int* __restrict__ flags) {
+                                                   float4* __restrict__ qc, int* __restrict__ flags, Sq6Prep q6) {
     // one workgroup per query: every element is loaded once, by one thread, and the reductions are
     // block-wide (a single wave per query walks 768 floats three times: ~8 µs of latency)
     __shared__ float s_m[4];
-    __shared__ long long s_a[4];
-    __shared__ double s_e[4], s_x[4];
+    __shared__ long long s_a[2][4];
+    __shared__ double s_e[2][4], s_x[4];
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform: scalar loop control
     const int64_t r = blockIdx.x;
     const bool real = r < nq;
@@ -135,6 +138,8 @@ __global__ __launch_bounds__(kBlock) void sq8_prep(const float* __restrict__ src
     }
     for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
     if (lane == 0) s_m[wave] = m;
+    if constexpr (Q6)
+        for (int i = tid; i < q6.floor_n; i += kBlock) q6.floor[r * q6.floor_n + i] = 0u;
     // device-order |q|² (wave 0): lane t of every L-lane group computes the same partial
     if (wave == 0) {
         const int t = lane & (L - 1);
@@ -152,16 +157,17 @@ __global__ __launch_bounds__(kBlock) void sq8_prep(const float* __restrict__ src
     }
     __syncthreads();
     m = fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]));
-    const float s8 = m / 127.0f;
-    long long a8 = 0;
-    double e8 = 0.0, sx = 0.0;
+    const float s8 = m / 127.0f, s6 = m / 119.0f;
+    long long a8 = 0, a6 = 0;
+    double e8 = 0.0, e6 = 0.0, sx = 0.0;
+    __shared__ uint32_t s_qb[Q6 ? kPer * kBlock : 1];   // Q6: the [-119, 119] codes of every dim, then split
     uint32_t* p0 = q8 + r * dw;
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
         const int d = u * kBlock + tid;
-        if (d >= dw) break;
+        if (!Q6 && d >= dw) break;
         const float xs[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
-        uint32_t w0 = 0u;
+        uint32_t w0 = 0u, w6 = 0u;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int qi = s8 > 0.0f ? (int)fminf(fmaxf(rintf(xs[e] / s8), -127.0f), 127.0f) : 0;
@@ -170,72 +176,78 @@ __global__ __launch_bounds__(kBlock) void sq8_prep(const float* __restrict__ src
             const double r8 = (double)xs[e] - (double)s8 * (double)qi;   // exact in double
             e8 += r8 * r8;
             sx += (double)xs[e] * (double)xs[e];
+            if constexpr (Q6) {
+                const int q6i = s6 > 0.0f ? (int)fminf(fmaxf(rintf(xs[e] / s6), -119.0f), 119.0f) : 0;
+                w6 |= ((uint32_t)q6i & 0xFFu) << (8 * e);
+                a6 += (long long)(q6i * q6i);
+                const double r6 = (double)xs[e] - (double)s6 * (double)q6i;
+                e6 += r6 * r6;
+            }
         }
-        p0[d] = w0;
+        if (d < dw) p0[d] = w0;
+        if constexpr (Q6) s_qb[d] = w6;   // (zero past dim)
+    }
+    if constexpr (Q6) {
+        __syncthreads();
+        // dword w = hc·8 + m: m < 4 bh, m ≥ 4 bl of dims 32hc + 8(m & 3) + n in nibble n
+        uint32_t* p6 = q6.q6 + r * 64 * q6.C;
+        for (int w = tid; w < 64 * q6.C; w += kBlock) {
+            const int hc = w >> 3, mm = w & 3;
+            const bool low = (w & 4) != 0;
+            const uint32_t d0 = s_qb[8 * hc + 2 * mm], d1 = s_qb[8 * hc + 2 * mm + 1];
+            uint32_t o = 0u;
+#pragma unroll
+            for (int n = 0; n < 8; ++n) {
+                const int qb = (int)(int8_t)((n < 4 ? d0 >> (8 * n) : d1 >> (8 * (n - 4))) & 0xFFu);
+                const int bl = ((qb + 8) & 15) - 8, bh = (qb - bl) >> 4;
+                o |= ((uint32_t)(low ? bl : bh) & 15u) << (4 * n);
+            }
+            p6[w] = o;
+        }
     }
     for (int o = 32; o >= 1; o >>= 1) {
         a8 += __shfl_xor(a8, o);
         e8 += __shfl_xor(e8, o);
         sx += __shfl_xor(sx, o);
+        if constexpr (Q6) {
+            a6 += __shfl_xor(a6, o);
+            e6 += __shfl_xor(e6, o);
+        }
     }
     if (lane == 0) {
-        s_a[wave] = a8;
-        s_e[wave] = e8;
+        s_a[0][wave] = a8;
+        s_e[0][wave] = e8;
+        s_a[1][wave] = a6;
+        s_e[1][wave] = e6;
         s_x[wave] = sx;
     }
     __syncthreads();
     if (tid == 0) {
-        a8 = s_a[0] + s_a[1] + s_a[2] + s_a[3];
-        e8 = s_e[0] + s_e[1] + s_e[2] + s_e[3];
         sx = s_x[0] + s_x[1] + s_x[2] + s_x[3];
-        const double A8 = (double)s8 * sqrt((double)a8) * (1.0 + 1e-12), B8 = sqrt(e8) * (1.0 + 1e-12);
-        qc[r] = make_float4(s8, f32_round_up(B8), f32_round_up((A8 + B8) * (1.0 + 1e-12)), (float)sx);
+        auto terms = [&](int i, float sc) {
+            const long long a = s_a[i][0] + s_a[i][1] + s_a[i][2] + s_a[i][3];
+            const double e = s_e[i][0] + s_e[i][1] + s_e[i][2] + s_e[i][3];
+            const double A = (double)sc * sqrt((double)a) * (1.0 + 1e-12), B = sqrt(e) * (1.0 + 1e-12);
+            return make_float4(sc, f32_round_up(B), f32_round_up((A + B) * (1.0 + 1e-12)), (float)sx);
+        };
+        qc[r] = terms(0, s8);
+        if constexpr (Q6) q6.qc6[r] = terms(1, s6);
         if (real) flags[r] = 0;
     }
 }
 
-using PrepFn = void (*)(const float*, int, int, int, int, int, float4*, float*, uint32_t*, float4*, int*);
-static const PrepFn kPrep[9] = {sq8_prep<4, 2>,  sq8_prep<8, 2>,  sq8_prep<8, 4>,  sq8_prep<16, 4>, sq8_prep<16, 8>,
-                                sq8_prep<16, 12>, sq8_prep<32, 8>, sq8_prep<64, 8>, sq8_prep<64, 16>};
+using PrepFn = void (*)(const float*, int, int, int, int, int, float4*, float*, uint32_t*, float4*, int*, Sq6Prep);
+#define OSK_PREP_ROW(Q6)                                                                                       \
+    {sq8_prep<4, 2, Q6>,   sq8_prep<8, 2, Q6>,  sq8_prep<8, 4, Q6>,  sq8_prep<16, 4, Q6>, sq8_prep<16, 8, Q6>, \
+     sq8_prep<16, 12, Q6>, sq8_prep<32, 8, Q6>, sq8_prep<64, 8, Q6>, sq8_prep<64, 16, Q6>}
+static const PrepFn kPrep[2][9] = {OSK_PREP_ROW(false), OSK_PREP_ROW(true)};
 
 hipError_t launch_sq8_prep(int cfg, const float* src, int dim, int nq, int nq_pad, int UP, int units8, float4* qpad,
-                           float* qnorm, void* q8, float4* qc, int* flags, hipStream_t s) {
-    hipLaunchKernelGGL(kPrep[cfg], dim3(nq_pad), dim3(kBlock), 0, s, src, dim, nq, nq_pad, UP, units8, qpad,
-                       qnorm, static_cast<uint32_t*>(q8), qc, flags);
+                           float* qnorm, void* q8, float4* qc, int* flags, hipStream_t s, const Sq6Prep& q6) {
+    if (q6.C < 0 || q6.C > 8) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(kPrep[q6.C > 0][cfg], dim3(nq_pad), dim3(kBlock), 0, s, src, dim, nq, nq_pad, UP, units8, qpad,
+                       qnorm, static_cast<uint32_t*>(q8), qc, flags, q6);
     return hipGetLastError();
-}
-
-// Quick-reject threshold of a wave list whose worst upper-bound key is `thr` (0 = list not full):
-// a row whose bound fails sq8_pass has upper-bound score ≤ the list's worst score, so it cannot
-// enter the list (the precise test below decides the rest).
-//   EUCLIDEAN: d² threshold; COSINE: dot threshold per |x|; others: dot threshold.
-__device__ __forceinline__ float sq8_quick(int sim, uint64_t thr, float sqn, float cos_slack) {
-    if (thr == 0ull) return sim == SIM_EUCLIDEAN ? __builtin_inff() : -__builtin_inff();
-    const float t = key_score(thr);
-    switch (sim) {
-        case SIM_EUCLIDEAN: {
-            const float tm = t * (1.0f - 0x1p-16f);
-            return tm > 0.0f ? 1.0f / tm - 1.0f : __builtin_inff();
-        }
-        case SIM_MIP: {
-            const float tm = t * (1.0f - 0x1p-16f);
-            if (!(tm > 0.0f)) return -__builtin_inff();
-            return tm >= 1.0f ? tm - 1.0f : 1.0f - 1.0f / tm;
-        }
-        case SIM_DOT_PRODUCT: {
-            const float tm = t - 0x1p-16f * fabsf(t) - 0x1p-20f;
-            return 2.0f * tm - 1.0f;
-        }
-        default: {   // COSINE
-            const float tm = t - 0x1p-16f * fabsf(t) - 0x1p-20f;
-            return (2.0f * tm - 1.0f - cos_slack) * sqn;
-        }
-    }
-}
-__device__ __forceinline__ bool sq8_pass(int sim, float lo, float hi, float tq, float sx) {
-    if (sim == SIM_EUCLIDEAN) return !(lo > tq);
-    if (sim == SIM_COSINE) return !(hi < tq * sx);
-    return !(hi < tq);
 }
 
 // Reduce-scatter of NQ per-query partial dots over the L lanes of a row: H = min(log2 NQ, log2 L)
