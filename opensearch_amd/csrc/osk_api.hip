@@ -1272,7 +1272,7 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     Sq6Prep q6{};
     if (use6) {
         q6.C = sq6_chunks(v->dim);
-        q6.floor_n = S * kFloorBuckets * kFloorStride;
+        q6.floor_n = S * (kFloorBuckets + 1) * kFloorStride;   // buckets + the floor cell per shard
         OSK_HIP(v->ws_q6.reserve((size_t)nq_pad * 256 * q6.C));
         OSK_HIP(v->ws_qc6.reserve(sizeof(float4) * nq_pad));
         OSK_HIP(v->ws_floor.reserve(sizeof(uint32_t) * (size_t)nq_pad * q6.floor_n));

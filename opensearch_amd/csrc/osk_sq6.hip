@@ -162,17 +162,21 @@ __device__ __forceinline__ uint32_t wave_kth_largest(uint32_t v, int lane, int k
 }
 
 // A lower bound of the exact score of a row whose raw device-order value is ≥ lo (dot kinds) or whose d²
-// is ≤ hi (EUCLIDEAN), for the floor: COSINE takes |x|² from the bound terms (Σx² in double, rounded)
-// instead of the device-order norm the exact score divides by, so the norm is widened by g2 (≥ the
-// device order's relative rounding) on the side that lowers the score, and the result by 2^-20.
+// is ≤ hi (EUCLIDEAN), for the floor only (never returned), in float arithmetic: COSINE takes |x|² from
+// the bound terms (Σx² in double, rounded) instead of the device-order norm the exact score divides by,
+// so the norm is widened by g2 (≥ the device order's relative rounding) on the side that lowers the
+// score, v_rsq's 1-ulp error and the few float roundings are covered by 2^-18, and the result is lowered
+// by 2^-18 more (Java's double cosine and float transform are within an ulp or two of it).
 __device__ __forceinline__ float floor_lb_score(int sim, float lo, float hi, float qnd, float xn_aux, float g2) {
-    if (sim == SIM_EUCLIDEAN) return score_f32_l2(hi) * (1.0f - 0x1p-20f);
-    if (sim != SIM_COSINE) return score_f32(sim, lo, qnd, 0.0f) * (1.0f - 0x1p-20f);
+    if (sim == SIM_EUCLIDEAN) return score_f32_l2(hi) * (1.0f - 0x1p-18f);
+    if (sim != SIM_COSINE) return score_f32(sim, lo, qnd, 0.0f) * (1.0f - 0x1p-18f);
     const float xn = lo >= 0.0f ? xn_aux * (1.0f + g2) : xn_aux * (1.0f - g2);
-    return score_f32_cos(lo, qnd, xn) * (1.0f - 0x1p-20f);
+    float c = lo * __builtin_amdgcn_rsqf(qnd * xn);
+    c = c >= 0.0f ? c * (1.0f - 0x1p-18f) : c * (1.0f + 0x1p-18f);
+    return fmaxf((1.0f + c) * 0.5f, 0.0f) * (1.0f - 0x1p-18f);
 }
 
-// Sampled int8 lower bounds seed the floor before the streaming pass: each wave scores the first 8 rows
+// Sampled int8 lower bounds seed the floor before the streaming pass: each wave scores the first 4 rows
 // of its range (the 6-bit pass's split) on the int8 copy (16 lanes per row, exact device-order norms)
 // and raises its floor bucket (list mod 64) to the best of them.
 template <int C>
@@ -191,15 +195,16 @@ __global__ __launch_bounds__(kBlock) void sq6_pilot(Sq8Params p) {
     const int64_t we = min(wb + per_wave, tile.row_end);
     const float4 qc = p.qc[0];
     const float qnd = sim == SIM_COSINE ? p.qn_dev[0] : 0.0f;
-    // both 4-row passes' loads first (u8 ≤ 16·C units: C per lane), one round trip
-    int4 xv[2][C], qv[C];
-    float4 ax[2];
-    float xnd[2] = {0.0f, 0.0f};
-    bool v[2];
+    // the first 4 rows of the wave's range (1 % of the rows), 16 lanes each (u8 ≤ 16·C units: C per lane)
+    constexpr int H = 1;
+    int4 xv[H][C], qv[C];
+    float4 ax[H];
+    float xnd[H] = {0.0f};
+    bool v[H];
 #pragma unroll
     for (int i = 0; i < C; ++i) qv[i] = ct + 16 * i < u8 ? p.q8[ct + 16 * i] : make_int4(0, 0, 0, 0);
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < H; ++h) {
         const int64_t r = wb + 4 * h + cg;
         v[h] = r < we;
         const int64_t rc = v[h] ? r : tile.row_begin;
@@ -211,7 +216,7 @@ __global__ __launch_bounds__(kBlock) void sq6_pilot(Sq8Params p) {
     }
     uint32_t best = 0u;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < H; ++h) {
         int a8 = 0;
 #pragma unroll
         for (int i = 0; i < C; ++i) {
@@ -229,7 +234,7 @@ __global__ __launch_bounds__(kBlock) void sq6_pilot(Sq8Params p) {
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) best = max(best, (uint32_t)__shfl_xor((int)best, o));
-    uint32_t* fb = p.floor + ((size_t)p.q0 * p.n_shards + tile.shard) * kFloorBuckets * kFloorStride;
+    uint32_t* fb = p.floor + ((size_t)p.q0 * p.n_shards + tile.shard) * (kFloorBuckets + 1) * kFloorStride;
     if (lane == 0 && best) atomicMax(fb + ((tix * 4 + wave) & (kFloorBuckets - 1)) * kFloorStride, best);
 }
 
@@ -273,32 +278,46 @@ __global__ __launch_bounds__(kBlock, 4) void sq6_scan(Sq8Params p) {   // ≤ 12
     const int64_t we = min(wb + per_wave, tile.row_end);
 
     const int list = tix * 4 + wave;
-    uint32_t* fb = p.floor + ((size_t)p.q0 * p.n_shards + tile.shard) * kFloorBuckets * kFloorStride;
+    uint32_t* fb = p.floor + ((size_t)p.q0 * p.n_shards + tile.shard) * (kFloorBuckets + 1) * kFloorStride;
     uint32_t* cbuf = p.cand6 + (size_t)list * p.cap6;
     uint64_t fkey = 0ull;
     uint32_t best = 0u, pub = 0u;
     float tq0 = sq8_quick(sim, 0ull, 0.0f, 0.0f);
     uint32_t nvis = 0;
     int nc = 0, it = 0;
-    // the floor is re-read at the wave's start (the pilot's and earlier tiles' bounds), every iteration
-    // for the first four, then every fourth; each bucket load is issued one refresh ahead
-    uint32_t fv = __hip_atomic_load(fb + lane * kFloorStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t* cell = fb + kFloorBuckets * kFloorStride;   // the shard's floor: max of the k-th values computed
+    auto set_floor = [&](uint32_t f32) {
+        uint64_t f = (uint64_t)f32 << 32;
+        if (!(key_score(f) > 0.0f)) f = 0ull;
+        if (f > fkey) {
+            fkey = f;
+            tq0 = sq8_quick(sim, fkey, sqn0, p.cos_slack);
+        }
+    };
+    // k-th best of the buckets now (the pilot's and earlier tiles' bounds) → the cell and this wave
+    auto recompute = [&](bool write) {
+        const uint32_t v = __hip_atomic_load(fb + lane * kFloorStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t kth = wave_kth_largest(v, lane, p.k);
+        if (write && kth > (uint32_t)(fkey >> 32) && lane == 0) atomicMax(cell, kth);
+        set_floor(kth);
+    };
+    // at the start every wave computes the k-th itself but only one wave in 64 writes the cell: all of a
+    // round's waves start together, and thousands of atomics on one address would queue for 100+ µs
+    if (!(ablate & 2)) recompute((list & (kFloorBuckets - 1)) == 0);
+    // then the cell is re-read every iteration for the first four, every fourth later (one load, issued
+    // a refresh ahead); a wave whose best lower bound can still lift the floor publishes it to its bucket
+    // and recomputes (same-address atomics queue at L2, and the wave's next load waits behind its own)
+    uint32_t cv = __hip_atomic_load(cell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
     for (int64_t r0 = wb; r0 < we; r0 += R * U, ++it) {
         if ((it < 4 || (it & 3) == 0) && !(ablate & 2)) {
-            // this wave's best lower bound so far → its bucket, only when it can still raise the floor:
-            // same-address atomics queue at L2, and the wave's next load waits behind its own atomic
+            set_floor(cv);
             if (best > pub && best > (uint32_t)(fkey >> 32)) {
                 pub = best;
                 if (lane == 0) atomicMax(fb + (list & (kFloorBuckets - 1)) * kFloorStride, best);
+                recompute(true);
             }
-            uint64_t f = (uint64_t)wave_kth_largest(fv, lane, p.k) << 32;
-            if (!(key_score(f) > 0.0f)) f = 0ull;
-            if (f > fkey) {
-                fkey = f;
-                tq0 = sq8_quick(sim, fkey, sqn0, p.cos_slack);
-            }
-            fv = __hip_atomic_load(fb + lane * kFloorStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            cv = __hip_atomic_load(cell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         int4 hv[U][C];
         int2 lv[U][C];
@@ -393,8 +412,9 @@ __global__ __launch_bounds__(kBlock) void sq6_rebound(Sq8Params p) {
     const float4 qc = p.qc[0];
     const float qnd0 = sim == SIM_COSINE ? p.qn_dev[0] : 0.0f;
     const float sqn0 = sqrtf(qnd0);
-    const uint32_t* fb = p.floor + ((size_t)p.q0 * p.n_shards + tile.shard) * kFloorBuckets * kFloorStride;
-    uint64_t fkey = (uint64_t)wave_kth_largest(fb[lane * kFloorStride], lane, p.k) << 32;
+    const uint32_t* fb = p.floor + ((size_t)p.q0 * p.n_shards + tile.shard) * (kFloorBuckets + 1) * kFloorStride;
+    uint64_t fkey = (uint64_t)max(wave_kth_largest(fb[lane * kFloorStride], lane, p.k),
+                                  fb[kFloorBuckets * kFloorStride]) << 32;
     if (!(key_score(fkey) > 0.0f)) fkey = 0ull;
     const int nc = p.cnt6[(size_t)p.q0 * p.n_lists + list];
     int4 qv8[C];   // this lane's units of the int8 query
@@ -405,40 +425,51 @@ __global__ __launch_bounds__(kBlock) void sq6_rebound(Sq8Params p) {
     uint32_t lp0 = 0u;
     float tq0 = sq8_quick(sim, fkey, sqn0, p.cos_slack);
     if (nc <= p.cap6) {
-        for (int c0 = 0; c0 < nc; c0 += 4) {
-            const bool v = c0 + cg < nc;
-            const uint32_t r = v ? cbuf[c0 + cg] : 0u;
-            int a8 = 0;
-            // unconditional loads of a clamped row (one round trip), masked after
-            const int4* xr = X8 + (int64_t)r * u8;
-            int4 xv[C];
+        // 8 candidates per pass (two halves of 4 rows × 16 lanes), every load of both halves issued
+        // before any is used: one round trip per 8 candidates
+        for (int c0 = 0; c0 < nc; c0 += 8) {
+            bool v[2];
+            uint32_t r[2];
 #pragma unroll
-            for (int i = 0; i < C; ++i) xv[i] = ct + 16 * i < u8 ? xr[ct + 16 * i] : make_int4(0, 0, 0, 0);
-            const float4 ax = v ? AX8[r] : make_float4(0.f, 0.f, 0.f, 0.f);
-            if (v) {
+            for (int h = 0; h < 2; ++h) {
+                v[h] = c0 + 4 * h + cg < nc;
+                r[h] = v[h] ? cbuf[c0 + 4 * h + cg] : cbuf[0];
+            }
+            int4 xv[2][C];
+            float4 ax[2];
+            float xnd[2] = {0.0f, 0.0f};
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {   // unconditional loads of clamped rows, masked after
+                const int4* xr = X8 + (int64_t)r[h] * u8;
+#pragma unroll
+                for (int i = 0; i < C; ++i) xv[h][i] = ct + 16 * i < u8 ? xr[ct + 16 * i] : make_int4(0, 0, 0, 0);
+                ax[h] = AX8[r[h]];
+                if (sim == SIM_COSINE) xnd[h] = seg.xnorm_f[r[h]];
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                int a8 = 0;
 #pragma unroll
                 for (int i = 0; i < C; ++i) {
                     const int4 qv = qv8[i];
-                    a8 = __builtin_amdgcn_sdot4(xv[i].x, qv.x, a8, false);
-                    a8 = __builtin_amdgcn_sdot4(xv[i].y, qv.y, a8, false);
-                    a8 = __builtin_amdgcn_sdot4(xv[i].z, qv.z, a8, false);
-                    a8 = __builtin_amdgcn_sdot4(xv[i].w, qv.w, a8, false);
+                    a8 = __builtin_amdgcn_sdot4(xv[h][i].x, qv.x, a8, false);
+                    a8 = __builtin_amdgcn_sdot4(xv[h][i].y, qv.y, a8, false);
+                    a8 = __builtin_amdgcn_sdot4(xv[h][i].z, qv.z, a8, false);
+                    a8 = __builtin_amdgcn_sdot4(xv[h][i].w, qv.w, a8, false);
                 }
-            }
 #pragma unroll
-            for (int m = 1; m < 16; m <<= 1) a8 += __shfl_xor(a8, m);
-            float lo, hi;
-            sq8_bounds(sim, (float)a8, ax, qc, p.gam, p.g2, lo, hi);
-            const float sx = sim == SIM_COSINE ? __builtin_amdgcn_sqrtf(ax.w) : 0.0f;
-            const bool pass = v && sq8_pass(sim, lo, hi, tq0, sx);
-            if (__ballot(pass && ct == 0)) {
-                float xnd = 0.0f;
-                if (sim == SIM_COSINE && pass) xnd = seg.xnorm_f[r];
-                const float ub = sim == SIM_EUCLIDEAN ? score_f32_l2(lo) : score_f32(sim, hi, qnd0, xnd);
-                const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qnd0, xnd);
-                const uint64_t key = pass ? make_key(ub, vbase + r) : 0ull;
-                wave_offer2(key, float_to_sortable(lb), pass && ct == 0, lk0, lp0, thr0, lane, kKQ);
-                tq0 = sq8_quick(sim, max(thr0, fkey), sqn0, p.cos_slack);
+                for (int m = 1; m < 16; m <<= 1) a8 += __shfl_xor(a8, m);
+                float lo, hi;
+                sq8_bounds(sim, (float)a8, ax[h], qc, p.gam, p.g2, lo, hi);
+                const float sx = sim == SIM_COSINE ? __builtin_amdgcn_sqrtf(ax[h].w) : 0.0f;
+                const bool pass = v[h] && sq8_pass(sim, lo, hi, tq0, sx);
+                if (__ballot(pass && ct == 0)) {
+                    const float ub = sim == SIM_EUCLIDEAN ? score_f32_l2(lo) : score_f32(sim, hi, qnd0, xnd[h]);
+                    const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qnd0, xnd[h]);
+                    const uint64_t key = pass ? make_key(ub, vbase + r[h]) : 0ull;
+                    wave_offer2(key, float_to_sortable(lb), pass && ct == 0, lk0, lp0, thr0, lane, kKQ);
+                    tq0 = sq8_quick(sim, max(thr0, fkey), sqn0, p.cos_slack);
+                }
             }
         }
     } else if (lane == kKQ - 1) {
