@@ -302,7 +302,7 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         {"sq8_mfma_ablate", &g_tuning.sq8_mfma_ablate, 0, 15, true},   // (also sq6_scan's: 1 no re-bound, 2 no floor)
         {"sq8_force_fallback", &g_tuning.sq8_force_fallback, 0, 1, true},
         {"settle_trace", &g_tuning.settle_trace, 0, 1, true},
-        {"mfma_ablate", &g_tuning.mfma_ablate, 0, 31, true},
+        {"mfma_ablate", &g_tuning.mfma_ablate, 0, 255, true},
     };
     for (const Knob& kn : knobs) {
         if (k != kn.name) continue;
@@ -952,6 +952,11 @@ int32_t batched_search(osk_view* v, int nq, int k, int UP, const uint64_t* const
     mp.nq_pad = std::min(nq_pad, (int)(v->ws_qnorm.cap / sizeof(float)));
     mp.sim = v->sim;
     mp.ablate = g_tuning.mfma_ablate;
+    if (!v->d_mfma_full.p) {
+        OSK_HIP(v->d_mfma_full.reserve(sizeof(unsigned long long)));
+        OSK_HIP(hipMemsetAsync(v->d_mfma_full.p, 0, sizeof(unsigned long long), st));
+    }
+    mp.full_tiles = v->d_mfma_full.as<unsigned long long>();
     mp.n_shards = S;
     OSK_HIP(v->ws_akeys.reserve(sizeof(uint64_t) * (size_t)nq * S * kKC));
     OSK_HIP(v->ws_acounts.reserve(sizeof(int32_t) * (size_t)nq * S));
@@ -1832,6 +1837,16 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
     if (n == "sq8_slices") {
         std::lock_guard<std::mutex> lk(v->mu);
         *value = v->n_slices;
+        return OSK_OK;
+    }
+    if (n == "mfma_full_tiles") {   // (root view only)
+        std::lock_guard<std::mutex> lk(v->mu);
+        unsigned long long c = 0;
+        if (v->d_mfma_full.p) {
+            OSK_HIP(hipDeviceSynchronize());
+            OSK_HIP(hipMemcpy(&c, v->d_mfma_full.p, sizeof(c), hipMemcpyDeviceToHost));
+        }
+        *value = (int64_t)c;
         return OSK_OK;
     }
     const bool dev = n == "sq8_fallback_queries" || n == "sq8_rescored_rows" || n == "sq8_exact_tiles" ||

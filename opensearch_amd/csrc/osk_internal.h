@@ -79,6 +79,7 @@ struct MfmaParams {
     int nq_pad;
     int ablate;
     int sim;
+    unsigned long long* full_tiles;   // tiles whose epilogue took the staging path (counter "mfma_full_tiles")
 };
 
 struct RescoreParams {
@@ -397,7 +398,8 @@ struct Tuning {
     std::atomic<int> sq8_force_fallback{0};   // TESTING. tests: every list of a prefiltered search is re-scanned exactly
     std::atomic<int> settle_trace{0};     // TESTING. A/B only: record settle phase timestamps (debug copy "settle_trace")
     std::atomic<int> mfma_ablate{0};      // TESTING. A/B only: 1 skip the epilogue, 2 skip query staging, 4 skip corpus staging,
-                              // 8 force the full staging epilogue, 16 skip the pilot pass
+                              // 8 force the full staging epilogue, 16 skip the pilot pass, 32 skip the
+                              // main epilogue's quick tests, 64 skip its merge (barriers + list inserts)
                               // (results are wrong and the exact fallback is skipped)
 };
 extern Tuning g_tuning;

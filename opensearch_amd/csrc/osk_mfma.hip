@@ -184,7 +184,10 @@ __device__ __forceinline__ void list_insert(uint64_t (&lst)[kKC], uint64_t key) 
 
 // PILOT = true: only the first tile of each unit, every score staged (the lists it leaves are
 // merged per (query, shard) into the thresholds of the main pass).
-template <bool PILOT>
+// SIM is compile-time: with the similarity a runtime value every unrolled scoring site carried all
+// four transforms (260 IEEE divisions, 17k instructions in one kernel: more than the instruction cache
+// holds, so the epilogue's rare paths missed it on every tile).
+template <bool PILOT, int SIM>
 __global__ __launch_bounds__(kMB) void mfma_cand(MfmaParams p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float* staged = reinterpret_cast<float*>(smem + kOffStaged);
@@ -198,7 +201,8 @@ __global__ __launch_bounds__(kMB) void mfma_cand(MfmaParams p) {
     const SegDev seg = p.segs[unit.seg];
     const char* __restrict__ A = static_cast<const char*>(p.seg_split[unit.seg]);
     const int qblock = blockIdx.y;
-    const int KS = p.KS, sim = p.sim;
+    const int KS = p.KS;
+    constexpr int sim = SIM;
     // this wave's two 16-query blocks, fragment-ordered [qb][ks][hi/lo][64 lanes][16 B]
     const char* __restrict__ Bw = static_cast<const char*>(p.qsplit) +
                                   (size_t)(qblock * 16 + wave * 2) * KS * 2048 + lane * 16;
@@ -352,53 +356,110 @@ __global__ __launch_bounds__(kMB) void mfma_cand(MfmaParams p) {
         // (query, row quarter) thread offers its 32 rows of the half to its list.
         bool full = PILOT || (p.ablate & 8);
         if (!full) {
-            // Per query a dot-product bound equivalent to "approx score ≥ threshold", loosened by
-            // 2^-16·max(1, |t|) (far above the rounding of either form): d ≥ cq·a_row, a = |x| for
-            // COSINE, else 1.  Only rows past it get the exact approx score and the real test.
+            // Per query a bound equivalent to "approx score ≥ threshold" in the dot domain, loosened by
+            // 2^-16·max(1, |t|) (far above the rounding of either form), evaluated branch-free as
+            //   α·d − β·v_row ≥ γ_q:
+            //   COSINE      α = 1, β = cq_q, v = |x|, γ = 0              (d ≥ cq·|x|)
+            //   DOT / MIP   α = 1, β = 0, γ = cq_q                       (d ≥ cq)
+            //   EUCLIDEAN   α = 2, β = 1 − 2^-18, v = |x|², γ = |q|² − D − 2^-18·(|q|² + D), D = 1/tm − 1
+            //               (1/(1 + max(|x|² + |q|² − 2d, 0)) ≥ tm ⟸ 2d − |x|² ≥ |q|² − D; the 2^-18 terms
+            //               cover the float rounding of both sides, 2|d| ≤ |x|² + |q|²)
+            // Only a row block (8 pairs per lane) with a passing lane in the wave runs the exact approx
+            // score and the real test; the per-pair branches of that path cost 0.36 of the 0.66 ms of a C2
+            // b256 search when every pair took them (EUCLIDEAN had no quick test).
             uint32_t thr_l[2];
-            float cq[2];
+            float be[2], ga[2];
+            const bool cosine = sim == SIM_COSINE, l2 = sim == SIM_EUCLIDEAN;
+            const float al = l2 ? 2.0f : 1.0f;
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 thr_l[j] = s_thr[wave * 32 + j * 16 + (lane & 15)];
                 const float t = sortable_to_float(thr_l[j]);
-                const float tm = t - 0x1p-16f * fmaxf(1.0f, fabsf(t));
+                // EUCLIDEAN scores 1/(1 + d²) are tiny at large d² (≈ 3e-6 on C2's SIFT-like rows): an
+                // absolute 2^-16 slack made tm negative and let every pair through to the exact test
+                // (half of all (row, query) pairs: 0.37 of 0.71 ms at C2 b256), so its slack is relative
+                const float tm = l2 ? t * (1.0f - 0x1p-16f) : t - 0x1p-16f * fmaxf(1.0f, fabsf(t));
                 float c = -__builtin_inff();
                 if (thr_l[j] != 0u) {
                     if (sim == SIM_COSINE) c = (2.0f * tm - 1.0f) * sqrtf(qn_l[j]);
                     else if (sim == SIM_DOT_PRODUCT) c = 2.0f * tm - 1.0f;
                     else if (sim == SIM_MIP && tm > 0.0f) c = tm >= 1.0f ? tm - 1.0f : 1.0f - 1.0f / tm;
+                    else if (l2 && tm > 0.0f) {
+                        const float D = 1.0f / tm - 1.0f, qn = qn_l[j];
+                        c = (qn - D) - 0x1p-18f * (fabsf(qn) + fabsf(D));
+                    }
                 }
                 // padded query columns (batch not a multiple of 256) have no threshold: without this
                 // every one of their accumulators would pass, overflow the slots and send every
                 // tile down the full path (C2 b128: 1.18 ms against 0.65 at b256)
                 const int qg = qblock * 256 + wave * 32 + j * 16 + (lane & 15);
-                cq[j] = qg < p.nq ? c : __builtin_inff();
+                c = qg < p.nq ? c : __builtin_inff();
+                if (cosine) {   // d − c·|x| ≥ 0; ±∞ (no threshold / padded column): always / never
+                    const bool fin = c > -__builtin_inff() && c < __builtin_inff();
+                    be[j] = fin ? c : 0.0f;
+                    ga[j] = fin ? 0.0f : c;
+                } else {
+                    be[j] = l2 ? 1.0f - 0x1p-18f : 0.0f;
+                    ga[j] = c;
+                }
             }
-            const bool cosine = sim == SIM_COSINE;
+            const float* vrow = cosine ? xr : xs;
+            uint32_t mh[2] = {0u, 0u};   // pass masks per half tile: bit (i & 3)·8 + r·2 + j
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
+            for (int i = 0; i < 8; ++i) {
+                if (p.ablate & 32) break;   // A/B: no quick tests
+                const int rl0 = i * 16 + (lane >> 4) * 4;
+                const float4 v4 = (cosine || l2) ? *reinterpret_cast<const float4*>(vrow + rl0)
+                                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+                const float vr[4] = {v4.x, v4.y, v4.z, v4.w};
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row_local = i * 16 + (lane >> 4) * 4 + r;
-                    const float a = cosine ? xr[row_local] : 1.0f;
+                for (int r = 0; r < 4; ++r)
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {
-                        if (!(acc[i][j][r] < cq[j] * a)) {   // (NaN goes to the exact test)
-                            const int64_t row = tile_rb0 * 16 + row_local;
-                            if (row >= seg.n_rows) continue;
-                            const float s = approx_score(sim, acc[i][j][r], qn_l[j], xs[row_local]);
-                            if (float_to_sortable(s) < thr_l[j]) continue;
-                            if (abits) {
-                                const int32_t doc = seg.ord_to_doc ? seg.ord_to_doc[row] : (int32_t)row;
-                                if (!((abits[doc >> 6] >> (doc & 63)) & 1ull)) continue;
-                            }
-                            const int ql = wave * 32 + j * 16 + (lane & 15);
-                            const int slot = atomicAdd(&s_cnt[ql], 1);
-                            if (slot < kSlots) s_slot[ql * kSlots + slot] = make_key(s, (uint32_t)(unit.vrow_base + row));
-                            else s_ovf[0] = 1;
-                        }
+                        const float lhs = fmaf(al, acc[i][j][r], -be[j] * vr[r]);
+                        mh[i >> 2] |= !(lhs < ga[j]) ? (1u << ((i & 3) * 8 + r * 2 + j)) : 0u;   // (NaN passes)
                     }
+            }
+            // the pairs that pass: this wave stages its own 32 query columns of the half tile in LDS (no
+            // other wave touches them, so no barrier) and each lane walks its own passing pairs in a
+            // rolled loop — one copy of the exact test and the slot insertion instead of 64 unrolled
+            // ones (the kernel outgrew the instruction cache)
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                if (p.ablate & 128) {   // A/B: quick tests only (results wrong)
+                    if (mh[half] == 0xFFFFFFFFu) s_ovf[1] = 1;
+                    continue;
                 }
+                if (!__ballot(mh[half] != 0u)) continue;   // wave-uniform
+
+#pragma unroll
+                for (int i = half * 4; i < half * 4 + 4; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j)
+                            staged[(i * 16 + (lane >> 4) * 4 + r - half * 64) * kStagePitch + wave * 32 + j * 16 + (lane & 15)] =
+                                acc[i][j][r];
+                for (uint32_t m = mh[half]; m; m &= m - 1u) {
+                    const int e = __builtin_ctz(m);
+                    const int i = half * 4 + (e >> 3), r = (e >> 1) & 3, j = e & 1;
+                    const int row_local = i * 16 + (lane >> 4) * 4 + r;
+                    const int ql = wave * 32 + j * 16 + (lane & 15);
+                    const int64_t row = tile_rb0 * 16 + row_local;
+                    if (row >= seg.n_rows) continue;
+                    const float d = staged[(row_local - half * 64) * kStagePitch + ql];
+                    const float sc = approx_score(sim, d, j ? qn_l[1] : qn_l[0], xs[row_local]);
+                    if (float_to_sortable(sc) < (j ? thr_l[1] : thr_l[0])) continue;
+                    if (abits) {
+                        const int32_t doc = seg.ord_to_doc ? seg.ord_to_doc[row] : (int32_t)row;
+                        if (!((abits[doc >> 6] >> (doc & 63)) & 1ull)) continue;
+                    }
+                    const int slot = atomicAdd(&s_cnt[ql], 1);
+                    if (slot < kSlots) s_slot[ql * kSlots + slot] = make_key(sc, (uint32_t)(unit.vrow_base + row));
+                    else s_ovf[0] = 1;
+                }
+            }
+            if (p.ablate & 64) continue;   // A/B: no merge (results wrong)
             __syncthreads();
             full = s_ovf[0] != 0;   // uniform
             if (h_sel == 0) {
@@ -413,6 +474,7 @@ __global__ __launch_bounds__(kMB) void mfma_cand(MfmaParams p) {
             if (tid == 0) s_ovf[0] = 0;
         }
         if (full) {
+            if (!PILOT && p.full_tiles && tid == 0) atomicAdd(p.full_tiles, 1ull);
 #pragma unroll
             for (int half = 0; half < 2; ++half) {
 #pragma unroll
@@ -462,20 +524,24 @@ __global__ __launch_bounds__(kMB) void mfma_cand(MfmaParams p) {
         atomicAdd(&p.visited[unit.seg], (unsigned long long)nvis);
 }
 
+using MfmaCandFn = void (*)(MfmaParams);
+static const MfmaCandFn kMfmaCand[2][4] = {
+    {mfma_cand<false, 0>, mfma_cand<false, 1>, mfma_cand<false, 2>, mfma_cand<false, 3>},
+    {mfma_cand<true, 0>, mfma_cand<true, 1>, mfma_cand<true, 2>, mfma_cand<true, 3>}};
+
 hipError_t launch_mfma_cand(const MfmaParams& p, int n_qblocks, bool pilot, hipStream_t s) {
-    if (p.KS % kDepth != 0) return hipErrorInvalidValue;
+    if (p.KS % kDepth != 0 || p.sim < 0 || p.sim > 3) return hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)mfma_cand<false>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTotal);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)mfma_cand<true>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTotal);
-        if (e != hipSuccess) return e;
+        for (int pl = 0; pl < 2; ++pl)
+            for (int sm = 0; sm < 4; ++sm) {
+                const hipError_t e = hipFuncSetAttribute((const void*)kMfmaCand[pl][sm],
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTotal);
+                if (e != hipSuccess) return e;
+            }
         attr_set = true;
     }
-    if (pilot) hipLaunchKernelGGL(mfma_cand<true>, dim3(p.n_units, n_qblocks), dim3(kMB), kLdsTotal, s, p);
-    else hipLaunchKernelGGL(mfma_cand<false>, dim3(p.n_units, n_qblocks), dim3(kMB), kLdsTotal, s, p);
+    hipLaunchKernelGGL(kMfmaCand[pilot ? 1 : 0][p.sim], dim3(p.n_units, n_qblocks), dim3(kMB), kLdsTotal, s, p);
     return hipGetLastError();
 }
 

@@ -171,6 +171,7 @@ struct osk_view {
         ws_fbcounts;
     osk::HostPinned h_flags;
     int64_t mfma_calls = 0, mfma_fallback_queries = 0;
+    osk::DevBuf d_mfma_full;               // [1] tiles whose candidate epilogue took the staging path
     // certified int8 prefilter
     bool sq8_ready = false;
     int units8 = 0;

@@ -178,6 +178,8 @@ def emit(name, view, batch, ms_step, kernel_ms, bytes_per_launch, extra=None):
         per = 8 if batch < 2 else 32
         b8 = rows * (-(-view.dim // 16) * 16 + 16) * -(-batch // per)
         rec["int8_prefilter_GBps"] = b8 / (kernel_ms * 1e-3) / 1e9
+    if batch >= 96:   # the bf16×3 candidate pass: tiles whose epilogue took the staging path, all calls so far
+        rec["mfma_full_tiles"] = counter(view, "mfma_full_tiles")
     if extra:
         rec.update(extra)
     print(json.dumps(rec), flush=True)
