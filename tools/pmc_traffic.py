@@ -32,7 +32,9 @@ def main():
     out = {}
     for k in f:
         # 16-B-per-lane streaming loads: apply the gfx950 ×2 FETCH correction
-        wide = "scan_f32<" in k or "scan_i8<" in k or "sq8_scan<" in k
+        # (sq6_scan mixes 16-B and 8-B loads: its ×2-corrected bytes match the 5.92 GB of 6-bit codes +
+        # bound terms per C3 search to 0.2 %, profiles/r03b/; sq8_mfma and mfma_cand stream 16-B LDS-DMA)
+        wide = any(t in k for t in ("scan_f32<", "scan_i8<", "sq8_scan<", "sq6_scan<", "sq8_mfma<", "mfma_cand<"))
         rd = f[k] * 1024 * (2 if wide else 1)
         wr = w.get(k, 0.0) * 1024
         out[k] = {"dispatches": n[k], "fetch_kib_raw": f[k], "write_kib_raw": w.get(k),
