@@ -67,18 +67,21 @@ def pmc_traffic(rows_local: int, batch: int, prefilter: bool, six: bool = False)
     """HBM bytes per scan launch from the committed rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes of this
     same command (tools/pmc_traffic.py; gfx950 ×2 FETCH correction applied), scaled to this rank's rows.
     The passes were taken at N=1 (10M rows, batch 1).  None when absent or for another batch size."""
-    if batch != 1 or not os.path.exists(PMC_SUMMARY):
+    path = PMC_SUMMARY_SQ6 if six else PMC_SUMMARY
+    if batch != 1 or not os.path.exists(path):
         return None, None
-    data = json.load(open(PMC_SUMMARY))
+    data = json.load(open(path))
     # (a prefix: the headline instance is sq8_scan<16, 3, 1, 4, MODE>)
     want = "sq6_scan<3, 3>" if six else "sq8_scan<16, 3, 1, 4" if prefilter else "scan_f32<16, 12, 1, false"
     for name, v in data.items():
         if want in name:
-            return v["hbm_bytes"] * rows_local / (N_SHARDS * ROWS_PER_SHARD), os.path.relpath(PMC_SUMMARY, ROOT)
+            return v["hbm_bytes"] * rows_local / (N_SHARDS * ROWS_PER_SHARD), os.path.relpath(path, ROOT)
     return None, None
 
 
 READ_CEILING = os.path.join(ROOT, "profiles", "r02j", "hbm_read_ceiling.json")
+# the 6-bit tier's pass (tools/pmc_round3.sh: FETCH_SIZE / WRITE_SIZE of this bench at N = 1)
+PMC_SUMMARY_SQ6 = os.path.join(ROOT, "profiles", "r03b", "pmc", "pmc_c3b1.json")
 
 
 def read_ceiling():
@@ -403,13 +406,11 @@ def main():
     elif six:
         # the 6-bit codes (3/4 of the int8 row, dims padded to 256 per lane set) + 16-B bound terms of every
         # row, plus the int8 rows + bound terms the scan re-bounded (counted on the device, per launch)
-        n_six = counter("sq6_calls") - six0
-        rebound = (counter("sq6_rebound_rows") - rb0) / max(1, n_six)
         passes = B
-        bytes_per_launch = rows_local * (((DIM + 255) // 256) * 192 + 16) + rebound * (u8 * 16 + 16)
-        kernel_name = ("sq6_scan<C=3,U=3> certified 6-bit first tier (bytes = 6-bit codes + 16-B bound terms per "
-                       "row + the int8 rows + terms re-bounded for the rows that pass the 6-bit test; one query "
-                       "per launch)")
+        bytes_per_launch = rows_local * (((DIM + 255) // 256) * 192 + 16)
+        kernel_name = ("sq6_scan<C=3,U=3> the 6-bit pass of the certified prefilter (bytes = 6-bit codes + 16-B "
+                       "bound terms per row, one query per launch; its pilot and int8 re-bound kernels read "
+                       "≈ 2-3 % more, profiles/r03b/pmc/)")
     elif prefilter:
         passes = (B + 7) // 8
         bytes_per_launch = rows_local * (u8 * 16 + 16) * passes

@@ -338,32 +338,42 @@ __global__ __launch_bounds__(kBlock, 4) void sq6_scan(Sq8Params p) {   // ≤ 12
             }
             ax[u] = AX6[valid[u] ? row[u] : wb];
         }
+        // every group's dot first, then the bounds and tests: the four v_dot8 chains of a group are serial
+        // dependencies, and with the tests (ballot, branch) between groups the compiler could not overlap
+        // one group's chains with the next one's (36 % of the wave cycles were issue stalls)
+        int accu[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            nvis += __popcll(__ballot(t == 0 && valid[u]));
-            const float sx = sim == SIM_COSINE ? __builtin_amdgcn_sqrtf(ax[u].w) : 0.0f;   // (1 ulp ≪ the quick test's slack)
-            int hh = 0, hl = 0, lh = 0, ll = 0;
+            int hh[2] = {0, 0}, hl[2] = {0, 0}, lh[2] = {0, 0}, ll[2] = {0, 0};   // two chains each
 #pragma unroll
             for (int j = 0; j < C; ++j) {
                 const int hw[4] = {hv[u][j].x, hv[u][j].y, hv[u][j].z, hv[u][j].w};
 #pragma unroll
                 for (int m = 0; m < 4; ++m) {
-                    hh = __builtin_amdgcn_sdot8(hw[m], qh[j][m], hh, false);
-                    hl = __builtin_amdgcn_sdot8(hw[m], ql[j][m], hl, false);
+                    hh[m & 1] = __builtin_amdgcn_sdot8(hw[m], qh[j][m], hh[m & 1], false);
+                    hl[m & 1] = __builtin_amdgcn_sdot8(hw[m], ql[j][m], hl[m & 1], false);
                 }
                 const int lw[2] = {lv[u][j].x, lv[u][j].y};
 #pragma unroll
                 for (int w = 0; w < 2; ++w) {
                     const int a = lw[w] & 0x33333333, b = (int)(((uint32_t)lw[w] >> 2) & 0x33333333u);
-                    lh = __builtin_amdgcn_sdot8(a, qh[j][2 * w], lh, false);
-                    lh = __builtin_amdgcn_sdot8(b, qh[j][2 * w + 1], lh, false);
-                    ll = __builtin_amdgcn_sdot8(a, ql[j][2 * w], ll, false);
-                    ll = __builtin_amdgcn_sdot8(b, ql[j][2 * w + 1], ll, false);
+                    lh[0] = __builtin_amdgcn_sdot8(a, qh[j][2 * w], lh[0], false);
+                    lh[1] = __builtin_amdgcn_sdot8(b, qh[j][2 * w + 1], lh[1], false);
+                    ll[0] = __builtin_amdgcn_sdot8(a, ql[j][2 * w], ll[0], false);
+                    ll[1] = __builtin_amdgcn_sdot8(b, ql[j][2 * w + 1], ll[1], false);
                 }
             }
-            int acc = 64 * hh + 4 * hl + 16 * lh + ll;
+            accu[u] = 64 * (hh[0] + hh[1]) + 4 * (hl[0] + hl[1]) + 16 * (lh[0] + lh[1]) + (ll[0] + ll[1]);
+        }
 #pragma unroll
-            for (int m = 1; m < 8; m <<= 1) acc += __shfl_xor(acc, m);
+        for (int m = 1; m < 8; m <<= 1)
+#pragma unroll
+            for (int u = 0; u < U; ++u) accu[u] += __shfl_xor(accu[u], m);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            nvis += __popcll(__ballot(t == 0 && valid[u]));
+            const float sx = sim == SIM_COSINE ? __builtin_amdgcn_sqrtf(ax[u].w) : 0.0f;   // (1 ulp ≪ the quick test's slack)
+            const int acc = accu[u];
             const float side6 = sq8_bound_side(sim, (float)acc, ax[u], qc6, p.gam, p.g2);
             const bool pass6 = valid[u] && sq8_pass(sim, side6, side6, tq0, sx);
             const uint64_t pm = __ballot(pass6 && t == 0);
@@ -493,21 +503,19 @@ static const Sq6Fn kSq6[5] = {sq6_scan<2, 4>, sq6_scan<3, 3>, sq6_scan<4, 2>, sq
 static const Sq6Fn kSq6Pilot[5] = {sq6_pilot<2>, sq6_pilot<3>, sq6_pilot<4>, sq6_pilot<5>, sq6_pilot<6>};
 static const Sq6Fn kSq6Rebound[5] = {sq6_rebound<2>, sq6_rebound<3>, sq6_rebound<4>, sq6_rebound<5>, sq6_rebound<6>};
 
-// pilot → streaming pass → int8 re-bound pass (the scan's events bracket all three)
+// pilot → streaming pass → int8 re-bound pass; the profiling events bracket the streaming pass, the
+// dominant kernel whose roofline bench.py reports (the pilot and the re-bound read ≈ 2-3 % of its bytes)
 hipError_t launch_sq6_scan(const Sq8Params& p, int dim, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
     const int C = sq6_chunks(dim);
     if (C < 2 || C > 6 || p.q_count != 1 || p.k < 1 || p.k > kKQ || !p.floor || !p.q6 || !p.cand6 || !p.cnt6 ||
         !p.tile_order || p.cap6 < 1)
         return hipErrorInvalidValue;
-    if (ev_start)
-        hipExtLaunchKernelGGL(kSq6Pilot[C - 2], dim3(p.n_tiles), dim3(kBlock), 0, s, ev_start, nullptr, 0, p);
+    hipLaunchKernelGGL(kSq6Pilot[C - 2], dim3(p.n_tiles), dim3(kBlock), 0, s, p);
+    if (ev_start || ev_stop)
+        hipExtLaunchKernelGGL(kSq6[C - 2], dim3(p.n_tiles), dim3(kBlock), 0, s, ev_start, ev_stop, 0, p);
     else
-        hipLaunchKernelGGL(kSq6Pilot[C - 2], dim3(p.n_tiles), dim3(kBlock), 0, s, p);
-    hipLaunchKernelGGL(kSq6[C - 2], dim3(p.n_tiles), dim3(kBlock), 0, s, p);
-    if (ev_stop)
-        hipExtLaunchKernelGGL(kSq6Rebound[C - 2], dim3(p.n_tiles), dim3(kBlock), 0, s, nullptr, ev_stop, 0, p);
-    else
-        hipLaunchKernelGGL(kSq6Rebound[C - 2], dim3(p.n_tiles), dim3(kBlock), 0, s, p);
+        hipLaunchKernelGGL(kSq6[C - 2], dim3(p.n_tiles), dim3(kBlock), 0, s, p);
+    hipLaunchKernelGGL(kSq6Rebound[C - 2], dim3(p.n_tiles), dim3(kBlock), 0, s, p);
     return hipGetLastError();
 }
 
