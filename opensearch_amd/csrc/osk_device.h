@@ -3,6 +3,7 @@
 // lane order, and global-address-space loads.
 #pragma once
 #include "osk_internal.h"
+#include "osk_wave.h"
 
 namespace osk {
 
@@ -134,8 +135,7 @@ __device__ __forceinline__ float settle_exact(const float4* xr, bool valid, int 
         }
     }
     float sum = (ax + ay) + (az + aw);
-#pragma unroll
-    for (int m = 1; m < L; m <<= 1) sum += __shfl_xor(sum, m);
+    sum = lane_sum<L>(sum);
     if constexpr (L2K) return score_f32_l2(sum);
     else return score_f32(sim, sum, qn, xn);
 }

@@ -83,8 +83,7 @@ __global__ __launch_bounds__(kBlock) void scan_f32(ScanParams p) {
                 az = fmaf(qv.z, qv.z, az); aw = fmaf(qv.w, qv.w, aw);
             }
             float s = (ax + ay) + (az + aw);
-#pragma unroll
-            for (int m = 1; m < L; m <<= 1) s += __shfl_xor(s, m);
+            s = lane_sum<L>(s);
             qn[b] = s;
         }
     }
@@ -135,8 +134,7 @@ __global__ __launch_bounds__(kBlock) void scan_f32(ScanParams p) {
                 }
             }
             float s = (ax + ay) + (az + aw);
-#pragma unroll
-            for (int m = 1; m < L; m <<= 1) s += __shfl_xor(s, m);
+            s = lane_sum<L>(s);
             float sc;
             if constexpr (L2K) sc = score_f32_l2(s);
             else sc = score_f32(sim, s, qn[b], xn);
@@ -204,8 +202,7 @@ __global__ __launch_bounds__(kBlock) void scan_i8(ScanParams p) {
             acc = dot4_i8(qv.x, qv.x, acc); acc = dot4_i8(qv.y, qv.y, acc);
             acc = dot4_i8(qv.z, qv.z, acc); acc = dot4_i8(qv.w, qv.w, acc);
         }
-#pragma unroll
-        for (int m = 1; m < L; m <<= 1) acc += __shfl_xor(acc, m);
+        acc = lane_sum<L>(acc);
         qn[b] = acc;
     }
 
@@ -248,8 +245,7 @@ __global__ __launch_bounds__(kBlock) void scan_i8(ScanParams p) {
                 acc = dot4_i8(xv[j].z, qv.z, acc);
                 acc = dot4_i8(xv[j].w, qv.w, acc);
             }
-#pragma unroll
-            for (int m = 1; m < L; m <<= 1) acc += __shfl_xor(acc, m);
+            acc = lane_sum<L>(acc);
             const int32_t s = sim == SIM_EUCLIDEAN ? qn[b] + xn - 2 * acc : acc;
             const float sc = score_i8(sim, s, qn[b], xn, dim);
             const uint64_t key = valid ? make_key(sc, (uint32_t)(seg.doc_base + doc)) : 0ull;
@@ -300,8 +296,7 @@ __global__ __launch_bounds__(kBlock) void scan_i8_stream(ScanParams p) {
         qn = dot4_i8(qf[j].x, qf[j].x, qn); qn = dot4_i8(qf[j].y, qf[j].y, qn);
         qn = dot4_i8(qf[j].z, qf[j].z, qn); qn = dot4_i8(qf[j].w, qf[j].w, qn);
     }
-#pragma unroll
-    for (int m = 1; m < L; m <<= 1) qn += __shfl_xor(qn, m);
+    qn = lane_sum<L>(qn);
     const int64_t rows = tile.row_end - tile.row_begin;
     const int64_t per_wave = ((rows + 4 * R - 1) / (4 * R)) * R;
     const int64_t wb = tile.row_begin + wave * per_wave;
@@ -337,8 +332,7 @@ __global__ __launch_bounds__(kBlock) void scan_i8_stream(ScanParams p) {
                 acc = dot4_i8(xv[u][j].x, qf[j].x, acc); acc = dot4_i8(xv[u][j].y, qf[j].y, acc);
                 acc = dot4_i8(xv[u][j].z, qf[j].z, acc); acc = dot4_i8(xv[u][j].w, qf[j].w, acc);
             }
-#pragma unroll
-            for (int m = 1; m < L; m <<= 1) acc += __shfl_xor(acc, m);
+            acc = lane_sum<L>(acc);
             nvis += __popcll(__ballot(t == 0 && valid[u]));
             const int32_t s = sim == SIM_EUCLIDEAN ? qn + xn[u] - 2 * acc : acc;
             const float sc = score_i8(sim, s, qn, xn[u], dim);
@@ -452,8 +446,7 @@ __global__ __launch_bounds__(kBlock) void row_norms_f32(const float4* __restrict
             az = fmaf(x.z, x.z, az); aw = fmaf(x.w, x.w, aw);
         }
         float s = (ax + ay) + (az + aw);
-#pragma unroll
-        for (int m = 1; m < L; m <<= 1) s += __shfl_xor(s, m);
+        s = lane_sum<L>(s);
         if (valid && t == 0) out[row] = s;
     }
 }

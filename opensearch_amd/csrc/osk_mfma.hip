@@ -15,6 +15,7 @@
 // is recomputed by the exact streaming scan.  Results are therefore bit-identical to the
 // streaming path (and to the ORDER_DEVICE oracle) — asserted by tests/test_gpu_parity.py.
 #include "osk_internal.h"
+#include "osk_wave.h"
 
 namespace osk {
 
@@ -590,8 +591,7 @@ __global__ __launch_bounds__(64) void rescore(RescoreParams p) {
             }
         }
         float sum = (ax + ay) + (az + aw);
-#pragma unroll
-        for (int m = 1; m < L; m <<= 1) sum += __shfl_xor(sum, m);
+        sum = lane_sum<L>(sum);
         float sc;
         if constexpr (L2K) sc = score_f32_l2(sum);
         else sc = score_f32(sim, sum, qn, (sim == SIM_COSINE && valid) ? seg.xnorm_f[ord] : 0.0f);

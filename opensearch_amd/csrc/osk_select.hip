@@ -113,8 +113,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_keys_i8(SelParams p) {
         qn = __builtin_amdgcn_sdot4(qf[j].z, qf[j].z, qn, false);
         qn = __builtin_amdgcn_sdot4(qf[j].w, qf[j].w, qn, false);
     }
-#pragma unroll
-    for (int m = 1; m < L; m <<= 1) qn += __shfl_xor(qn, m);
+    qn = lane_sum<L>(qn);
     const int4* __restrict__ X = static_cast<const int4*>(seg.rows);
     const int64_t vbase = p.seg_vrow[tile.seg];
     int64_t wb, we;
@@ -152,8 +151,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_keys_i8(SelParams p) {
                 acc = __builtin_amdgcn_sdot4(xv[u][j].z, qf[j].z, acc, false);
                 acc = __builtin_amdgcn_sdot4(xv[u][j].w, qf[j].w, acc, false);
             }
-#pragma unroll
-            for (int m = 1; m < L; m <<= 1) acc += __shfl_xor(acc, m);
+            acc = lane_sum<L>(acc);
             const int32_t x2 = valid[u] ? xn[u] : 0;
             const int32_t sv = p.sim == SIM_EUCLIDEAN ? qn + x2 - 2 * acc : acc;
             const float sc = score_i8(p.sim, sv, qn, x2, p.dim);
@@ -250,8 +248,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_bounds(SelParams p) {
                 acc = __builtin_amdgcn_sdot4(xv[u][j].z, qf[j].z, acc, false);
                 acc = __builtin_amdgcn_sdot4(xv[u][j].w, qf[j].w, acc, false);
             }
-#pragma unroll
-            for (int m = 1; m < L; m <<= 1) acc += __shfl_xor(acc, m);
+            acc = lane_sum<L>(acc);
             float lo, hi;
             sq8_bounds(sim, (float)acc, ax[u], qc, p.gam, p.g2, lo, hi);
             const float xnd = (sim == SIM_COSINE && valid[u]) ? seg.xnorm_f[row[u]] : 0.0f;

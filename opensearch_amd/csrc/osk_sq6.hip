@@ -225,8 +225,7 @@ __global__ __launch_bounds__(kBlock) void sq6_pilot(Sq8Params p) {
             a8 = __builtin_amdgcn_sdot4(xv[h][i].z, qv[i].z, a8, false);
             a8 = __builtin_amdgcn_sdot4(xv[h][i].w, qv[i].w, a8, false);
         }
-#pragma unroll
-        for (int m = 1; m < 16; m <<= 1) a8 += __shfl_xor(a8, m);
+        a8 = lane_sum<16>(a8);
         float lo, hi;
         sq8_bounds(sim, (float)a8, ax[h], qc, p.gam, p.g2, lo, hi);
         const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qnd, xnd[h]);
@@ -366,9 +365,7 @@ __global__ __launch_bounds__(kBlock, 4) void sq6_scan(Sq8Params p) {   // ≤ 12
             accu[u] = 64 * (hh[0] + hh[1]) + 4 * (hl[0] + hl[1]) + 16 * (lh[0] + lh[1]) + (ll[0] + ll[1]);
         }
 #pragma unroll
-        for (int m = 1; m < 8; m <<= 1)
-#pragma unroll
-            for (int u = 0; u < U; ++u) accu[u] += __shfl_xor(accu[u], m);
+        for (int u = 0; u < U; ++u) accu[u] = lane_sum<8>(accu[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             nvis += __popcll(__ballot(t == 0 && valid[u]));
@@ -467,8 +464,7 @@ __global__ __launch_bounds__(kBlock) void sq6_rebound(Sq8Params p) {
                     a8 = __builtin_amdgcn_sdot4(xv[h][i].z, qv.z, a8, false);
                     a8 = __builtin_amdgcn_sdot4(xv[h][i].w, qv.w, a8, false);
                 }
-#pragma unroll
-                for (int m = 1; m < 16; m <<= 1) a8 += __shfl_xor(a8, m);
+                a8 = lane_sum<16>(a8);
                 float lo, hi;
                 sq8_bounds(sim, (float)a8, ax[h], qc, p.gam, p.g2, lo, hi);
                 const float sx = sim == SIM_COSINE ? __builtin_amdgcn_sqrtf(ax[h].w) : 0.0f;

@@ -151,8 +151,7 @@ __global__ __launch_bounds__(kBlock) void sq8_prep(const float* __restrict__ src
             ax = fmaf(x0, x0, ax); ay = fmaf(x1, x1, ay); az = fmaf(x2, x2, az); aw = fmaf(x3, x3, aw);
         }
         float sn = (ax + ay) + (az + aw);
-#pragma unroll
-        for (int o = 1; o < L; o <<= 1) sn += __shfl_xor(sn, o);
+        sn = lane_sum<L>(sn);
         if (lane == 0) qnorm[r] = sn;
     }
     __syncthreads();
@@ -446,8 +445,7 @@ __global__ __launch_bounds__(kBlock, NQ == 1 && V <= 3 ? 4 : 1) void sq8_scan(Sq
                     acc = __builtin_amdgcn_sdot4(xv[u][j].z, qf[0][j].z, acc, false);
                     acc = __builtin_amdgcn_sdot4(xv[u][j].w, qf[0][j].w, acc, false);
                 }
-#pragma unroll
-                for (int m = 1; m < L; m <<= 1) acc += __shfl_xor(acc, m);
+                acc = lane_sum<L>(acc);
                 float lo, hi;
                 sq8_bounds(sim, (float)acc, ax[u], qc0, p.gam, p.g2, lo, hi);
                 const bool pass = valid[u] && sq8_pass(sim, lo, hi, tq0, sx);

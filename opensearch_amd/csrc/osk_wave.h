@@ -19,6 +19,37 @@ __device__ __forceinline__ uint64_t shfl_up1_64(uint64_t v) {
     return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 
+// Sum of v over each aligned group of L lanes (L a power of two ≤ 64), every lane of the group receiving
+// it.  The steps are the xor butterfly's (partners at distance 1, 2, 4, … in that order), so fp32 sums
+// have exactly its bits; distances 1 and 2 are DPP quad permutes and 4 and 8 DPP row mirrors (after the
+// first steps every lane of a quad / 8-lane half holds the same partial, so the mirrored partner's value
+// is the xor partner's), fused into the add: __shfl_xor compiles to ds_bpermute, an LDS round trip per
+// step on the scans' critical path.  16 and 32 stay shuffles.
+template <int CTRL>
+__device__ __forceinline__ int dpp_mov(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+template <int L>
+__device__ __forceinline__ int lane_sum(int v) {
+    if constexpr (L >= 2) v += dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]
+    if constexpr (L >= 4) v += dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]
+    if constexpr (L >= 8) v += dpp_mov<0x141>(v);   // row_half_mirror
+    if constexpr (L >= 16) v += dpp_mov<0x140>(v);  // row_mirror
+    if constexpr (L >= 32) v += __shfl_xor(v, 16);
+    if constexpr (L >= 64) v += __shfl_xor(v, 32);
+    return v;
+}
+template <int L>
+__device__ __forceinline__ float lane_sum(float v) {
+    if constexpr (L >= 2) v += __int_as_float(dpp_mov<0xB1>(__float_as_int(v)));
+    if constexpr (L >= 4) v += __int_as_float(dpp_mov<0x4E>(__float_as_int(v)));
+    if constexpr (L >= 8) v += __int_as_float(dpp_mov<0x141>(__float_as_int(v)));
+    if constexpr (L >= 16) v += __int_as_float(dpp_mov<0x140>(__float_as_int(v)));
+    if constexpr (L >= 32) v += __shfl_xor(v, 16);
+    if constexpr (L >= 64) v += __shfl_xor(v, 32);
+    return v;
+}
+
 // Insert key K (known to beat thr = lk[k-1]) into the wave's sorted-descending list held in
 // lanes 0..k-1 of lk.  Entries better than K form a prefix; K goes to lane `pos`, the tail
 // shifts down one lane and the old k-th entry falls off.
