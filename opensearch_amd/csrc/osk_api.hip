@@ -299,7 +299,7 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         {"sq8_mfma_ring", &g_tuning.sq8_mfma_ring, -1, 8, false},
         {"i8_stream", &g_tuning.i8_stream, 0, 1, false},
         {"call_timing", &g_tuning.call_timing, 0, 1, false},
-        {"sq8_mfma_ablate", &g_tuning.sq8_mfma_ablate, 0, 15, true},   // (also sq6_scan's: 1 no re-bound, 2 no floor)
+        {"sq8_mfma_ablate", &g_tuning.sq8_mfma_ablate, 0, 127, true},   // (also sq6_scan's: 1 no re-bound, 2 no floor, 16 loads only)
         {"sq8_force_fallback", &g_tuning.sq8_force_fallback, 0, 1, true},
         {"settle_trace", &g_tuning.settle_trace, 0, 1, true},
         {"mfma_ablate", &g_tuning.mfma_ablate, 0, 255, true},

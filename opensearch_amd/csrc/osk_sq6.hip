@@ -152,7 +152,7 @@ __device__ __forceinline__ int2 load_i2_nt(const int2* p) {
 // (ties by lane), read with v_readlane — no LDS round trips, unlike a shuffle sort.
 __device__ __forceinline__ uint32_t wave_kth_largest(uint32_t v, int lane, int k) {
     int rank = 0;
-#pragma unroll 16
+#pragma unroll 4   // (16 kept 16 compare masks live in SGPRs and spilled the callers' scalars)
     for (int j = 0; j < 64; ++j) {
         const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)v, j);
         rank += (o > v) || (o == v && j < lane);
@@ -254,7 +254,7 @@ __global__ __launch_bounds__(kBlock, 4) void sq6_scan(Sq8Params p) {   // ≤ 12
     const int sim = p.sim;
 #ifdef OSK_TESTING
     const int ablate = p.ablate;   // A/B timing only (results wrong): 1 no candidates, 2 no floor refresh, 4 no
-                                   // candidate stores, 8 no 6-bit lower bounds
+                                   // candidate stores, 8 no 6-bit lower bounds, 16 no dots (loads only)
 #else
     constexpr int ablate = 0;
 #endif
@@ -280,9 +280,8 @@ __global__ __launch_bounds__(kBlock, 4) void sq6_scan(Sq8Params p) {   // ≤ 12
     uint32_t* fb = p.floor + ((size_t)p.q0 * p.n_shards + tile.shard) * (kFloorBuckets + 1) * kFloorStride;
     uint32_t* cbuf = p.cand6 + (size_t)list * p.cap6;
     uint64_t fkey = 0ull;
-    uint32_t best = 0u, pub = 0u;
+    uint32_t best = 0u;
     float tq0 = sq8_quick(sim, 0ull, 0.0f, 0.0f);
-    uint32_t nvis = 0;
     int nc = 0, it = 0;
     uint32_t* cell = fb + kFloorBuckets * kFloorStride;   // the shard's floor: max of the k-th values computed
     auto set_floor = [&](uint32_t f32) {
@@ -304,45 +303,49 @@ __global__ __launch_bounds__(kBlock, 4) void sq6_scan(Sq8Params p) {   // ≤ 12
     // round's waves start together, and thousands of atomics on one address would queue for 100+ µs
     if (!(ablate & 2)) recompute((list & (kFloorBuckets - 1)) == 0);
     // then the cell is re-read every iteration for the first four, every fourth later (one load, issued
-    // a refresh ahead); a wave whose best lower bound can still lift the floor publishes it to its bucket
-    // and recomputes (same-address atomics queue at L2, and the wave's next load waits behind its own)
+    // a refresh ahead).  A wave publishes its best lower bound to its bucket once, at its end, for the
+    // later rounds of workgroups: publishing and re-ranking inside the loop (same-address atomics queue at
+    // L2, and the ranking's registers spilled the loop's scalars) left the re-bound count unchanged at C3
+    // and cost ≈ 10 % of the pass (profiles/r03c/sq6_ablate_r3.jsonl)
     uint32_t cv = __hip_atomic_load(cell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
     for (int64_t r0 = wb; r0 < we; r0 += R * U, ++it) {
         if ((it < 4 || (it & 3) == 0) && !(ablate & 2)) {
             set_floor(cv);
-            if (best > pub && best > (uint32_t)(fkey >> 32)) {
-                pub = best;
-                if (lane == 0) atomicMax(fb + (list & (kFloorBuckets - 1)) * kFloorStride, best);
-                recompute(true);
-            }
             cv = __hip_atomic_load(cell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         int4 hv[U][C];
         int2 lv[U][C];
-        float4 ax[U];
-        bool valid[U];
-        int64_t row[U];
         // unconditional loads from a clamped in-range block (masked after): see sq8_scan
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t gb = r0 + u * R;   // wave-uniform, 8-aligned
-            row[u] = gb + g;
-            valid[u] = row[u] < we;
             const char* blk = X6 + ((gb < we ? gb : wb) >> 3) * (int64_t)(1536 * C);
 #pragma unroll
             for (int j = 0; j < C; ++j) {
                 hv[u][j] = load_i4_nt(reinterpret_cast<const int4*>(blk + j * 1024) + lane);
                 lv[u][j] = load_i2_nt(reinterpret_cast<const int2*>(blk + C * 1024 + j * 512) + lane);
             }
-            ax[u] = AX6[valid[u] ? row[u] : wb];
         }
+        // the tests run once per iteration, lane (g, t < U) on group t's row g (the U groups' sums are
+        // gathered to those lanes below): one bound term load, one test and at most one candidate block
+        // per iteration instead of U — their latency sits between this wave's loads
+        const int64_t row = r0 + (int64_t)t * R + g;
+        const bool valid = t < U && row < we;
+        const float4 ax = AX6[valid ? row : wb];
         // every group's dot first, then the bounds and tests: the four v_dot8 chains of a group are serial
         // dependencies, and with the tests (ballot, branch) between groups the compiler could not overlap
         // one group's chains with the next one's (36 % of the wave cycles were issue stalls)
         int accu[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
+            if (ablate & 16) {   // loads only: the words folded, no dots
+                int x = 0;
+#pragma unroll
+                for (int j = 0; j < C; ++j) x ^= hv[u][j].x ^ hv[u][j].y ^ hv[u][j].z ^ hv[u][j].w ^ lv[u][j].x ^ lv[u][j].y;
+                accu[u] = x & 1;
+                continue;
+            }
             int hh[2] = {0, 0}, hl[2] = {0, 0}, lh[2] = {0, 0}, ll[2] = {0, 0};   // two chains each
 #pragma unroll
             for (int j = 0; j < C; ++j) {
@@ -366,35 +369,33 @@ __global__ __launch_bounds__(kBlock, 4) void sq6_scan(Sq8Params p) {   // ≤ 12
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) accu[u] = lane_sum<8>(accu[u]);
+        int acc = accu[0];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            nvis += __popcll(__ballot(t == 0 && valid[u]));
-            const float sx = sim == SIM_COSINE ? __builtin_amdgcn_sqrtf(ax[u].w) : 0.0f;   // (1 ulp ≪ the quick test's slack)
-            const int acc = accu[u];
-            const float side6 = sq8_bound_side(sim, (float)acc, ax[u], qc6, p.gam, p.g2);
-            const bool pass6 = valid[u] && sq8_pass(sim, side6, side6, tq0, sx);
-            const uint64_t pm = __ballot(pass6 && t == 0);
-            if (!pm || (ablate & 1)) continue;   // wave-uniform: rare once the floor has risen
-            // the passing rows (one lane per row) → the candidate buffer, and their 6-bit lower bounds
-            const int slot = nc + __popcll(pm & ((1ull << lane) - 1ull));
-            if (pass6 && t == 0) {
-                if (slot < p.cap6 && !(ablate & 4)) cbuf[slot] = (uint32_t)row[u];
-                if (!(ablate & 8)) {
-                    float lo, hi;
-                    sq8_bounds(sim, (float)acc, ax[u], qc6, p.gam, p.g2, lo, hi);
-                    best = max(best, float_to_sortable(floor_lb_score(sim, lo, hi, qnd0, ax[u].w, p.g2)));
-                }
+        for (int u = 1; u < U; ++u) acc = t == u ? accu[u] : acc;
+        const uint64_t vm = __ballot(valid);
+        if (!vm) continue;
+        const float sx = sim == SIM_COSINE ? __builtin_amdgcn_sqrtf(ax.w) : 0.0f;   // (1 ulp ≪ the quick test's slack)
+        const float side6 = sq8_bound_side(sim, (float)acc, ax, qc6, p.gam, p.g2);
+        const bool pass6 = valid && sq8_pass(sim, side6, side6, tq0, sx);
+        const uint64_t pm = __ballot(pass6);
+        if (!pm || (ablate & 1)) continue;   // wave-uniform: rare once the floor has risen
+        // the passing rows (one lane per row) → the candidate buffer, and their 6-bit lower bounds
+        const int slot = nc + __popcll(pm & ((1ull << lane) - 1ull));
+        if (pass6) {
+            if (slot < p.cap6 && !(ablate & 4)) cbuf[slot] = (uint32_t)row;
+            if (!(ablate & 8)) {
+                float lo, hi;
+                sq8_bounds(sim, (float)acc, ax, qc6, p.gam, p.g2, lo, hi);
+                best = max(best, float_to_sortable(floor_lb_score(sim, lo, hi, qnd0, ax.w, p.g2)));
             }
-            nc += __popcll(pm);
         }
+        nc += __popcll(pm);
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) best = max(best, (uint32_t)__shfl_xor((int)best, o));
     if (lane == 0) {
-        if (best > pub && best > (uint32_t)(fkey >> 32)) atomicMax(fb + (list & (kFloorBuckets - 1)) * kFloorStride, best);
-        p.cnt6[(size_t)p.q0 * p.n_lists + list] = nc;
-        if (p.visited && p.q0 == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
-        if (p.counters && nc) atomicAdd(&p.counters[3], (unsigned long long)nc);
+        if (best > (uint32_t)(fkey >> 32)) atomicMax(fb + (list & (kFloorBuckets - 1)) * kFloorStride, best);
+        p.cnt6[(size_t)p.q0 * p.n_lists + list] = nc;   // (visited rows and the re-bound counter: sq6_rebound)
     }
 }
 
@@ -491,6 +492,17 @@ __global__ __launch_bounds__(kBlock) void sq6_rebound(Sq8Params p) {
         p.cand_lb[l * kKQ + lane] = lp0;
     }
     if (lane == 0) p.list_lbmax[l] = m;
+    // the tile's visited rows (every row: the 6-bit pass is unfiltered) and its candidates, one atomic
+    // each per workgroup, here rather than at the end of every 6-bit wave (same-address atomics queue)
+    __shared__ int s_nc;
+    if (tid == 0) s_nc = 0;
+    __syncthreads();
+    if (lane == 0 && nc) atomicAdd(&s_nc, nc);
+    __syncthreads();
+    if (tid == 0) {
+        if (p.visited && p.q0 == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)(tile.row_end - tile.row_begin));
+        if (p.counters && s_nc) atomicAdd(&p.counters[3], (unsigned long long)s_nc);
+    }
 }
 
 // row groups per wave-iteration by C: ≈ 12–14 KiB of loads in flight per wave

@@ -209,7 +209,7 @@ def main():
         _lib.tune(key, int(val))
     only = set(a.only.split(","))
     torch.cuda.set_device(0)
-    st, wu = a.steps, 3
+    st, wu = a.steps, 6   # ≥ kSq6Probes + 1: the 6-bit tier's calibration calls (synchronous) stay out of the timing
 
     def qpool(n, dim, dist, enc=_lib.FLOAT32):
         return torch.from_numpy(synth_host(0, n, dim, 43, dist)).cuda()
@@ -232,8 +232,12 @@ def main():
         q = qpool(512, 768, _lib.DIST_NORMALISH_UNIT)
         if "C3" in only:
             for b in [int(x) for x in a.c3_batches.split(",")]:
+                c0, s0, b0 = counter(v, "sq8_calls"), counter(v, "sq6_calls"), counter(v, "sq6_rebound_rows")
                 ms, km = run(v, q, b, st, wu)
-                emit("C3", v, b, ms, km, 10_000_000 * 768 * 4)
+                n6 = counter(v, "sq6_calls") - s0
+                emit("C3", v, b, ms, km, 10_000_000 * 768 * 4,
+                     {"sq6_share_of_calls": n6 / max(1, counter(v, "sq8_calls") - c0),
+                      "rebound_rows_per_query": (counter(v, "sq6_rebound_rows") - b0) / n6 if n6 else None})
         if "C5f" in only:
             rng = np.random.default_rng(44)
             for sel in [float(x) for x in a.c5f_sel.split(",")]:
@@ -263,19 +267,25 @@ def main():
             n_out = int(n_out)
             v = TorchView(8, 1_250_000, 768, _lib.COSINE, lambda s: outlier_rows(1_250_000, 768, n_out, scale, 100 + s))
             q = outlier_rows(512, 768, n_out, scale, 99)
-            for sq8 in (1, 0):
+            for sq8, sq6 in ((1, 1), (1, 0), (0, 0)):   # 6-bit tier (if the view keeps it), int8 tier, fp32
                 _lib.tune("sq8", sq8)
+                _lib.tune("sq6", sq6)
                 r0, x0 = counter(v, "sq8_rescored_rows"), counter(v, "sq8_exact_tiles")
                 f0 = counter(v, "sq8_fallback_queries")
-                c0 = counter(v, "sq8_calls")
+                c0, s0, b0 = counter(v, "sq8_calls"), counter(v, "sq6_calls"), counter(v, "sq6_rebound_rows")
                 ms, km = run(v, q, 1, st, wu)
                 nc = max(1, counter(v, "sq8_calls") - c0)
+                n6 = counter(v, "sq6_calls") - s0
                 emit(f"C3o-{n_out}x{scale:g}", v, 1, ms, km, 10_000_000 * 768 * 4,
                      {"outlier_dims": n_out, "outlier_scale": scale, "prefilter": sq8,
+                      "tier": "6-bit" if n6 else "int8" if sq8 else "fp32",
+                      "sq6_share_of_calls": n6 / nc if sq8 else None,
+                      "rebound_rows_per_query": (counter(v, "sq6_rebound_rows") - b0) / max(1, n6) if n6 else None,
                       "rescored_rows_per_query": (counter(v, "sq8_rescored_rows") - r0) / nc,
                       "exact_lists_per_query": (counter(v, "sq8_exact_tiles") - x0) / nc,
                       "fallback_queries": counter(v, "sq8_fallback_queries") - f0})
             _lib.tune("sq8", 1)
+            _lib.tune("sq6", 1)
             v.close()
     if "C4" in only:
         v = View(8, 12_500_000, 96, _lib.DOT_PRODUCT, _lib.FLOAT32, _lib.DIST_NORMALISH_UNIT)

@@ -39,7 +39,7 @@ def counter(name):
 
 _lib.tune("sq6_probe_pct", 100)   # keep the tier whatever the calibration says (A/B)
 VARIANTS = [("int8", 0, 0), ("sq6", 1, 0), ("sq6_no_rebound", 1, 1), ("sq6_no_floor", 1, 2),
-            ("sq6_no_store", 1, 4), ("sq6_no_lb", 1, 8), ("sq6_no_store_no_lb", 1, 12), ("sq6", 1, 0), ("int8", 0, 0)]
+            ("sq6_no_store", 1, 4), ("sq6_no_lb", 1, 8), ("sq6_no_store_no_lb", 1, 12), ("sq6_loads_only", 1, 1 | 2 | 16), ("sq6_no_cand", 1, 1 | 2), ("sq6", 1, 0), ("int8", 0, 0)]
 only = os.environ.get("ONLY")   # e.g. ONLY=sq6 (rocprof runs)
 for name, six, ab in VARIANTS:
     if only and name not in only.split(","):
