@@ -90,6 +90,18 @@ __device__ __forceinline__ bool sq8_pass(int sim, float lo, float hi, float tq, 
     return !(hi < tq);
 }
 
+// A workgroup's visited rows, added with ONE global atomic per workgroup: per-wave atomics on a
+// segment's counter queue at L2 behind each other and hold the kernel's last waves (every thread of the
+// workgroup must call this: it has barriers).
+__device__ __forceinline__ void add_visited_wg(unsigned long long* visited, uint32_t nvis) {
+    __shared__ uint32_t s_vis;
+    if (threadIdx.x == 0) s_vis = 0u;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0 && nvis) atomicAdd(&s_vis, nvis);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_vis) atomicAdd(visited, (unsigned long long)s_vis);
+}
+
 // Global-address-space loads (global_load, not flat_load): a flat load also counts in lgkmcnt, so
 // the first LDS read after it would wait for every row load in flight, prefetched ones included.
 __device__ __forceinline__ int4 load_i4_g(const int4* p, bool nt) {

@@ -143,7 +143,7 @@ __global__ __launch_bounds__(kBlock) void scan_f32(ScanParams p) {
         }
     });
 
-    if (p.visited && p.q0 == 0 && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
+    if (p.visited && p.q0 == 0) add_visited_wg(&p.visited[tile.seg], (uint32_t)nvis);
 
 #pragma unroll
     for (int b = 0; b < NQ; ++b) slist[(b * 4 + wave) * 64 + lane] = lane < k ? lk[b] : 0ull;
@@ -253,7 +253,7 @@ __global__ __launch_bounds__(kBlock) void scan_i8(ScanParams p) {
         }
     });
 
-    if (p.visited && p.q0 == 0 && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
+    if (p.visited && p.q0 == 0) add_visited_wg(&p.visited[tile.seg], (uint32_t)nvis);
 
 #pragma unroll
     for (int b = 0; b < NQ; ++b) slist[(b * 4 + wave) * 64 + lane] = lane < k ? lk[b] : 0ull;
@@ -341,7 +341,7 @@ __global__ __launch_bounds__(kBlock) void scan_i8_stream(ScanParams p) {
             wave_offer(key, t == 0, lk, thr, lane, k);
         }
     }
-    if (p.visited && p.q0 == 0 && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
+    if (p.visited && p.q0 == 0) add_visited_wg(&p.visited[tile.seg], (uint32_t)nvis);
     slist[wave * 64 + lane] = lane < k ? lk : 0ull;
     __syncthreads();
     if (wave == 0) {

@@ -84,7 +84,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_keys_f32(SelParams p) {
         nvis += __popcll(__ballot(t == 0 && valid));
         if (in && t == 0) p.keys[vbase + row] = valid ? make_key(sc, (uint32_t)(seg.doc_base + doc)) : 0ull;
     }
-    if (p.visited && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
+    if (p.visited) add_visited_wg(&p.visited[tile.seg], (uint32_t)nvis);
 }
 
 // Byte vectors, exact keys: byte-unit lane configs (L lanes × V 16-B units ≥ the row's units, sq8_scan's),
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_keys_i8(SelParams p) {
         }
         if (lane < U * R && r0 + lane < we) p.keys[vbase + r0 + lane] = ko;
     }
-    if (p.visited && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
+    if (p.visited) add_visited_wg(&p.visited[tile.seg], (uint32_t)nvis);
 }
 
 // COSINE bounds without Java's double transform.  LB/UB only have to bracket the exact score: with
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(kSelThreads) void sel_bounds(SelParams p) {
             p.ub[vbase + r0 + j] = ubo;
         }
     }
-    if (p.visited && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
+    if (p.visited) add_visited_wg(&p.visited[tile.seg], (uint32_t)nvis);
 }
 
 // ---- radix select of the k-th largest LB (u32) / key (u64) per shard ---------------------------

@@ -569,8 +569,6 @@ __global__ __launch_bounds__(kBlock, NQ == 1 && V <= 3 ? 4 : 1) void sq8_scan(Sq
         for (int64_t r0 = wb; r0 < we; r0 += R * U) process(r0, false, 0, 0, 0);
     }
 
-    if (p.visited && p.q0 == 0 && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
-
     // one list per wave (its own row range of the tile): finer lists overflow the certificate less
     // often than one folded list per tile, and need no LDS fold.  With it, the list's best lower
     // bound (the settle's threshold is selected among these, one distinct row per list).
@@ -593,6 +591,7 @@ __global__ __launch_bounds__(kBlock, NQ == 1 && V <= 3 ? 4 : 1) void sq8_scan(Sq
             if (lane == 0) p.list_lbmax[l] = m;
         }
     }
+    if (p.visited && p.q0 == 0) add_visited_wg(&p.visited[tile.seg], (uint32_t)nvis);   // (after the lists)
 }
 
 // int8 lane configs by 16-byte units per row: {L, V} (the int32 sums are exact: any order)
@@ -1143,6 +1142,8 @@ __global__ __launch_bounds__(kBlock, QB == 1 || (NS && KS == 2) ? 4 : (NS ? 2 : 
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) nvis += __shfl_xor(nvis, o);
     }
+    // (per wave: a workgroup-level sum would add static LDS to a kernel whose dynamic LDS is sized to
+    // fit 4 workgroups per CU)
     if (p.visited && p.q0 == 0 && lane == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)nvis);
 
     for (int b = 0; b < NQ; ++b) {
