@@ -312,8 +312,8 @@ def main():
         for v in views:
             _lib.check(_lib.lib().osk_view_profile(v, enable))
 
-    # setup: each view's first single queries calibrate the 6-bit tier with synchronous counter reads
-    # (osk_view::sq6_probes); issue them here, with the other one-time builds, not inside the warmup
+    # setup: the first single queries calibrate the 6-bit tier per segment (asynchronous probes, folded by
+    # later calls; osk_seg::sq6_state); issue them here, with the other one-time builds, not inside the warmup
     for i in range(4 * F):
         step(n_pool - 1 - (i % n_pool), F)
     torch.cuda.synchronize()

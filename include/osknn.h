@@ -364,11 +364,18 @@ int32_t osk_comm_all_gather(osk_comm* comm, const void* d_send, void* d_recv, in
  * sequence number, batch, k, from/size, shards per rank, dim/encoding and a fingerprint of the query
  * bytes — and the shard indices of the rank's lists, which the device reduce compares across ranks.
  * Ranks whose calls differ get count = −1 (and total hits −1) for every query of that call, and the
- * communicator becomes poisoned: every later call returns OSK_ERR_INVALID (release and re-create it).
- * osk_comm_status reports it (OSK_ERR_INVALID + message) without synchronising: synchronise the call's
- * stream first.  info (optional, 4 values): [flag, rank 0's call number, first differing rank, its call
- * number].  (A rank that never issues its call leaves the others blocked inside RCCL, as the
- * coordinator would wait on a shard that never answers.) */
+ * communicator becomes poisoned (sticky): every later call still issues its collective — a refusal based
+ * on a flag the previous call's reduce writes asynchronously could differ between ranks and leave one
+ * rank inside the all-gather forever — but its reduce reports count −1, and the synchronous host entry
+ * returns OSK_ERR_INVALID (release and re-create the communicator).  The batch, k and shards per rank size
+ * the all-gather, and RCCL requires every rank to pass the same count: the host entry agrees on a
+ * fixed-size call header first and refuses on every rank together when they differ; the device entry
+ * cannot (it never waits on the host), so its callers must pass the same n_queries, k and
+ * shards_per_rank on every rank — its header check catches calls that differ in anything else (sequence,
+ * queries, from/size).  osk_comm_status reports the flag (OSK_ERR_INVALID + message) without
+ * synchronising: synchronise the call's stream first.  info (optional, 4 values): [flag, rank 0's call
+ * number, first differing rank, its call number].  (A rank that never issues its call leaves the others
+ * blocked inside RCCL, as the coordinator would wait on a shard that never answers.) */
 int32_t osk_comm_status(const osk_comm* comm, int64_t* info);
 /* Testing build only (libosknn_testing.so; the shipped library returns OSK_ERR_UNSUPPORTED): a
  * communicator of `world` processes that may share ONE device (RCCL refuses that), whose all-gather
@@ -377,6 +384,10 @@ int32_t osk_comm_status(const osk_comm* comm, int64_t* info);
  * one-GPU machine; a peer missing for 120 s is an error, not a hang. */
 int32_t osk_comm_init_loopback(int32_t device, int32_t rank, int32_t world, const uint8_t* id, int64_t slot_bytes,
                                osk_comm** out);
+/* Testing build only: osk_comm_init_all's communicator (one process, local device i = rank i of n) whose
+ * grouped all-gather is replaced by device copies, so devices may repeat — n local "devices" mapped to one
+ * GPU run the multi-device code of osk_shards_search_merge on a one-GPU machine. */
+int32_t osk_comm_init_all_loopback(const int32_t* devices, int32_t n, osk_comm** out);
 
 /* The whole multi-GPU query, host buffers, synchronous: every local view (views[i] on the
  * communicator's local device i) scans its shards, the per-shard top-k lists of every rank are

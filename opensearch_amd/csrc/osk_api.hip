@@ -15,6 +15,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <vector>
 
@@ -171,6 +172,10 @@ osk_view::~osk_view() {
     for (hipStream_t st : lease_streams)
         if (st) (void)hipStreamDestroy(st);
     if (xs_event) (void)hipEventDestroy(xs_event);
+    if (ev_probe) {   // a calibration read-back may still be landing in h_seg_rebound
+        if (probe_pending) (void)hipEventSynchronize(ev_probe);
+        (void)hipEventDestroy(ev_probe);
+    }
     for (hipEvent_t e : ev_call)
         if (e) (void)hipEventDestroy(e);
     for (int i = 0; i < kEvRing; ++i) {
@@ -1057,10 +1062,11 @@ int32_t ensure_sq8_seg(osk_seg* s, hipStream_t st) {
     }
     OSK_HIP(launch_sq8_quantize(static_cast<const float4*>(s->d_rows), s->n_rows, s->units, s->units, u8, q8, aux,
                                 0, st));
-    // the 6-bit tier of single queries, where the dim has one
+    // the 6-bit tier of single queries, where the dim has one and the tier is on (a node
+    // that sets tune sq6 = 0 before staging never holds the copy; calibration frees it per segment)
     void* q6 = nullptr;
     float4* aux6 = nullptr;
-    if (sq6_supported(s->dim)) {
+    if (sq6_supported(s->dim) && g_tuning.sq6.load(std::memory_order_relaxed)) {
         const int64_t b6 = sq6_bytes(s->n_rows, s->dim), ba = std::max<int64_t>(1, s->n_rows) * 16;
         e = hipMalloc(&q6, (size_t)(b6 - ba));
         if (e == hipSuccess) e = hipMalloc(&aux6, (size_t)ba);
@@ -1249,6 +1255,42 @@ int32_t ensure_sq8(osk_view* v, hipStream_t st) {
     return OSK_OK;
 }
 
+// The 6-bit tier's calibration, folded without waiting: when this view's last probe has
+// landed (its event completed), its per-segment int8 re-bound counts join the segments' calibration; a
+// segment with kSq6Probes probes keeps the tier, or turns it off (re-bounds above sq6_probe_pct % of the
+// rows probed) and frees its 6-bit copy.  The free is the only wait, once per segment: every launch that
+// may read the copy was issued under the shared side of g_sq6_free_mu, so the exclusive side plus a device
+// synchronisation retire them all, and no later call launches it (state off).
+std::shared_mutex g_sq6_free_mu;
+void fold_probe(osk_view* v) {
+    if (!v->probe_pending || hipEventQuery(v->ev_probe) != hipSuccess) return;
+    v->probe_pending = false;
+    const unsigned long long* rb = static_cast<const unsigned long long*>(v->h_seg_rebound.p);
+    std::vector<osk_seg*> off;
+    for (size_t i = 0; i < v->segs.size(); ++i) {
+        osk_seg* sg = v->segs[i];
+        std::lock_guard<std::mutex> lk(sg->mu);
+        if (sg->sq6_state.load() != 0) continue;
+        sg->sq6_probe_rows += sg->n_rows;
+        sg->sq6_probe_rebound += (int64_t)rb[i];
+        if (++sg->sq6_probes < kSq6Probes) continue;
+        const bool keep = (double)sg->sq6_probe_rebound * 100.0 <=
+                          (double)sg->sq6_probe_rows * (double)g_tuning.sq6_probe_pct;
+        sg->sq6_state.store(keep ? 1 : 2, std::memory_order_release);
+        if (!keep) off.push_back(sg);
+    }
+    if (off.empty()) return;
+    std::unique_lock<std::shared_mutex> ex(g_sq6_free_mu);
+    if (hipDeviceSynchronize() != hipSuccess) return;   // (keep the copies: a later release frees them)
+    for (osk_seg* sg : off) {
+        std::lock_guard<std::mutex> lk(sg->mu);
+        if (sg->d_q6) (void)hipFree(sg->d_q6);
+        if (sg->d_q6aux) (void)hipFree(sg->d_q6aux);
+        sg->d_q6 = nullptr;
+        sg->d_q6aux = nullptr;
+    }
+}
+
 // Certified int8 prefilter search (float32, k ≤ kKQ): int8 scan → settle per slice of tiles (exact
 // re-score of the rows the certificate cannot exclude; a tile whose list overflowed is re-scanned
 // exactly inside the settle) → per-shard merge.  Nothing waits on the host.
@@ -1263,13 +1305,29 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     // scan, ≤ 8 per launch.  Filtered VALU scans run over the compacted accepted ordinals.  A single
     // unfiltered query scans the 6-bit tier where the view has one.
     const bool use_mfma = g_tuning.sq8_mfma_min > 0 && nq >= g_tuning.sq8_mfma_min && sq8_mfma_supported(u8);
-    const bool use6 = nq == 1 && !d_accept && !use_mfma && v->sq6_ready && !v->sq6_off && g_tuning.sq6;
-    const bool probe6 = use6 && v->sq6_probes < kSq6Probes;
-    unsigned long long rb_before = 0;
-    if (probe6) {   // calibration: this call's int8 re-bounds, counted synchronously (first calls only)
-        OSK_HIP(hipStreamSynchronize(st));
-        OSK_HIP(hipMemcpy(&rb_before, v->d_counters.as<unsigned long long>() + 3, sizeof(rb_before),
-                          hipMemcpyDeviceToHost));
+    // the 6-bit tier: single unfiltered queries, every segment's calibration probing or on.  The shared
+    // lock keeps a segment's copy alive from this check to the launches (fold_probe frees it under the
+    // exclusive one after a device synchronisation)
+    fold_probe(v);
+    std::shared_lock<std::shared_mutex> tier_lock(g_sq6_free_mu, std::defer_lock);
+    bool use6 = nq == 1 && !d_accept && !use_mfma && v->sq6_ready && g_tuning.sq6;
+    bool probing = false;
+    if (use6) {
+        tier_lock.lock();
+        for (const osk_seg* sg : v->segs) {
+            const int st6 = sg->sq6_state.load(std::memory_order_acquire);
+            use6 = use6 && st6 != 2 && sg->d_q6;
+            probing |= st6 == 0;
+        }
+    }
+    // calibration: this call counts its int8 re-bounds per segment (one probe in flight per view)
+    const bool probe6 = use6 && probing && !v->probe_pending;
+    const int ns = (int)v->segs.size();
+    if (probe6) {
+        OSK_HIP(v->d_seg_rebound.reserve(sizeof(unsigned long long) * ns));
+        OSK_HIP(v->h_seg_rebound.reserve(sizeof(unsigned long long) * ns));
+        if (!v->ev_probe) OSK_HIP(hipEventCreateWithFlags(&v->ev_probe, hipEventDisableTiming));
+        OSK_HIP(hipMemsetAsync(v->d_seg_rebound.p, 0, sizeof(unsigned long long) * ns, st));
     }
     OSK_HIP(v->ws_q8.reserve((size_t)nq_pad * u8 * 16));
     OSK_HIP(v->ws_qc.reserve(sizeof(float4) * nq_pad));
@@ -1387,6 +1445,7 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             p.cand6 = v->ws_cand6.as<uint32_t>();
             p.cnt6 = v->ws_cnt6.as<int32_t>();
             p.cap6 = kSq6Cap;
+            p.seg_rebound = probe6 ? v->d_seg_rebound.as<unsigned long long>() : nullptr;
             OSK_HIP(launch_sq6_scan(p, v->dim, st, e0, e1));
         } else {
             OSK_HIP(launch_sq8_scan(p.q_count, p, st, e0, e1));
@@ -1433,18 +1492,11 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     OSK_HIP(launch_sq8_settle(v->cfg, nq, sp, st));
     v->sq8_calls += 1;
     v->sq6_calls += use6 ? 1 : 0;
-    if (probe6) {
-        unsigned long long rb_after = 0;
-        OSK_HIP(hipStreamSynchronize(st));
-        OSK_HIP(hipMemcpy(&rb_after, v->d_counters.as<unsigned long long>() + 3, sizeof(rb_after),
-                          hipMemcpyDeviceToHost));
-        int64_t rows = 0;
-        for (const osk_seg* sg : v->segs) rows += sg->n_rows;
-        v->sq6_probe_rows += rows;
-        v->sq6_probe_rebound += (int64_t)(rb_after - rb_before);
-        if (++v->sq6_probes == kSq6Probes &&
-            (double)v->sq6_probe_rebound * 100.0 > (double)v->sq6_probe_rows * (double)g_tuning.sq6_probe_pct)
-            v->sq6_off = true;
+    if (probe6) {   // read back asynchronously: a later call folds it (fold_probe), nothing waits here
+        OSK_HIP(hipMemcpyAsync(v->h_seg_rebound.p, v->d_seg_rebound.p, sizeof(unsigned long long) * ns,
+                               hipMemcpyDeviceToHost, st));
+        OSK_HIP(hipEventRecord(v->ev_probe, st));
+        v->probe_pending = true;
     }
     return OSK_OK;
 }

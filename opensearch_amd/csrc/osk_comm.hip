@@ -59,8 +59,9 @@ struct osk_comm {
     // [mismatch flag, rank 0's sequence number, first mismatching rank, its sequence number], written by
     // the reduce kernel (pinned host memory); a set flag makes the communicator refuse further calls
     osk::HostPinned h_err;
-    osk::HostPinned h_spr;               // the host entry's shards-per-rank agreement (agree_spr)
+    osk::HostPinned h_spr;               // the host entry's call agreement (agree_call)
     void* lb = nullptr;                  // testing build: loopback transport instead of RCCL
+    bool lb_local = false;               // testing build: init_all's local devices exchange by device copies
     void (*lb_free)(void*) = nullptr;
     ~osk_comm() {
         if (lb_free) lb_free(lb);
@@ -304,6 +305,27 @@ int32_t lb_allgather(Loopback* L, const void* d_send, void* d_recv, size_t bytes
     OSK_REQUIRE(same, "loopback all-gather: the ranks passed blocks of different sizes");
     return OSK_OK;
 }
+
+// Testing build: the grouped all-gather of one process's n local devices (osk_comm_init_all) as device
+// copies, so the multi-device code of the host entry runs with every local "device" mapped to one GPU
+// (RCCL refuses two ranks on one device).  Local device i = rank i; send r → slot r of every receive
+// buffer.  The host waits for every send (its exchange stream drained) before copying: the transport
+// stands in for the collective, its latency is not the product's.
+int32_t local_allgather(osk_comm* c, const void* const* sends, void* const* recvs, size_t bytes) {
+    const size_t n = c->devices.size();
+    OSK_REQUIRE(n == (size_t)c->world, "local all-gather: one rank per local device");
+    for (size_t i = 0; i < n; ++i) {
+        OSK_HIP(hipSetDevice(c->devices[i]));
+        OSK_HIP(hipStreamSynchronize(c->xstreams[i]));
+    }
+    for (size_t i = 0; i < n; ++i) {
+        OSK_HIP(hipSetDevice(c->devices[i]));
+        for (size_t r = 0; r < n; ++r)
+            OSK_HIP(hipMemcpyAsync(static_cast<char*>(recvs[i]) + r * bytes, sends[r], bytes, hipMemcpyDefault,
+                                   c->xstreams[i]));
+    }
+    return OSK_OK;
+}
 #endif
 
 // One all-gather of every local view's block (ws_xkeys, `words` u64) into its ws_xgath, on the
@@ -316,6 +338,15 @@ int32_t gather_blocks(osk_comm* c, osk_view* const* views, size_t words, const h
 #ifdef OSK_TESTING
     if (c->lb) return lb_allgather(static_cast<Loopback*>(c->lb), views[0]->ws_xkeys.p, views[0]->ws_xgath.p,
                                    words * 8, sts[0]);
+    if (c->lb_local) {
+        std::vector<const void*> sends(c->devices.size());
+        std::vector<void*> recvs(c->devices.size());
+        for (size_t i = 0; i < c->devices.size(); ++i) {
+            sends[i] = views[i]->ws_xkeys.p;
+            recvs[i] = views[i]->ws_xgath.p;
+        }
+        return local_allgather(c, sends.data(), recvs.data(), words * 8);
+    }
 #endif
     OSK_NCCL(g_rccl.GroupStart());
     for (size_t i = 0; i < c->devices.size(); ++i)
@@ -347,42 +378,80 @@ XLayout image_layout(const osk_comm* c, const uint64_t* image, const Block& B, c
     return x;
 }
 
-// The largest shard count over every view of every rank (host entry).  Each local device sends its
-// view's count through the exchange stream; the host waits for the tiny gather (the scans already run).
-int32_t agree_spr(osk_comm* c, osk_view* const* views, int* spr) {
+// The host entry's call agreement, before any variable-size collective: every rank gathers a fixed-size
+// call header (sequence number, batch, k, from/size, dim/encoding, world; and its view's shard count) on
+// the exchange streams and the host compares them (the scans already run).  RCCL requires every rank to
+// pass the same count to ncclAllGather, and the block size depends on the batch, k and the shards per
+// rank, so a rank that issued another call must be caught HERE — a block gather with different counts is
+// undefined behaviour (a hang or garbage), never a header mismatch.  Every rank sees the same gathered
+// headers, so every rank refuses together (and poisons its communicator) or proceeds together.  Shards
+// per rank = the largest view of any rank (ranks may hold different numbers of shards: 8 over 3 GPUs),
+// agreed on every call rather than cached (a cache would let ranks disagree on whether to exchange).
+constexpr int kCallWords = 8;
+int32_t agree_call(osk_comm* c, osk_view* const* views, int nq, int k, int from, int size, int* spr) {
     const size_t nl = c->devices.size(), W = (size_t)c->world;
-    OSK_HIP(c->h_spr.reserve(sizeof(int64_t) * nl * (W + 1)));
-    int64_t* h = static_cast<int64_t*>(c->h_spr.p);   // [nl] send values, then [nl][W] received
+    OSK_HIP(c->h_spr.reserve(sizeof(int64_t) * kCallWords * (nl + W)));
+    int64_t* h = static_cast<int64_t*>(c->h_spr.p);   // [nl][kCallWords] send values, then [W][kCallWords] received
     for (size_t i = 0; i < nl; ++i) {
         osk_view* v = views[i];
+        int64_t* w = h + i * kCallWords;
+        w[0] = (int64_t)kXMagic;
+        w[1] = (int64_t)(c->seq + 1);
+        w[2] = (int64_t)((uint32_t)nq | ((uint64_t)(uint32_t)k << 32));
+        w[3] = (int64_t)((uint32_t)from | ((uint64_t)(uint32_t)size << 32));
+        w[4] = (int64_t)(v->dim | v->enc << 16);
+        w[5] = c->world;
+        w[6] = v->n_shards;
+        w[7] = 0;
         OSK_HIP(hipSetDevice(v->device));
-        OSK_HIP(v->ws_xspr.reserve(sizeof(int64_t) * (W + 1)));
-        h[i] = v->n_shards;
-        OSK_HIP(hipMemcpyAsync(v->ws_xspr.as<int64_t>() + W, h + i, 8, hipMemcpyHostToDevice, c->xstreams[i]));
+        OSK_HIP(v->ws_xspr.reserve(sizeof(int64_t) * kCallWords * (W + 1)));
+        OSK_HIP(hipMemcpyAsync(v->ws_xspr.as<int64_t>() + W * kCallWords, w, 8 * kCallWords, hipMemcpyHostToDevice,
+                               c->xstreams[i]));
     }
 #ifdef OSK_TESTING
     if (c->lb) {
-        int32_t rc = lb_allgather(static_cast<Loopback*>(c->lb), views[0]->ws_xspr.as<int64_t>() + W,
-                                  views[0]->ws_xspr.p, 8, c->xstreams[0]);
+        int32_t rc = lb_allgather(static_cast<Loopback*>(c->lb), views[0]->ws_xspr.as<int64_t>() + W * kCallWords,
+                                  views[0]->ws_xspr.p, 8 * kCallWords, c->xstreams[0]);
+        if (rc) return rc;
+    } else if (c->lb_local) {
+        std::vector<const void*> sends(nl);
+        std::vector<void*> recvs(nl);
+        for (size_t i = 0; i < nl; ++i) {
+            sends[i] = views[i]->ws_xspr.as<int64_t>() + W * kCallWords;
+            recvs[i] = views[i]->ws_xspr.p;
+        }
+        int32_t rc = local_allgather(c, sends.data(), recvs.data(), 8 * kCallWords);
         if (rc) return rc;
     } else
 #endif
     {
         OSK_NCCL(g_rccl.GroupStart());
         for (size_t i = 0; i < nl; ++i)
-            OSK_NCCL(g_rccl.AllGather(views[i]->ws_xspr.as<int64_t>() + W, views[i]->ws_xspr.p, 1, ncclInt64,
-                                      c->comms[i], c->xstreams[i]));
+            OSK_NCCL(g_rccl.AllGather(views[i]->ws_xspr.as<int64_t>() + W * kCallWords, views[i]->ws_xspr.p,
+                                      kCallWords, ncclInt64, c->comms[i], c->xstreams[i]));
         OSK_NCCL(g_rccl.GroupEnd());
     }
-    int64_t* recv = h + nl;
+    int64_t* recv = h + nl * kCallWords;
     OSK_HIP(hipSetDevice(views[0]->device));
-    OSK_HIP(hipMemcpyAsync(recv, views[0]->ws_xspr.p, 8 * W, hipMemcpyDeviceToHost, c->xstreams[0]));
+    OSK_HIP(hipMemcpyAsync(recv, views[0]->ws_xspr.p, 8 * kCallWords * W, hipMemcpyDeviceToHost, c->xstreams[0]));
     for (size_t i = 0; i < nl; ++i) {
         OSK_HIP(hipSetDevice(views[i]->device));
         OSK_HIP(hipStreamSynchronize(c->xstreams[i]));
     }
     int m = 1;
-    for (size_t r = 0; r < W; ++r) m = std::max<int>(m, (int)recv[r]);
+    for (size_t r = 0; r < W; ++r) {
+        const int64_t* w = recv + r * kCallWords;
+        for (int j = 0; j < 6; ++j)
+            if (w[j] != recv[j]) {   // another call on rank r: refuse on every rank, before the block gather
+                int64_t* e = static_cast<int64_t*>(c->h_err.p);
+                e[1] = recv[1];
+                e[2] = (int64_t)r;
+                e[3] = w[1];
+                e[0] = 1;
+                return poisoned(c);
+            }
+        m = std::max<int>(m, (int)w[6]);
+    }
     *spr = m;
     return OSK_OK;
 }
@@ -590,6 +659,34 @@ int32_t osk_comm_init_loopback(int32_t device, int32_t rank, int32_t world, cons
     OSK_GUARD_END
 }
 
+int32_t osk_comm_init_all_loopback(const int32_t* devices, int32_t n, osk_comm** out) {
+    OSK_GUARD_BEGIN
+    clear_error();
+#ifndef OSK_TESTING
+    (void)devices; (void)n; (void)out;
+    set_error("osk_comm_init_all_loopback exists only in the testing build (libosknn_testing.so)");
+    return OSK_ERR_UNSUPPORTED;
+#else
+    OSK_REQUIRE(out != nullptr && devices != nullptr && n >= 1 && n <= 64, "null argument or n outside [1, 64]");
+    for (int i = 0; i < n; ++i) {
+        int32_t rc = check_device(devices[i]);
+        if (rc) return rc;
+    }
+    auto c = std::make_unique<osk_comm>();
+    c->id = ++g_comm_ids;
+    c->rank = 0;
+    c->world = n;
+    c->devices.assign(devices, devices + n);   // (may repeat: local "devices" mapped to one GPU)
+    c->comms.assign(n, nullptr);
+    int32_t rc = make_xstreams(c.get());
+    if (rc) return rc;
+    c->lb_local = true;
+    *out = c.release();
+    return OSK_OK;
+#endif
+    OSK_GUARD_END
+}
+
 int32_t osk_shards_search_merge_device(osk_comm* comm, osk_view* view, const void* d_queries, int32_t n_queries,
                                        int32_t k, const uint64_t* const* d_accept, int32_t shards_per_rank,
                                        int32_t from, int32_t size, float* d_scores, int32_t* d_docs,
@@ -607,9 +704,11 @@ int32_t osk_shards_search_merge_device(osk_comm* comm, osk_view* view, const voi
     rc = check_device(view->device);
     if (rc) return rc;
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : device_stream(view->device);
+    // No refusal on the poison flag here: the previous call's reduce writes it asynchronously, so a rank
+    // whose reduce had finished would refuse while a rank whose reduce had not would enter the all-gather
+    // and wait forever.  Every call issues its collective; a poisoned communicator's reduce reports
+    // count −1 on the device instead (xchg_header_check reads the sticky flag), and osk_comm_status says why.
     std::lock_guard<std::mutex> lc(comm->mu);
-    rc = poisoned(comm);
-    if (rc) return rc;
     std::lock_guard<std::mutex> lv(view->mu);
     rc = order_after_last(view, st);
     if (rc) return rc;
@@ -658,9 +757,8 @@ int32_t osk_shards_search_merge(osk_comm* comm, osk_view* const* views, int32_t 
     }
     int32_t rc = check_merge_args(comm, n_queries, k, from, size, spr);
     if (rc) return rc;
+    // (no refusal on the poison flag before the collectives: see osk_shards_search_merge_device)
     std::lock_guard<std::mutex> lc(comm->mu);
-    rc = poisoned(comm);
-    if (rc) return rc;
     std::vector<std::unique_lock<std::mutex>> locks;
     std::vector<hipStream_t> sts(n_views);
     const int64_t elem = views[0]->enc == ENC_FLOAT32 ? 4 : 1;
@@ -709,12 +807,17 @@ int32_t osk_shards_search_merge(osk_comm* comm, osk_view* const* views, int32_t 
                                 v->ws_counts.as<int32_t>(), nullptr, sts[i]);
         if (rc) return rc;
     }
-    // Shards per rank = the largest view of any rank.  Ranks may hold different numbers of shards (8 shards
-    // over 3 GPUs), so it is agreed on every call — a small all-gather on the exchange streams while the
-    // scans run — rather than cached (a cache would let ranks disagree on whether to exchange).
+    // the call agreement (fixed-size headers, shards per rank) while the scans run: a rank that issued
+    // another call is caught before the variable-size block gather (agree_call)
     if (comm->world > 1) {
-        rc = agree_spr(comm, views, &spr);
-        if (rc) return rc;
+        rc = agree_call(comm, views, n_queries, k, from, size, &spr);
+        if (rc) {
+            for (int i = 0; i < n_views; ++i) {   // the scans already issued write the views' workspaces
+                (void)hipSetDevice(views[i]->device);
+                (void)hipStreamSynchronize(sts[i]);
+            }
+            return rc;
+        }
     }
     const Block B = block_of(n_queries, k, spr);
     uint64_t hw[kXHdrWords];

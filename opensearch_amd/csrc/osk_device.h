@@ -123,6 +123,22 @@ __device__ __forceinline__ int4 load_i4_nt(const int4* p) {
     return make_int4(v.x, v.y, v.z, v.w);
 }
 
+// LDS-DMA (global_load_lds_dwordx4) from a per-lane source into a wave-uniform LDS base (+ lane·16 B).
+// Written as asm so the compiler keeps no bookkeeping for it (its own LDS-DMA tracking puts vmcnt(0)
+// before every LDS read of the buffer): completion is counted by hand (vm_wait), and only the issuing
+// wave reads what it loaded.  M0 is saved and restored inside the statement (compiler-reserved).
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_byte) {
+    lds_byte = __builtin_amdgcn_readfirstlane(lds_byte);   // wave-uniform by construction; make it an SGPR
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_byte)
+                 : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 // (kept in the scan's lane layout: L lanes per row, V float4 per lane, 4 fma chains, pairwise tree)
 // exact score of one row (the streaming scan's arithmetic: same lane layout and fma order)
 template <int L, int V, bool L2K>
@@ -155,7 +171,10 @@ __device__ __forceinline__ float settle_exact(const float4* xr, bool valid, int 
 // The exchange header check of the coordinator reduce (one wave, lane = 0..63): 1 when some rank's
 // header words differ from rank 0's — the ranks did not issue the same call (osk_comm.hip).  The first
 // mismatch is recorded in x.err: [1, rank 0's call sequence number, the rank, its sequence number].
+// The flag is sticky: once an earlier call of the communicator has set it, every later reduce reports a
+// mismatch too (count −1), without the host refusing the call before its collective (osk_comm.hip).
 __device__ __forceinline__ int xchg_header_check(const XLayout& x, int n_ranks, size_t rank_words, int lane) {
+    if (x.err && __hip_atomic_load(&x.err[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return 1;
     const int pairs = (n_ranks - 1) * kXHdrWords;
     int bad_pair = 0x7FFFFFFF;
     for (int e = lane; e < pairs; e += 64) {

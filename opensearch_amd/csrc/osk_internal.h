@@ -174,10 +174,12 @@ struct Sq8Params {
     const float4* qc6;
     uint32_t* floor;
     unsigned long long* counters;    // sq6_scan adds its int8 re-bounds to [3] (SettleParams::counters)
+    unsigned long long* seg_rebound; // calibration probes: the int8 re-bounds per segment [n_segs], or null
     const int32_t* tile_order;       // sq6_scan: the tile of each workgroup (tiles interleaved over shards)
     uint32_t* cand6;                 // sq6_scan → sq6_rebound: per list, the rows that passed the 6-bit test
     int32_t* cnt6;                   // [q][n_lists] their count (> cap6: overflowed)
     int cap6;
+    const float4* const* bmax;       // sq8_wide: per segment, the 16-row block maxima (launch_sq8_block_max)
 };
 
 struct SettleParams {
@@ -329,6 +331,19 @@ int sq8_ring_slots(int units8, int qb, int want);   // sq8_mfma LDS-DMA ring dep
 hipError_t launch_sq8_tile(const void* q8, int64_t n_rows, int units8, int ks, void* out, hipStream_t s);
 hipError_t launch_sq8_mfma(const Sq8Params& p, hipStream_t s, hipEvent_t ev_start = nullptr,
                            hipEvent_t ev_stop = nullptr);
+// int8 MFMA prefilter for large batches (osk_sq8w.hip): kWideQ queries per launch, 64 per wave, rows
+// ≤ 256 int8 dims, unfiltered.  One workgroup per (tile, quarter) — the settle's list of a scan wave with
+// scan_R = kMfmaScanR — whose 4 waves share the quarter's rows, staged once through an LDS-DMA ring, and
+// each own 64 of the queries (lists per (quarter, query) in LDS).  pilot = 1: each workgroup bounds only
+// its quarter's first 16 rows and writes, per query, the best lower-bound key of them to
+// pilot_keys [q][4·n_tiles].
+constexpr int kWideQB = 4;                      // 16-query MFMA blocks per wave
+constexpr int kWideQ = 4 * 16 * kWideQB;        // queries per launch
+int sq8_wide_supported(int units8);
+hipError_t launch_sq8_wide(const Sq8Params& p, hipStream_t s, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
+// per 16-row block of a segment's int8 copy: {max s·|q|, max |δ|, max |x|², min |x|²} of its rows (zeros past
+// the last row), the wide kernel's per-step quick-test terms
+hipError_t launch_sq8_block_max(const float4* aux, int64_t n_rows, float4* out, hipStream_t s);
 // The 6-bit tier's share of the query prep (C = 0: none): the nibble-split query [nq_pad][64·C dwords],
 // its bound terms, and the floor buckets [nq_pad][floor_n] zeroed
 struct Sq6Prep {
@@ -347,7 +362,7 @@ int64_t sq6_bytes(int64_t n_rows, int dim);   // the tiled codes + bound terms o
 constexpr int kSq6ScanR = 8;             // rows per wave-iteration of sq6_scan (the settle's scan_R)
 constexpr int kFloorBuckets = 64;       // sq6_scan's floor: the k-th best of 64 bucket maxima of lists' best lbs,
 constexpr int kFloorStride = 16;        // one 64-B line per bucket (uint32 units)
-constexpr int kSq6Probes = 4;            // calibration calls of the 6-bit tier per view (osk_view::sq6_probes)
+constexpr int kSq6Probes = 4;            // calibration probes of the 6-bit tier per segment (osk_seg::sq6_state)
 constexpr int kSq6Cap = 256;             // candidate rows per list between the 6-bit pass and the int8 re-bound
 hipError_t launch_sq6_quantize(const float4* x, int64_t n, int units, int dim, void* out, float4* aux, hipStream_t s);
 hipError_t launch_sq6_scan(const Sq8Params& p, int dim, hipStream_t s, hipEvent_t ev_start = nullptr,
@@ -378,7 +393,7 @@ struct Tuning {
     std::atomic<int> mfma_units{0};       // workgroup units of the MFMA candidate pass per view (0: auto)
     std::atomic<int> sq8{1};              // certified int8 prefilter for float32 batches below mfma_min_batch
     std::atomic<int> sq6{1};              // ...whose single unfiltered queries scan the 6-bit tier where the dim has one,
-    std::atomic<int> sq6_probe_pct{10};   // ...unless its first calls on a view re-bound more than this % of the rows
+    std::atomic<int> sq6_probe_pct{10};   // ...unless its first probes re-bound more than this % of a segment's rows
     std::atomic<int> gather_min{0};       // ...at most one gather tile per this many accepted rows (0 = every gather
                                           // tile; fewer, longer tiles were slower: profiles/r02c/gather_min_ab.jsonl)
     std::atomic<int> sel_writer{2};       // select path bounds writer: 0 U4 + Java transform, 1 U4 fast COSINE
@@ -395,6 +410,7 @@ struct Tuning {
     std::atomic<int> sq8_mfma_queries{32};    // queries per sq8_mfma launch: 16 or 32 (two MFMA chains per row operand)
     std::atomic<int> sq8_mfma_ablate{0};  // TESTING. A/B timing only: 1 skip sq8_mfma's epilogue, 2 its MFMAs (results wrong)
     std::atomic<int> sq8_mfma_min{2};     // prefilter batches ≥ this scan on int8 MFMA, 16 queries per launch (0 = never)
+    std::atomic<int> sq8_wide_min{48};    // ...and unfiltered batches ≥ this on the wide kernel, kWideQ per launch (0 = never)
     std::atomic<int> sq8_force_fallback{0};   // TESTING. tests: every list of a prefiltered search is re-scanned exactly
     std::atomic<int> settle_trace{0};     // TESTING. A/B only: record settle phase timestamps (debug copy "settle_trace")
     std::atomic<int> mfma_ablate{0};      // TESTING. A/B only: 1 skip the epilogue, 2 skip query staging, 4 skip corpus staging,
@@ -418,7 +434,7 @@ hipError_t launch_pad_rows(const void* src, int64_t src_pitch, void* dst, int64_
                            int64_t n_rows, int64_t row_bytes, hipStream_t s);
 hipError_t launch_merge_shards(const uint64_t* cand, int n_tiles, const int32_t* shard_tile_begin,
                                int n_shards, int nq, int k, uint64_t* shard_keys,
-                               int32_t* shard_counts, hipStream_t s);
+                               int32_t* shard_counts, hipStream_t s, int kin = 0);   // kin: keys per tile (0 = k)
 hipError_t launch_merge_coord(const uint64_t* shard_keys, const int32_t* shard_counts,
                               const int32_t* shard_index, int nq, int n_ranks, int sl, int k, int from,
                               int size, float* scores, int32_t* docs, int32_t* shard_out,

@@ -602,17 +602,18 @@ hipError_t launch_pad_rows(const void* src, int64_t src_pitch, void* dst, int64_
 // ------------------------------------------------------------------------------------------------
 // per-shard top-k from per-tile lists: one workgroup per (shard, query)
 // ------------------------------------------------------------------------------------------------
+// (kin: keys per tile in cand — k for tile lists, 1 for one key per tile; the output holds k per shard)
 __global__ __launch_bounds__(kBlock) void merge_shards(const uint64_t* __restrict__ cand, int n_tiles,
                                                        const int32_t* __restrict__ shard_tile_begin,
-                                                       int n_shards, int k,
+                                                       int n_shards, int k, int kin,
                                                        uint64_t* __restrict__ shard_keys,
                                                        int32_t* __restrict__ shard_counts) {
     __shared__ uint64_t lists[4 * 64];
     const int s = blockIdx.x, b = blockIdx.y;
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int t0 = shard_tile_begin[s], t1 = shard_tile_begin[s + 1];
-    const uint64_t* c = cand + ((size_t)b * n_tiles + t0) * k;
-    const int64_t n = (int64_t)(t1 - t0) * k;
+    const uint64_t* c = cand + ((size_t)b * n_tiles + t0) * kin;
+    const int64_t n = (int64_t)(t1 - t0) * kin;
     uint64_t lk = 0ull, thr = 0ull;
     for (int64_t base = (int64_t)wave * 64; base < n; base += kBlock) {
         const int64_t i = base + lane;
@@ -632,9 +633,9 @@ __global__ __launch_bounds__(kBlock) void merge_shards(const uint64_t* __restric
 
 hipError_t launch_merge_shards(const uint64_t* cand, int n_tiles, const int32_t* shard_tile_begin,
                                int n_shards, int nq, int k, uint64_t* shard_keys,
-                               int32_t* shard_counts, hipStream_t s) {
+                               int32_t* shard_counts, hipStream_t s, int kin) {
     hipLaunchKernelGGL(merge_shards, dim3(n_shards, nq), dim3(kBlock), 0, s, cand, n_tiles,
-                       shard_tile_begin, n_shards, k, shard_keys, shard_counts);
+                       shard_tile_begin, n_shards, k, kin > 0 ? kin : k, shard_keys, shard_counts);
     return hipGetLastError();
 }
 
@@ -819,34 +820,38 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {   // splitmix64 finalise
     return z ^ (z >> 31);
 }
 
-// One workgroup.  The fingerprint is Σ mix64(word_i + i·φ) over the query's 32-bit words (a strided
-// sample of at most 16384 of them for large batches, plus the tail bytes and the byte count):
-// order-independent across threads, so identical bytes give identical fingerprints on every rank.
+// The fingerprint is Σ mix64(word_i + i·φ) over EVERY 32-bit word of the query bytes (plus the tail bytes
+// and the byte count): order-independent, so identical bytes give identical fingerprints on every rank,
+// and a batch that differs in any word — its last query only, say — almost surely does not.  (A strided
+// sample of 16384 words left up to half of a 22–42-query batch at 768 dims unhashed.)  kXhdrWords per
+// workgroup; each adds its partial sum into w[5] (zeroed first by launch_xhdr_fill) with one atomic;
+// workgroup 0 writes the other header words and the shard indices.
+constexpr int64_t kXhdrWords = 16384;
 __global__ __launch_bounds__(256) void xhdr_fill(uint64_t* __restrict__ hdr, XHdrWords w,
                                                  const uint8_t* __restrict__ q, int64_t qbytes,
                                                  const int32_t* __restrict__ shard_index, int n_shards, int sl) {
     __shared__ uint64_t s_part[4];
     const int tid = threadIdx.x;
     const int64_t n32 = qbytes >> 2;
-    const int64_t n_sample = n32 < 16384 ? n32 : 16384;
-    const int64_t stride = n_sample ? n32 / n_sample : 1;
+    const int64_t e0 = (int64_t)blockIdx.x * kXhdrWords, e1 = min(n32, e0 + kXhdrWords);
     uint64_t h = 0;
-    for (int64_t i = tid; i < n_sample; i += 256) {
-        const int64_t e = i * stride;
+    for (int64_t e = e0 + tid; e < e1; e += 256) {
         uint32_t v;
         __builtin_memcpy(&v, q + e * 4, 4);
         h += mix64((uint64_t)v + (uint64_t)e * 0x9E3779B97F4A7C15ull);
     }
-    if (tid < (int)(qbytes & 3)) h += mix64((uint64_t)q[n32 * 4 + tid] + 0xA5A5ull * (uint64_t)(tid + 1));
+    if (blockIdx.x == 0) {
+        if (tid < (int)(qbytes & 3)) h += mix64((uint64_t)q[n32 * 4 + tid] + 0xA5A5ull * (uint64_t)(tid + 1));
+        if (tid == 0) h += mix64((uint64_t)qbytes);
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o);
     if ((tid & 63) == 0) s_part[tid >> 6] = h;
     __syncthreads();
-    if (tid < kXHdrWords) {
-        uint64_t v = w.w[tid];
-        if (tid == 5) v = mix64(s_part[0] + s_part[1] + s_part[2] + s_part[3] + (uint64_t)qbytes);
-        hdr[tid] = v;
-    }
+    if (tid == 0) atomicAdd(reinterpret_cast<unsigned long long*>(hdr + 5),
+                            (unsigned long long)(s_part[0] + s_part[1] + s_part[2] + s_part[3]));
+    if (blockIdx.x != 0) return;
+    if (tid < kXHdrWords && tid != 5) hdr[tid] = w.w[tid];
     int32_t* si = reinterpret_cast<int32_t*>(hdr + kXHdrWords);
     for (int j = tid; j < sl; j += 256) si[j] = j < n_shards ? shard_index[j] : 0x7FFFFFFF;
 }
@@ -855,8 +860,11 @@ hipError_t launch_xhdr_fill(uint64_t* hdr, const uint64_t* w, const void* querie
                             const int32_t* shard_index, int n_shards, int sl, hipStream_t s) {
     XHdrWords hw;
     for (int i = 0; i < kXHdrWords; ++i) hw.w[i] = w[i];
-    hipLaunchKernelGGL(xhdr_fill, dim3(1), dim3(256), 0, s, hdr, hw, static_cast<const uint8_t*>(queries),
-                       query_bytes, shard_index, n_shards, sl);
+    hipError_t e = hipMemsetAsync(hdr + 5, 0, sizeof(uint64_t), s);
+    if (e != hipSuccess) return e;
+    const int64_t blocks = std::max<int64_t>(1, ((query_bytes >> 2) + kXhdrWords - 1) / kXhdrWords);
+    hipLaunchKernelGGL(xhdr_fill, dim3((unsigned)blocks), dim3(256), 0, s, hdr, hw,
+                       static_cast<const uint8_t*>(queries), query_bytes, shard_index, n_shards, sl);
     return hipGetLastError();
 }
 

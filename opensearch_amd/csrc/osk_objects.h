@@ -136,8 +136,15 @@ struct osk_seg {
     void* d_q8 = nullptr;
     float4* d_q8aux = nullptr;
     void* d_q8t = nullptr;    // the int8 rows in sq8_mfma's tiled layout (osk_seg_warm / first batched prefilter)
-    void* d_q6 = nullptr;     // the 6-bit tier (dims with sq6_supported): tiled codes, built with the int8 copy
-    float4* d_q6aux = nullptr;
+    void* d_q6 = nullptr;     // the 6-bit tier (dims with sq6_supported, tune sq6 on at staging): tiled codes,
+    float4* d_q6aux = nullptr;   // built with the int8 copy; freed when the segment's calibration turns it off
+    // The 6-bit tier's calibration, per segment: every view over the segment (a searcher's view, its
+    // leased replicas, the next refresh's view) shares it.  Probe calls count, per segment, the rows they
+    // re-bound from the int8 copy (read back asynchronously, osk_api.hip fold_probe); after kSq6Probes
+    // probes the tier stays on, or turns off (above sq6_probe_pct % of the rows) and its copy is freed.
+    std::atomic<int> sq6_state{0};     // 0 probing, 1 on, 2 off
+    int sq6_probes = 0;                // (guarded by mu)
+    int64_t sq6_probe_rows = 0, sq6_probe_rebound = 0;
     int units8 = 0;
     std::mutex mu;
     std::atomic<int> refs{1};          // the reader's reference + one per view that groups the segment
@@ -184,12 +191,13 @@ struct osk_view {
     int64_t sq6_calls = 0;
     osk::DevBuf ws_q6, ws_qc6, ws_floor;              // its query (nibble split, bound terms), floor buckets,
     osk::DevBuf ws_cand6, ws_cnt6;                    // the streaming pass's candidates per list
-    // the tier's calibration: its first kSq6Probes calls count the rows they re-bound from the int8 copy;
-    // when that exceeds sq6_probe_pct % of the rows scanned the view stops using the tier (data whose
-    // 6-bit bounds do not separate, e.g. uniform EUCLIDEAN rows: DESIGN.md §3f)
-    int sq6_probes = 0;
-    int64_t sq6_probe_rows = 0, sq6_probe_rebound = 0;
-    bool sq6_off = false;
+    // the tier's calibration (per segment, osk_seg::sq6_state): a probe call of this view counts its int8
+    // re-bounds per segment into d_seg_rebound, copies them to h_seg_rebound on its stream and records
+    // ev_probe; a later call folds them into the segments once the event has completed — nothing waits
+    osk::DevBuf d_seg_rebound;
+    osk::HostPinned h_seg_rebound;
+    hipEvent_t ev_probe = nullptr;
+    bool probe_pending = false;
     osk::DevBuf ws_q8, ws_qc, ws_sq8cand, ws_sq8lb, ws_lbmax, ws_trace;
     // settle slices: kSliceLists wave lists each, never spanning shards (an empty shard gets one
     // empty slice so that its result is still written)

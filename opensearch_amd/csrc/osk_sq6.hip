@@ -21,9 +21,9 @@
 // Results are bit-identical to the fp32 streaming scan.  Tiles are dispatched interleaved over shards
 // (osk_view::d_tile_order) so every round of workgroups scans a slice of every shard and each shard's
 // floor rises from the first round.  4-bit and 5-bit codes were simulated and rejected: their bounds
-// pass ≈ 100 % and ≈ 18 % of isotropic 768-dim rows.  A view whose first calls send more than
-// sq6_probe_pct % of the rows to the re-bound (e.g. uniform EUCLIDEAN rows, whose 6-bit bounds do not
-// separate) stops using the tier (osk_api.hip sq8_search).
+// pass ≈ 100 % and ≈ 18 % of isotropic 768-dim rows.  A segment whose first probe calls send more than
+// sq6_probe_pct % of its rows to the re-bound (e.g. uniform EUCLIDEAN rows, whose 6-bit bounds do not
+// separate) stops using the tier (osk_api.hip fold_probe).
 //
 // Code layout (per segment, "tiled"): blocks of 8 rows.  Lane t ∈ [0, 8) of a row owns the half-chunks
 // hc = 8j + t (j < C), each 32 dims [32hc, 32hc + 32); C = ⌈dim / 256⌉.  A code q = 4h + l with
@@ -502,6 +502,7 @@ __global__ __launch_bounds__(kBlock) void sq6_rebound(Sq8Params p) {
     if (tid == 0) {
         if (p.visited && p.q0 == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)(tile.row_end - tile.row_begin));
         if (p.counters && s_nc) atomicAdd(&p.counters[3], (unsigned long long)s_nc);
+        if (p.seg_rebound && s_nc) atomicAdd(&p.seg_rebound[tile.seg], (unsigned long long)s_nc);
     }
 }
 

@@ -639,22 +639,6 @@ hipError_t launch_sq8_scan(int nq, const Sq8Params& p, hipStream_t s, hipEvent_t
 // numbering are sq8_scan's with R = 16 rows per wave-iteration (the settle re-scans with scan_R = 16).
 // Filter pushdown: accepted rows are compacted 64 at a time; any row can feed any MFMA row slot.
 // ------------------------------------------------------------------------------------------------
-// LDS-DMA (global_load_lds_dwordx4) from a per-lane source into a wave-uniform LDS base (+ lane·16 B).
-// Written as asm so the compiler keeps no bookkeeping for it (its own LDS-DMA tracking puts vmcnt(0)
-// before every LDS read of the buffer): completion is counted by hand (vm_wait), and only the issuing
-// wave reads what it loaded.  M0 is saved and restored inside the statement (compiler-reserved).
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_byte) {
-    lds_byte = __builtin_amdgcn_readfirstlane(lds_byte);   // wave-uniform by construction; make it an SGPR
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(gsrc), "s"(lds_byte)
-                 : "memory");
-}
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
 // sq8_mfma's LDS-DMA ring: a group slot holds the group's 16 rows (row-major, exact width) then their
 // 16 bound terms.  The rows take KS LDS-DMA instructions; a slot holds exactly 16·u8 units when the
 // last instruction still has a lane of real data (u8 > 4(KS − 1)), else all KS·64 lanes land (clamped

@@ -73,6 +73,15 @@ class DeviceComm:
         check(lib().osk_comm_init_loopback(device, rank, world, buf, slot_bytes, C.byref(h)))
         return cls(h.value)
 
+    @classmethod
+    def init_all_loopback(cls, devices) -> "DeviceComm":
+        """Testing build only (inside `_lib.testing()`): init_all's one-process communicator whose grouped
+        all-gather is replaced by device copies, so `devices` may repeat (n local "devices" on one GPU)."""
+        d = np.asarray(devices, np.int32)
+        h = C.c_void_p()
+        check(lib().osk_comm_init_all_loopback(ptr(d), len(d), C.byref(h)))
+        return cls(h.value)
+
     def status(self) -> tuple[int, list[int]]:
         """(return code of osk_comm_status, [flag, rank 0's call number, differing rank, its call number]).
         Synchronise the calls' streams first."""

@@ -18,6 +18,7 @@ from __future__ import annotations
 import ctypes as C
 import enum
 import math
+import threading
 from dataclasses import dataclass, field
 from typing import Iterable, Sequence
 
@@ -227,6 +228,7 @@ class GpuFlatVectorsReader:
 
     def close(self) -> None:
         if self._h.value:
+            _GpuKnnVectorQuery._reader_closed(self)   # the reader-closed listener: drop views over it
             check(lib().osk_seg_release(self._h))
             self._h = C.c_void_p(None)
 
@@ -310,23 +312,48 @@ class _GpuKnnVectorQuery:
     * every filtered leaf goes to the device whatever its cost, so Lucene's `cost ≤ k` CPU exactSearch
       branch never runs; `exact_search` (the override of [L] AbstractKnnVectorQuery.exactSearch) serves a
       caller that still asks for a per-leaf exact search, on the device.
-    Results are identical to the per-leaf route (every device path is exact in the device order)."""
+    Results are identical to the per-leaf route (every device path is exact in the device order).
+
+    The view cache is keyed by the point-in-time leaf set and evicted by the reader-closed listener: when a
+    segment's reader closes (a refresh or merge dropped it), every cached view over it is released, so a
+    view never pins the HBM of segments no searcher can reach.  Creation is under a lock, so concurrent
+    rewrites of one leaf set share one view."""
     _views: dict = {}
+    _views_lock = threading.Lock()
 
     def _shard_view(self, leaves: Sequence[LeafReaderContext]) -> "DeviceShardSet":
         key = tuple((id(lf.reader), lf.reader.handle, lf.doc_base) for lf in leaves)
-        v = _GpuKnnVectorQuery._views.get(key)
-        if v is None:
-            v = DeviceShardSet([list(leaves)], [0])
-            _GpuKnnVectorQuery._views[key] = v
-        return v
+        with _GpuKnnVectorQuery._views_lock:
+            v = _GpuKnnVectorQuery._views.get(key)
+            if v is None:
+                v = DeviceShardSet([list(leaves)], [0])
+                _GpuKnnVectorQuery._views[key] = v
+            return v
 
-    @classmethod
-    def release_views(cls) -> None:
-        """The reader-closed listener: drop the cached views (the segments stay with their readers)."""
-        for v in cls._views.values():
+    # (the cache is the base class's: subclasses' classmethods must not rebind it on themselves)
+    @staticmethod
+    def _reader_closed(reader) -> None:
+        C_ = _GpuKnnVectorQuery
+        with C_._views_lock:
+            gone = [k for k in C_._views if any(rid == id(reader) for rid, _, _ in k)]
+            views = [C_._views.pop(k) for k in gone]
+        for v in views:
             v.close()
-        cls._views = {}
+
+    @staticmethod
+    def cached_views() -> int:
+        with _GpuKnnVectorQuery._views_lock:
+            return len(_GpuKnnVectorQuery._views)
+
+    @staticmethod
+    def release_views() -> None:
+        """Drop every cached view (the segments stay with their readers)."""
+        C_ = _GpuKnnVectorQuery
+        with C_._views_lock:
+            views = list(C_._views.values())
+            C_._views.clear()
+        for v in views:
+            v.close()
 
     def rewrite(self, leaves: Iterable[LeafReaderContext]) -> TopDocs:
         leaves = [lf for lf in leaves if lf.reader.field == self.field]

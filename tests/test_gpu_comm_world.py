@@ -13,8 +13,14 @@ device coordinator reduce with the cross-rank header check.  Only the byte trans
   and a k = 100 call that takes the merge_rank reduce;
 * a rank that recreates its view between calls (a refresh on one node only) still merges correctly —
   the shard indices travel with every call, nothing is cached per (communicator, view);
-* ranks that issue different calls (queries in another order, another from) get count −1 and a
-  poisoned communicator (OSK_ERR_INVALID), not a merge of unrelated lists.
+* ranks that issue different calls (queries in another order, another from, another batch size on the
+  host entry, batches that differ only in their last query) get count −1 and a poisoned communicator
+  (OSK_ERR_INVALID), not a merge of unrelated lists; a poisoned communicator's later device calls still
+  issue their collective (no rank may refuse on a flag the previous reduce writes asynchronously) and
+  report count −1;
+* one process driving several local devices (osk_comm_init_all; the testing build's
+  osk_comm_init_all_loopback maps its n "devices" to the one GPU and replaces the grouped all-gather by
+  device copies): the multi-device code of the host entry at n = 2 and 4 equals the oracle merge.
 
 Reference semantics: S/action/search/SearchPhaseController.java:224-253 (mergeTopDocs, setShardIndex),
 S/action/search/AbstractSearchAsyncAction.java:262-268 (one request per shard copy, loop index =
@@ -99,12 +105,30 @@ def _worker(rank, world, name, mode, out_q):
                 order = (5, 6) if rank == 0 else (6, 5)
                 first = device_call(1, 10, 0, 10, order[0])
                 rc, info = comm.status()
+                # the next call still runs its collective on every rank (sticky flag → count −1)
+                second = device_call(1, 10, 0, 10, order[1])
+                results = [int(first[3][0]), int(first[4][0]), rc, info, int(second[3][0])]
+            elif mode == "lastq":
+                # 165 queries × 100 dims = 16,500 words: the batches differ in the last query only
+                qs = _queries(165, 5)
+                if rank == 1:
+                    qs[-1] = qs[-1][::-1].copy()
+                dq = torch.from_numpy(qs).cuda()
+                torch.cuda.synchronize()
+                step = D.ShardSearchMerge(comm, view, spr, 165, 10, 0, 10, device=0)
+                res = step(dq.data_ptr(), stream.cuda_stream)
+                stream.synchronize()
+                rc, info = comm.status()
+                results = [res[3].cpu().numpy().copy(), rc]
+            elif mode == "misnq":
+                # host entry, another batch size on rank 1: caught by the fixed-size call agreement before
+                # the (differently sized) block gather
+                nq = 2 if rank == 0 else 3
                 try:
-                    device_call(1, 10, 0, 10, order[1])
-                    second = None
+                    D.shards_search_merge(comm, [view], _queries(nq, 5), 10, 0, 10)
+                    results = ["no error"]
                 except _lib.OskError as e:
-                    second = e.code
-                results = [int(first[3][0]), int(first[4][0]), rc, info, second]
+                    results = [e.code, str(e)]
             elif mode == "misfrom":
                 # host entry, same block size, another `from` on rank 1
                 from_ = 0 if rank == 0 else 2
@@ -196,10 +220,65 @@ def test_misordered_calls_poison_the_communicator():
         count, total, rc, info, second = out[r]
         assert count == -1 and total == -1
         assert rc == -1 and info[0] == 1 and info[1] == 1 and info[2] == 1 and info[3] == 1
-        assert second == -1   # OSK_ERR_INVALID: refused, no collective issued
+        assert second == -1   # the next call ran its collective; its reduce reports the sticky poison
 
 
 def test_mismatched_from_fails_the_host_entry():
     out = _run(2, "misfrom")
     for r in range(2):
         assert out[r][0] == -1 and "poisoned" in out[r][1], out[r]
+
+
+def test_batches_differing_only_in_the_last_query_are_caught():
+    out = _run(2, "lastq")
+    for r in range(2):
+        counts, rc = out[r]
+        assert (counts == -1).all() and rc == -1, (r, counts[:4], rc)
+
+
+def test_mismatched_batch_size_fails_the_host_entry_before_the_gather():
+    out = _run(2, "misnq")
+    for r in range(2):
+        assert out[r][0] == -1 and "poisoned" in out[r][1], out[r]
+
+
+@pytest.mark.parametrize("n_local", [2, 4])
+def test_init_all_multi_device_host_entry(n_local, expected):
+    """One process, n local "devices" (all the one GPU): views[i] holds local device i's shards, the grouped
+    exchange runs through the testing build's device-copy transport, the reduce on local device 0."""
+    import ctypes as C
+
+    from opensearch_amd import _lib, distributed as D
+    from opensearch_amd._lib import check, ptr
+    with _lib.testing():
+        L = _lib.lib()
+        segs, views = [], []
+        for i in range(n_local):
+            shards = D.owned_shards(i, N_SHARDS, n_local)
+            mine = []
+            for s in shards:
+                h = C.c_void_p()
+                check(L.osk_seg_synth(0, SIZES[s], DIM, _lib.FLOAT32, SIM, SEED, DIST, int(ROW0[s]), C.byref(h)))
+                mine.append(h.value)
+            arr = (C.c_void_p * len(mine))(*mine)
+            seg_shard = np.arange(len(mine), dtype=np.int32)
+            base = np.zeros(len(mine), np.int32)
+            sidx = np.asarray(shards, np.int32)
+            v = C.c_void_p()
+            check(L.osk_view_create(arr, len(mine), ptr(seg_shard), ptr(base), len(mine), ptr(sidx), C.byref(v)))
+            segs += mine
+            views.append(v)
+        comm = D.DeviceComm.init_all_loopback([0] * n_local)
+        try:
+            assert (comm.rank, comm.world, comm.n_local) == (0, n_local, n_local)
+            results = [list(D.shards_search_merge(comm, views, _queries(nq, qs), k, f, sz))
+                       for (nq, k, f, sz, _, qs) in CALLS]
+            _check(results, expected)
+            rc, info = comm.status()
+            assert rc == 0 and info[0] == 0
+        finally:
+            comm.close()
+            for v in views:
+                check(L.osk_view_release(v))
+            for h in segs:
+                check(L.osk_seg_release(C.c_void_p(h)))

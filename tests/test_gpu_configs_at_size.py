@@ -4,7 +4,9 @@ Every view here is at least CUs × 24 × 1,024 rows (≈ 6.29M on an MI355X, the
 osk_view_create) or is the benchmarked config itself, and each path the bench takes at
 that size is checked against the oracle — docs, shard indices and score bits of the coordinator merge:
 
-* C3-shaped 6.5M × 768 COSINE, 8 shards: batch 1 on the VALU int8 prefilter (sq8_scan), batch 32 on
+* C3-shaped 6.5M × 768 COSINE, 8 shards: batch 1 on the 6-bit tier (sq6_pilot + sq6_scan + the int8
+  re-bound, DESIGN.md §3f — the headline kernel), both on a calibration probe and in the steady state
+  after the segments' calibration has kept the tier, batch 32 on
   the int8 MFMA prefilter (sq8_mfma, register path at 768 dims), batch 256 on the bf16×3 MFMA
   candidate path, batches 128 / 160 / 192 on whichever path the library's cost model picks (the
   test restates the model and asserts the choice), and a 10 %-filtered single query (compacted
@@ -109,16 +111,25 @@ def c3():
         r.close()
 
 
-def _search_counted(ds, queries, k=10):
-    before = {c: ds.counter(c) for c in ("sq8_calls", "mfma_calls")}
+def _search_counted(ds, queries, k=10, counters=("sq8_calls", "mfma_calls")):
+    before = {c: ds.counter(c) for c in counters}
     out = ds.search(queries, k, 0, k)
     return out, {c: ds.counter(c) - before[c] for c in before}
 
 
-def test_c3_b1_sq8_scan(c3):
+def test_c3_b1_6bit_tier_probe_and_steady_state(c3):
+    """The headline path at C3 shape: a single query on the 6-bit tier, first as one of the segments'
+    calibration probes, then again once the calibration (4 probes, folded asynchronously by later calls)
+    has kept the tier — both equal the oracle bit for bit."""
     ds, q, samp, want = c3
-    out, d = _search_counted(ds, q["b1"])
-    assert d == {"sq8_calls": 1, "mfma_calls": 0}
+    counters = ("sq8_calls", "mfma_calls", "sq6_calls")
+    out, d = _search_counted(ds, q["b1"], counters=counters)
+    assert d == {"sq8_calls": 1, "mfma_calls": 0, "sq6_calls": 1}, d
+    _check(out, want["b1"], samp["b1"], 10)
+    for i in range(5):   # more probes (the 5th call folds the 4th), other queries
+        ds.search(q["b32"][i:i + 1], 10, 0, 10)
+    out, d = _search_counted(ds, q["b1"], counters=counters)
+    assert d == {"sq8_calls": 1, "mfma_calls": 0, "sq6_calls": 1}, d   # the calibration kept the tier
     _check(out, want["b1"], samp["b1"], 10)
 
 

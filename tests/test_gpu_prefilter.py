@@ -240,6 +240,7 @@ def test_prefilter_multi_shard_from_size():
         close_all(ds, readers)
 
 
+@pytest.mark.parametrize("scan_kernel", ["mfma32"], indirect=True)   # (one scan-kernel variant only)
 @pytest.mark.parametrize("slots", [2, 4])
 @pytest.mark.parametrize("dim,sim", [(17, COS), (96, LU.VectorSimilarityFunction.DOT_PRODUCT),
                                      (128, LU.VectorSimilarityFunction.EUCLIDEAN),
@@ -247,8 +248,6 @@ def test_prefilter_multi_shard_from_size():
 def test_mfma_ring_depths(slots, dim, sim, scan_kernel):
     """The LDS-DMA ring at every depth: ragged segment sizes (partial 16-row groups at wave ends),
     several segments and shards, a sparse field without a filter; equal to the fp32 scan and the oracle."""
-    if scan_kernel != "mfma32":
-        pytest.skip("ring depth sweep runs once")
     sizes = [5000, 1237, 16, 3, 777]
     segs = [corpus(n, dim, sim, 700 + i) for i, n in enumerate(sizes)]
     queries = corpus(33, dim, sim, 710)

@@ -96,3 +96,37 @@ def test_exact_search_override_serves_cost_le_k_leaves_on_the_device(shard):
         s, d = hits(td)
         assert len(d) == int(acc.sum()) <= K
         assert np.array_equal(d, ed + lf.doc_base) and np.array_equal(s, es.view(np.uint32))
+
+
+def test_view_cache_is_evicted_when_a_reader_closes_and_shared_under_concurrency():
+    """The query's per-leaf-set view cache: concurrent rewrites of one leaf set share one view, and the
+    reader-closed listener releases every view over a closed segment (no HBM pinned by stale views)."""
+    import threading
+
+    LU.GpuKnnFloatVectorQuery.release_views()
+    rows = [O.synth(0, n, DIM, 950 + i, 3) for i, n in enumerate([700, 900])]
+    readers = [LU.GpuFlatVectorsReader("v", r, COS) for r in rows]
+    leaves = [LU.LeafReaderContext(0, 0, readers[0]), LU.LeafReaderContext(1, 700, readers[1])]
+    q = O.synth(0, 1, DIM, 960, 3)[0]
+    outs, errs = [], []
+
+    def run():
+        try:
+            outs.append(LU.GpuKnnFloatVectorQuery("v", q, K).rewrite(leaves))
+        except Exception as e:   # pragma: no cover - reported below
+            errs.append(e)
+    try:
+        ts = [threading.Thread(target=run) for _ in range(8)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert not errs, errs
+        assert LU.GpuKnnFloatVectorQuery.cached_views() == 1
+        assert all([sd.doc for sd in o.score_docs] == [sd.doc for sd in outs[0].score_docs] for o in outs)
+        readers[0].close()
+        assert LU.GpuKnnFloatVectorQuery.cached_views() == 0
+    finally:
+        for r in readers:
+            r.close()
+        LU.GpuKnnFloatVectorQuery.release_views()

@@ -282,3 +282,91 @@ def test_large_view_keeps_the_tier(sim):
         ds.close()
         for r in readers:
             r.close()
+
+
+def _footprint(reader):
+    b = C.c_int64()
+    _lib.check(_lib.lib().osk_seg_footprint(reader.handle, C.byref(b)))
+    return b.value
+
+
+@pytest.mark.parametrize("sim", [LU.VectorSimilarityFunction.EUCLIDEAN, COS], ids=lambda s: s.name)
+def test_calibration_is_per_segment_and_shared_by_views(sim):
+    """The tier's calibration lives on the segments, not on a view object: the first view's probes decide
+    for every segment (read back asynchronously, folded by later calls), a second view over the same
+    segments and the replicas that concurrent host calls lease follow that decision without probing again,
+    and a segment whose tier turned off (uniform EUCLIDEAN rows) frees its 6-bit copy."""
+    import threading
+
+    rows = corpus(120_000, 768, sim, 120)
+    queries = corpus(12, 768, sim, 121)
+    ds, readers = view_of([rows[:60_000], rows[60_000:]], sim, [0, 1])
+    ds2 = None
+    try:
+        fp0 = [_footprint(r) for r in readers]
+        out = one_by_one(lambda q: ds.search(q, 10, 0, 10), queries[:5])   # 4 probes, the 5th call folds
+        c1 = ds.counter("sq6_calls")
+        keeps = sim == COS
+        assert c1 == (5 if keeps else 4), c1
+        fp1 = [_footprint(r) for r in readers]
+        sq6 = [((60_000 + 7) // 8) * 3 * 1536 + 60_000 * 16] * 2
+        assert fp1 == (fp0 if keeps else [a - b for a, b in zip(fp0, sq6)]), (fp0, fp1)
+        # a second view over the same segments: no probes, the segments' decision
+        ds2 = LU.DeviceShardSet([[LU.LeafReaderContext(0, 0, readers[0])], [LU.LeafReaderContext(0, 0, readers[1])]])
+        out2 = one_by_one(lambda q: ds2.search(q, 10, 0, 10), queries[:5])
+        assert ds2.counter("sq6_calls") == (5 if keeps else 0)
+        assert_same(out, out2)
+        # concurrent host calls lease replicas of the first view: every slot follows the segments' state
+        res, errs = {}, []
+
+        def worker(i):
+            try:
+                res[i] = ds.search(queries[5 + i % 7:6 + i % 7], 10, 0, 10)
+            except Exception as e:   # pragma: no cover - reported below
+                errs.append(e)
+        ts = [threading.Thread(target=worker, args=(i,)) for i in range(16)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert not errs, errs
+        assert ds.counter("sq6_calls") - c1 == (16 if keeps else 0)
+        want = tuned("sq6", 0, lambda: one_by_one(lambda q: ds.search(q, 10, 0, 10), queries[5:12]))
+        for i in range(16):
+            assert_same(res[i], tuple(w[i % 7:i % 7 + 1] for w in want))
+    finally:
+        if ds2 is not None:
+            ds2.close()
+        close_all(ds, readers)
+
+
+def test_first_device_call_returns_before_its_work_completes():
+    """A calibration probe is asynchronous: the view's first osk_view_search_device call (after warm) returns
+    while its launches are still running, and its counts are folded by a later call without a wait."""
+    import torch
+    rps, dim = 2_000_000, 768
+    readers = [LU.GpuFlatVectorsReader.synthetic("v", rps, dim, COS, seed=31, dist=3, row0=s * rps) for s in range(2)]
+    ds = LU.DeviceShardSet([[LU.LeafReaderContext(0, 0, r)] for r in readers])
+    try:
+        _lib.check(_lib.lib().osk_view_warm(ds.handle, _lib.OSK_WARM_PREFILTER))
+        q = torch.from_numpy(O.synth(0, 1, dim, 32, 3)).cuda()
+        keys = torch.zeros((1, 2, 10), dtype=torch.int64, device="cuda")
+        counts = torch.zeros((1, 2), dtype=torch.int32, device="cuda")
+        st = torch.cuda.Stream()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(st):
+            _lib.check(_lib.lib().osk_view_search_device(ds.handle, q.data_ptr(), 1, 10, None, keys.data_ptr(),
+                                                         counts.data_ptr(), None, st.cuda_stream))
+            pending = not st.query()
+        st.synchronize()
+        assert pending, "the probe call waited for its own work"
+        assert ds.counter("sq6_calls") == 1
+        assert counts.cpu().numpy().tolist() == [[10, 10]]
+        want = ds.search(q.cpu().numpy(), 10, 0, 10)   # (a later call: folds the probe)
+        got = np.sort(keys.cpu().numpy().view(np.uint64).reshape(-1))[::-1][:10]
+        sc, dc = LU.decode_keys(got)
+        assert np.array_equal(bits(sc), bits(want[0][0]))
+    finally:
+        ds.close()
+        for r in readers:
+            r.close()
