@@ -26,10 +26,10 @@ LIB = PKG / "libosknn.so"
 LIB_TESTING = PKG / "libosknn_testing.so"
 # the sources whose objects differ in the testing build (the C-ABI's test knobs; sq8_mfma's A/B ablations;
 # the loopback transport of the multi-rank exchange)
-TESTING_VARIANTS = ("osk_api.hip", "osk_sq8.hip", "osk_sq6.hip", "osk_comm.hip")
+TESTING_VARIANTS = ("osk_api.hip", "osk_sq8.hip", "osk_sq8w.hip", "osk_sq6.hip", "osk_comm.hip")
 OBJDIR = ROOT / "build" / "osknn"
 
-SOURCES = ["osk_kernels.hip", "osk_mfma.hip", "osk_sq8.hip", "osk_sq6.hip", "osk_filter.hip", "osk_select.hip", "osk_api.hip", "osk_comm.hip", "osk_host.cpp"]
+SOURCES = ["osk_kernels.hip", "osk_mfma.hip", "osk_sq8.hip", "osk_sq8w.hip", "osk_sq6.hip", "osk_filter.hip", "osk_select.hip", "osk_api.hip", "osk_comm.hip", "osk_host.cpp"]
 HEADERS = ["osk_common.h", "osk_internal.h", "osk_wave.h", "osk_objects.h", "osk_device.h"]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

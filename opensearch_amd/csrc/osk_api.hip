@@ -150,6 +150,7 @@ osk_seg::~osk_seg() {
     if (d_q8) (void)hipFree(d_q8);
     if (d_q8aux) (void)hipFree(d_q8aux);
     if (d_q8t) (void)hipFree(d_q8t);
+    if (d_q8bmax) (void)hipFree(d_q8bmax);
     if (d_q6) (void)hipFree(d_q6);
     if (d_q6aux) (void)hipFree(d_q6aux);
 }
@@ -163,6 +164,7 @@ int64_t osk_seg::hbm_bytes() const {
     if (d_split) b += std::max<int64_t>(1, (n_rows + 127) / 128) * 8 * split_KS * 2 * 1024 + n * 4 + 4;
     if (d_q8) b += n * units8 * 16 + n * 16;
     if (d_q8t) b += std::max<int64_t>(1, (n_rows + 15) / 16) * sq8_mfma_ks(units8) * 1024;
+    if (d_q8bmax) b += std::max<int64_t>(1, (n_rows + 15) / 16) * 16;
     if (d_q6) b += sq6_bytes(n_rows, dim);
     return b;
 }
@@ -301,6 +303,7 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         {"sq8_mfma_nt", &g_tuning.sq8_mfma_nt, 0, 1, false},
         {"sq8_mfma_queries", &g_tuning.sq8_mfma_queries, 16, 32, false},
         {"sq8_mfma_min", &g_tuning.sq8_mfma_min, 0, 1 << 20, false},
+        {"sq8_wide_min", &g_tuning.sq8_wide_min, 0, 1 << 20, false},
         {"sq8_mfma_ring", &g_tuning.sq8_mfma_ring, -1, 8, false},
         {"i8_stream", &g_tuning.i8_stream, 0, 1, false},
         {"call_timing", &g_tuning.call_timing, 0, 1, false},
@@ -694,8 +697,8 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
     OSK_HIP(v->d_tile_coff.reserve(sizeof(int32_t) * tile_coff.size()));
     OSK_HIP(v->d_tile_order.reserve(sizeof(int32_t) * tile_order.size()));
     OSK_HIP(v->d_seg_vrow.reserve(sizeof(int64_t) * n_segs));
-    OSK_HIP(v->d_counters.reserve(sizeof(unsigned long long) * 4));
-    OSK_HIP(hipMemsetAsync(v->d_counters.p, 0, sizeof(unsigned long long) * 4, st));
+    OSK_HIP(v->d_counters.reserve(sizeof(unsigned long long) * 8));
+    OSK_HIP(hipMemsetAsync(v->d_counters.p, 0, sizeof(unsigned long long) * 8, st));
     OSK_HIP(hipMemcpyAsync(v->d_seg_vrow.p, vrow.data(), sizeof(int64_t) * n_segs, hipMemcpyHostToDevice, st));
     OSK_HIP(hipMemcpyAsync(v->d_segs.p, sd.data(), sizeof(SegDev) * n_segs, hipMemcpyHostToDevice, st));
     if (!tiles.empty())
@@ -1104,22 +1107,41 @@ int32_t ensure_sq8t_seg(osk_seg* s, hipStream_t st) {
         return OSK_ERR_OOM;
     }
     OSK_HIP(launch_sq8_tile(s->d_q8, s->n_rows, u8, ks, q8t, st));
+    float4* bmax = nullptr;   // the wide kernel's per-block maxima of the bound terms (16 B per 16 rows)
+    if (sq8_wide_supported(u8)) {
+        e = hipMalloc(&bmax, (size_t)blocks * sizeof(float4));
+        if (e != hipSuccess) {
+            (void)hipFree(q8t);
+            set_error(std::string("hipMalloc of the block maxima failed: ") + hipGetErrorString(e));
+            return OSK_ERR_OOM;
+        }
+        OSK_HIP(launch_sq8_block_max(s->d_q8aux, s->n_rows, bmax, st));
+    }
     OSK_HIP(hipStreamSynchronize(st));
     s->d_q8t = q8t;
+    s->d_q8bmax = bmax;
     return OSK_OK;
 }
 
 int32_t ensure_sq8t(osk_view* v, hipStream_t st) {
     if (v->sq8t_ready) return OSK_OK;
     const int ns = (int)v->segs.size();
-    std::vector<const void*> rows(ns);
+    std::vector<const void*> rows(ns), bmax(ns);
     for (int i = 0; i < ns; ++i) {
         int32_t rc = ensure_sq8t_seg(v->segs[i], st);
         if (rc) return rc;
         rows[i] = v->segs[i]->d_q8t;
+        bmax[i] = v->segs[i]->d_q8bmax;
     }
+    std::vector<int32_t> sqb(v->shard_tile_begin.size());
+    for (size_t i = 0; i < sqb.size(); ++i) sqb[i] = 4 * v->shard_tile_begin[i];   // the wide kernel's quarters
     OSK_HIP(v->d_sq8_rows_t.reserve(sizeof(void*) * ns));
+    OSK_HIP(v->d_sq8_bmax.reserve(sizeof(void*) * ns));
+    OSK_HIP(v->d_shard_quarter_begin.reserve(sizeof(int32_t) * sqb.size()));
     OSK_HIP(hipMemcpyAsync(v->d_sq8_rows_t.p, rows.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
+    OSK_HIP(hipMemcpyAsync(v->d_sq8_bmax.p, bmax.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
+    OSK_HIP(hipMemcpyAsync(v->d_shard_quarter_begin.p, sqb.data(), sizeof(int32_t) * sqb.size(), hipMemcpyHostToDevice,
+                           st));
     OSK_HIP(hipStreamSynchronize(st));
     v->sq8t_ready = true;
     return OSK_OK;
@@ -1305,6 +1327,9 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     // scan, ≤ 8 per launch.  Filtered VALU scans run over the compacted accepted ordinals.  A single
     // unfiltered query scans the 6-bit tier where the view has one.
     const bool use_mfma = g_tuning.sq8_mfma_min > 0 && nq >= g_tuning.sq8_mfma_min && sq8_mfma_supported(u8);
+    // large unfiltered batches of ≤ 256-dim rows: one corpus pass per kWideQ queries (osk_sq8w.hip)
+    const bool use_wide = use_mfma && !d_accept && g_tuning.sq8_wide_min > 0 && nq >= g_tuning.sq8_wide_min &&
+                          sq8_wide_supported(u8);
     // the 6-bit tier: single unfiltered queries, every segment's calibration probing or on.  The shared
     // lock keeps a segment's copy alive from this check to the launches (fold_probe frees it under the
     // exclusive one after a device synchronisation)
@@ -1394,14 +1419,16 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
         p.scnt = fp.scnt;
         p.gather_min = g_tuning.gather_min;
     }
-    const int chunk = use_mfma ? (int)g_tuning.sq8_mfma_queries : kMaxNQ;
+    const int chunk = use_wide ? kWideQ : use_mfma ? (int)g_tuning.sq8_mfma_queries : kMaxNQ;
     if (use_mfma) {
         rc = ensure_sq8t(v, st);
         if (rc) return rc;
         p.rows8t = v->d_sq8_rows_t.as<const int4*>();
-        OSK_HIP(v->ws_pilot.reserve(sizeof(uint64_t) * (size_t)kMfmaQueries * v->n_tiles * 64));
-        OSK_HIP(v->ws_thr.reserve(sizeof(uint64_t) * (size_t)kMfmaQueries * S * 64));
-        OSK_HIP(v->ws_thr_counts.reserve(sizeof(int32_t) * (size_t)kMfmaQueries * S));
+        p.bmax = v->d_sq8_bmax.as<const float4*>();
+        const size_t qmax = use_wide ? kWideQ : kMfmaQueries;
+        OSK_HIP(v->ws_pilot.reserve(sizeof(uint64_t) * qmax * v->n_tiles * (use_wide ? 4 : 64)));
+        OSK_HIP(v->ws_thr.reserve(sizeof(uint64_t) * qmax * S * 64));
+        OSK_HIP(v->ws_thr_counts.reserve(sizeof(int32_t) * qmax * S));
     }
     for (int q0 = 0; q0 < nq; q0 += chunk) {
         p.q0 = q0;
@@ -1411,7 +1438,30 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
         p.qn_dev = v->ws_qnorm.as<float>() + q0;
         hipEvent_t e0 = v->profile && q0 == 0 ? v->ev0 : nullptr;
         hipEvent_t e1 = v->profile && q0 + chunk >= nq ? v->ev1 : nullptr;
-        if (use_mfma) {
+        if (use_wide) {
+            // pilot: the first 16 rows of every quarter → per (query, quarter) the best lower-bound key →
+            // per (query, shard) the top k (one key per quarter); its k-th floors the main pass
+            if (v->n_cus <= 0 &&
+                (hipDeviceGetAttribute(&v->n_cus, hipDeviceAttributeMultiprocessorCount, v->device) != hipSuccess ||
+                 v->n_cus <= 0))
+                v->n_cus = 256;
+            p.wide_grid = v->n_cus;
+            p.tile_order = v->d_tile_order.as<int32_t>();
+            p.k = k;
+            p.n_shards = S;
+            p.ablate = g_tuning.sq8_mfma_ablate;
+            p.counters = v->d_counters.as<unsigned long long>();   // (testing build: event counts)
+            p.pilot = 1;
+            p.pilot_keys = v->ws_pilot.as<uint64_t>();
+            OSK_HIP(launch_sq8_wide(p, st, e0, nullptr));
+            OSK_HIP(launch_merge_shards(v->ws_pilot.as<uint64_t>(), 4 * v->n_tiles,
+                                        v->d_shard_quarter_begin.as<int32_t>(), S, p.q_count, k,
+                                        v->ws_thr.as<uint64_t>(), v->ws_thr_counts.as<int32_t>(), st, 1));
+            p.pilot = 0;
+            p.thr_keys = v->ws_thr.as<uint64_t>();
+            p.thr_counts = v->ws_thr_counts.as<int32_t>();
+            OSK_HIP(launch_sq8_wide(p, st, nullptr, e1));
+        } else if (use_mfma) {
             // pilot: 16 sampled rows per wave → per (query, tile) the top k sampled lower bounds →
             // per (query, shard) the top k; its k-th floors the main pass's quick thresholds
             // (sq8_mfma comment)
@@ -1489,8 +1539,14 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
         OSK_HIP(v->ws_trace.reserve(sizeof(unsigned long long) * 8 * (size_t)nq * n_slices));
         sp.trace = v->ws_trace.as<unsigned long long>();
     }
-    OSK_HIP(launch_sq8_settle(v->cfg, nq, sp, st));
+    if (use_wide && !sp.force_fail) {   // (forced exact lists are the per-slice settle's test knob)
+        sp.shard_tile_begin = v->d_shard_tile_begin.as<int32_t>();
+        OSK_HIP(launch_sq8_settle_wide(v->cfg, nq, sp, st));
+    } else {
+        OSK_HIP(launch_sq8_settle(v->cfg, nq, sp, st));
+    }
     v->sq8_calls += 1;
+    v->sq8w_calls += use_wide ? 1 : 0;
     v->sq6_calls += use6 ? 1 : 0;
     if (probe6) {   // read back asynchronously: a later call folds it (fold_probe), nothing waits here
         OSK_HIP(hipMemcpyAsync(v->h_seg_rebound.p, v->d_seg_rebound.p, sizeof(unsigned long long) * ns,
@@ -1696,8 +1752,14 @@ int32_t view_search_device(osk_view* v, const void* d_queries, int nq, int k,
     const bool sq8_ok = sq8_on && k <= kKQ - 4;
     double R = 0.0;
     for (const osk_seg* sg : v->segs) R += (double)sg->n_rows;
+    const int u8v = (v->dim + 15) / 16;
+    const bool wide_ok = sq8_wide_supported(u8v) && !d_accept && g_tuning.sq8_wide_min > 0 &&
+                         nq >= g_tuning.sq8_wide_min && g_tuning.sq8_mfma_min > 0 && nq >= g_tuning.sq8_mfma_min;
+    // the wide int8 MFMA kernel (osk_sq8w.hip), per launch of ≤ 256 queries: the tiled rows (64 B per 64-dim
+    // k-step), their 16-B bound terms and the block maxima at ≈ 5 TB/s, plus pilot, merges and settle
     const double sq8_us =
-        (double)((nq + 31) / 32) * (R * (16.0 * ((v->dim + 15) / 16) + 16.0) / 4.3e6 + 165.0 + 0.28 * v->dim);
+        wide_ok ? (double)((nq + kWideQ - 1) / kWideQ) * (R * (64.0 * sq8_mfma_ks(u8v) + 17.0) / 5.0e6 + 100.0)
+                : (double)((nq + 31) / 32) * (R * (16.0 * u8v + 16.0) / 4.3e6 + 165.0 + 0.28 * v->dim);
     const double bf_us = (double)((nq + 255) / 256) * (R * (0.153 + 0.00119 * v->dim) * 1e-3 + 325.0);
     const bool blocks_cheaper = bf_us * 100.0 <= sq8_us * (double)g_tuning.sq8_cost_pct;
     const bool batched = v->enc == ENC_FLOAT32 && g_tuning.mfma_min_batch > 0 &&
@@ -1902,9 +1964,9 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
         return OSK_OK;
     }
     const bool dev = n == "sq8_fallback_queries" || n == "sq8_rescored_rows" || n == "sq8_exact_tiles" ||
-                     n == "sq6_rebound_rows";
+                     n == "sq6_rebound_rows" || n == "sq8_wide_events" || n == "sq8_wide_pairs";
     OSK_REQUIRE(dev || n == "mfma_calls" || n == "mfma_fallback_queries" || n == "sq8_calls" || n == "sq6_calls" ||
-                    n == "select_calls",
+                    n == "select_calls" || n == "sq8_wide_calls",
                 "unknown counter: " + n);
     // summed over the view and the replicas its host entries leased
     int64_t sum = 0;
@@ -1912,14 +1974,17 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
         std::lock_guard<std::mutex> lk(s->mu);
         if (dev) {
             if (!s->d_counters.p) continue;
-            unsigned long long c[4];
+            unsigned long long c[8];
             OSK_HIP(hipDeviceSynchronize());   // the last search may be on any stream
             OSK_HIP(hipMemcpy(c, s->d_counters.p, sizeof(c), hipMemcpyDeviceToHost));
+            // [4], [5]: the wide kernel's insertion events and quick-test passes (testing build only)
             sum += (int64_t)(n == "sq8_fallback_queries" ? c[0] : n == "sq8_rescored_rows" ? c[1]
-                             : n == "sq8_exact_tiles" ? c[2] : c[3]);
+                             : n == "sq8_exact_tiles" ? c[2] : n == "sq6_rebound_rows" ? c[3]
+                             : n == "sq8_wide_events" ? c[4] : c[5]);
         } else {
             sum += n == "mfma_calls" ? s->mfma_calls : n == "mfma_fallback_queries" ? s->mfma_fallback_queries
-                 : n == "sq8_calls" ? s->sq8_calls : n == "sq6_calls" ? s->sq6_calls : s->sel_calls;
+                 : n == "sq8_calls" ? s->sq8_calls : n == "sq6_calls" ? s->sq6_calls
+                 : n == "sq8_wide_calls" ? s->sq8w_calls : s->sel_calls;
         }
     }
     *value = sum;

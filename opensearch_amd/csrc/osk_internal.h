@@ -180,6 +180,7 @@ struct Sq8Params {
     int32_t* cnt6;                   // [q][n_lists] their count (> cap6: overflowed)
     int cap6;
     const float4* const* bmax;       // sq8_wide: per segment, the 16-row block maxima (launch_sq8_block_max)
+    int wide_grid;                   // sq8_wide: persistent workgroups (the device's CUs)
 };
 
 struct SettleParams {
@@ -214,7 +215,12 @@ struct SettleParams {
     const int32_t* scnt;
     int gather_min;
     unsigned long long* trace;       // A/B only: per (query, slice) 8 slots of phase timestamps, or null
+    const int32_t* shard_tile_begin; // sq8_settle_wide: [n_shards + 1] (a shard's lists are 4·[begin, end))
 };
+// The settle of wide batches (osk_sq8.hip): one workgroup per (shard, query) over all the shard's lists —
+// the per-slice settle's ≈ n_lists / 32 workgroups per query left 786k workgroups at 100M rows × 1024
+// queries (4.3 ms, mostly threshold loads).  Unfiltered views only; writes shard_keys / shard_counts itself.
+hipError_t launch_sq8_settle_wide(int cfg, int nq, const SettleParams& p, hipStream_t s);
 
 // Filter pushdown by compaction (osk_filter.hip): per segment, the accepted ordinals in ascending order
 // at comp[seg_vrow[seg] …], scnt[seg] of them.
@@ -335,7 +341,7 @@ hipError_t launch_sq8_mfma(const Sq8Params& p, hipStream_t s, hipEvent_t ev_star
 // ≤ 256 int8 dims, unfiltered.  One workgroup per (tile, quarter) — the settle's list of a scan wave with
 // scan_R = kMfmaScanR — whose 4 waves share the quarter's rows, staged once through an LDS-DMA ring, and
 // each own 64 of the queries (lists per (quarter, query) in LDS).  pilot = 1: each workgroup bounds only
-// its quarter's first 16 rows and writes, per query, the best lower-bound key of them to
+// its quarter's first 64 rows and writes, per query, the best lower-bound key of them to
 // pilot_keys [q][4·n_tiles].
 constexpr int kWideQB = 4;                      // 16-query MFMA blocks per wave
 constexpr int kWideQ = 4 * 16 * kWideQB;        // queries per launch
@@ -410,7 +416,7 @@ struct Tuning {
     std::atomic<int> sq8_mfma_queries{32};    // queries per sq8_mfma launch: 16 or 32 (two MFMA chains per row operand)
     std::atomic<int> sq8_mfma_ablate{0};  // TESTING. A/B timing only: 1 skip sq8_mfma's epilogue, 2 its MFMAs (results wrong)
     std::atomic<int> sq8_mfma_min{2};     // prefilter batches ≥ this scan on int8 MFMA, 16 queries per launch (0 = never)
-    std::atomic<int> sq8_wide_min{48};    // ...and unfiltered batches ≥ this on the wide kernel, kWideQ per launch (0 = never)
+    std::atomic<int> sq8_wide_min{0};     // ...and unfiltered batches ≥ this on the wide kernel, kWideQ per launch (0 = never)
     std::atomic<int> sq8_force_fallback{0};   // TESTING. tests: every list of a prefiltered search is re-scanned exactly
     std::atomic<int> settle_trace{0};     // TESTING. A/B only: record settle phase timestamps (debug copy "settle_trace")
     std::atomic<int> mfma_ablate{0};      // TESTING. A/B only: 1 skip the epilogue, 2 skip query staging, 4 skip corpus staging,

@@ -1530,11 +1530,169 @@ __global__ __launch_bounds__(kSettleThreads) void sq8_settle_merge(SettleParams 
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// the settle of a wide batch, one workgroup per (shard, query):
+//   (a) L = the k-th best of 64 bucket maxima of the lists' best lower bounds over ALL the shard's lists
+//       (bucket = list mod 64: each maximum is a distinct row's lb, so L ≤ the shard's k-th best lb — the
+//       per-slice settle's argument over one group of the shard's lists; over all of them L is no lower);
+//   (b) the lists in chunks of 256: a list with no row (best lb 0) is skipped without reading its keys;
+//       a full list whose 16th upper bound reaches L (it may have dropped a qualifying row) is re-scanned
+//       exactly; the other lists' rows with ub ≥ L are re-scored exactly (scan_f32's arithmetic);
+//   (c) the 4 waves' top k → shard_keys / shard_counts.
+// Exactness is sq8_settle's: every row of the shard's top k has ub ≥ exact ≥ T ≥ L, so it is re-scored or
+// lies in a re-scanned list.
+// ------------------------------------------------------------------------------------------------
+constexpr int kWideChunk = 256;   // lists per chunk of the list walk
+template <int L, int V, bool L2K>
+__global__ __launch_bounds__(kSettleThreads) void sq8_settle_wide(SettleParams p) {
+    constexpr int R = 64 / L, UP = L * V;
+    __shared__ uint32_t s_bm[kSettleWaves][64];
+    __shared__ uint64_t s_keys[64];
+    __shared__ uint32_t s_L;
+    __shared__ uint32_t s_cand[kWideChunk * kKQ];
+    __shared__ int32_t s_exact[kWideChunk];
+    __shared__ int s_nc, s_ne;
+    __shared__ uint64_t s_lists[kSettleWaves * 64];
+    __shared__ uint64_t s_top[64];
+    const int sh = blockIdx.x, q = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int t = lane & (L - 1), gr = lane / L;
+    const int k = p.k, sim = p.sim;
+    const int l0 = 4 * p.shard_tile_begin[sh], l1 = 4 * p.shard_tile_begin[sh + 1];
+    const uint32_t* __restrict__ lm = p.list_lbmax + (size_t)q * p.n_lists;
+    // (a) bucket maxima: thread t takes lists l0 + t + 256j (bucket t mod 64, four threads per bucket)
+    uint32_t mx = 0u;
+    for (int l = l0 + tid; l < l1; l += kSettleThreads) mx = max(mx, lm[l]);
+    s_bm[wave][lane] = mx;
+    const float4* __restrict__ Q = reinterpret_cast<const float4*>(p.q) + (size_t)q * UP;
+    float4 qf[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) qf[j] = Q[t + j * L];
+    const float qn = (!L2K && sim == SIM_COSINE) ? p.qnorm[q] : 0.0f;
+    __syncthreads();
+    if (tid < 64) {
+        const uint32_t m = max(max(s_bm[0][tid], s_bm[1][tid]), max(s_bm[2][tid], s_bm[3][tid]));
+        s_keys[tid] = ((uint64_t)m << 32) | (uint32_t)tid;   // distinct
+    }
+    __syncthreads();
+    if (tid < 64) {
+        const uint64_t mkey = s_keys[tid];
+        int rank = 0;
+        for (int j = 0; j < 64; ++j) rank += s_keys[j] > mkey;
+        if (rank == k - 1) s_L = (uint32_t)(mkey >> 32);   // (0 when fewer than k lists hold rows)
+        if (tid == 0 && k > 64) s_L = 0u;
+    }
+    if (tid == 0) {
+        s_nc = 0;
+        s_ne = 0;
+    }
+    __syncthreads();
+    const uint32_t Lb = s_L;
+    uint64_t lk = 0ull, thr = 0ull;   // this wave's top k of re-scored rows
+    unsigned long long n_res = 0, n_exact = 0;
+    auto rescore = [&](uint32_t vrow, bool valid) {
+        int sg = 0;
+        for (int j = 1; j < p.n_segs; ++j)
+            if ((int64_t)vrow >= p.seg_vrow[j]) sg = j;
+        const SegDev seg = p.segs[sg];
+        const int64_t ord = (int64_t)vrow - p.seg_vrow[sg];
+        const int32_t doc = valid ? (seg.ord_to_doc ? seg.ord_to_doc[ord] : (int32_t)ord) : 0;
+        const float xn = (!L2K && sim == SIM_COSINE && valid) ? seg.xnorm_f[ord] : 0.0f;
+        const float sc = settle_exact<L, V, L2K>(static_cast<const float4*>(seg.rows) + ord * p.units, valid,
+                                                 p.units, t, qf, sim, qn, xn);
+        wave_offer(valid ? make_key(sc, (uint32_t)(seg.doc_base + doc)) : 0ull, t == 0, lk, thr, lane, k);
+    };
+    for (int c0 = l0; c0 < l1; c0 += kWideChunk) {
+        const int c1 = min(c0 + kWideChunk, l1);
+        // (b) 4 lists per wave-iteration, 16 lanes each: entry e = lane & 15 of list c0 + 4i + (lane >> 4)
+        for (int i = wave; 4 * i < c1 - c0; i += kSettleWaves) {
+            const int l = c0 + 4 * i + (lane >> 4), e = lane & 15;
+            const bool in = l < c1;
+            const bool rows = in && lm[in ? l : c0] != 0u;   // an empty list has best lb 0: keys not read
+            const uint64_t key = rows ? p.cand[((size_t)q * p.n_lists + l) * kKQ + e] : 0ull;
+            const bool reach = key && (uint32_t)(key >> 32) >= Lb;
+            const uint64_t full = __ballot(reach && e == kKQ - 1);   // the list's 16th key reaches L
+            const bool exact = (full >> (lane | 15)) & 1ull;
+            if (reach && e == kKQ - 1) s_exact[atomicAdd(&s_ne, 1)] = l;
+            if (reach && !exact) s_cand[atomicAdd(&s_nc, 1)] = 0xFFFFFFFFu - (uint32_t)key;
+        }
+        __syncthreads();
+        const int nc = s_nc, ne = s_ne;
+        n_res += nc;
+        n_exact += ne;
+        for (int i0 = wave * R; i0 < nc; i0 += kSettleWaves * R) {
+            const int ci = i0 + gr;
+            rescore(s_cand[ci < nc ? ci : 0], ci < nc);
+        }
+        // (b') lists that may have dropped a qualifying row: every row of the scan quarter, exactly
+        for (int x = 0; x < ne; ++x) {
+            const int list = s_exact[x];
+            const TileDev td = p.tiles[list >> 2];
+            const SegDev seg = p.segs[td.seg];
+            const int64_t trows = td.row_end - td.row_begin;
+            const int64_t spw = ((trows + 4 * p.scan_R - 1) / (4 * p.scan_R)) * p.scan_R;
+            const int64_t lb0 = min(td.row_begin + (list & 3) * spw, td.row_end);
+            const int64_t lb1 = min(lb0 + spw, td.row_end);
+            const int64_t per_wave = ((lb1 - lb0 + kSettleWaves * R - 1) / (kSettleWaves * R)) * R;
+            const int64_t wb = lb0 + wave * per_wave, we = min(wb + per_wave, lb1);
+            const float4* X = static_cast<const float4*>(seg.rows);
+            for (int64_t r0 = wb; r0 < we; r0 += R) {
+                const int64_t row = r0 + gr;
+                const bool valid = row < we;
+                const int32_t doc = valid ? (seg.ord_to_doc ? seg.ord_to_doc[row] : (int32_t)row) : 0;
+                const float xn = (!L2K && sim == SIM_COSINE && valid) ? seg.xnorm_f[row] : 0.0f;
+                const float sc = settle_exact<L, V, L2K>(X + (valid ? row : 0) * p.units, valid, p.units, t, qf, sim, qn, xn);
+                wave_offer(valid ? make_key(sc, (uint32_t)(seg.doc_base + doc)) : 0ull, t == 0, lk, thr, lane, k);
+            }
+        }
+        __syncthreads();   // every wave is done with this chunk's candidates before the counters reset
+        if (tid == 0) {
+            s_nc = 0;
+            s_ne = 0;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        if (n_exact) {
+            if (atomicOr(&p.flags[q], 1) == 0) atomicAdd(&p.counters[0], 1ull);
+            atomicAdd(&p.counters[2], n_exact);
+        }
+        if (n_res) atomicAdd(&p.counters[1], n_res);
+    }
+    // (c) the shard's top k
+    s_lists[wave * 64 + lane] = lane < k ? lk : 0ull;
+    if (tid < 64) s_top[tid] = 0ull;
+    __syncthreads();
+    block_rank_topk<kSettleWaves>(s_lists, k, tid, s_top);
+    __syncthreads();
+    if (wave == 0) {
+        const uint64_t key = lane < k ? s_top[lane] : 0ull;
+        const size_t o = (size_t)q * p.n_shards + sh;
+        if (lane < k) p.shard_keys[o * k + lane] = key;
+        const int cnt = __popcll(__ballot(key != 0ull));
+        if (lane == 0) p.shard_counts[o] = cnt;
+    }
+}
+
 using SettleFn = void (*)(SettleParams);
 #define OSK_SETTLE_ROW(L, V) {sq8_settle<L, V, false>, sq8_settle<L, V, true>}
 static const SettleFn kSettle[9][2] = {OSK_SETTLE_ROW(4, 2),  OSK_SETTLE_ROW(8, 2),  OSK_SETTLE_ROW(8, 4),
                                        OSK_SETTLE_ROW(16, 4), OSK_SETTLE_ROW(16, 8), OSK_SETTLE_ROW(16, 12),
                                        OSK_SETTLE_ROW(32, 8), OSK_SETTLE_ROW(64, 8), OSK_SETTLE_ROW(64, 16)};
+
+static const SettleFn kSettleWide[9][2] = {
+    {sq8_settle_wide<4, 2, false>, sq8_settle_wide<4, 2, true>},    {sq8_settle_wide<8, 2, false>, sq8_settle_wide<8, 2, true>},
+    {sq8_settle_wide<8, 4, false>, sq8_settle_wide<8, 4, true>},    {sq8_settle_wide<16, 4, false>, sq8_settle_wide<16, 4, true>},
+    {sq8_settle_wide<16, 8, false>, sq8_settle_wide<16, 8, true>},  {sq8_settle_wide<16, 12, false>, sq8_settle_wide<16, 12, true>},
+    {sq8_settle_wide<32, 8, false>, sq8_settle_wide<32, 8, true>},  {sq8_settle_wide<64, 8, false>, sq8_settle_wide<64, 8, true>},
+    {sq8_settle_wide<64, 16, false>, sq8_settle_wide<64, 16, true>}};
+
+hipError_t launch_sq8_settle_wide(int cfg, int nq, const SettleParams& p, hipStream_t s) {
+    if (p.accept || p.gtiles || !p.shard_tile_begin || p.k < 1 || p.k > 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(kSettleWide[cfg][p.sim == SIM_EUCLIDEAN ? 1 : 0], dim3(p.n_shards, nq), dim3(kSettleThreads), 0,
+                       s, p);
+    return hipGetLastError();
+}
 
 hipError_t launch_sq8_settle(int cfg, int nq, const SettleParams& p, hipStream_t s) {
     hipLaunchKernelGGL(kSettle[cfg][p.sim == SIM_EUCLIDEAN ? 1 : 0], dim3(p.n_slices, nq), dim3(kSettleThreads), 0, s,

@@ -6,7 +6,8 @@ the same tie order — which the oracle's ORDER_DEVICE restatement pins.  These 
 two paths (tune "sq8" 1 vs 0) and the oracle over similarities, ragged dims, batch sizes, k,
 filters, sparse doc maps, multi-segment multi-shard views, heavy ties and adversarial data where
 the certificate cannot exclude a whole tile and the settle re-scans that tile exactly instead.
-Every test runs four times: batches scanned by the int8 MFMA kernel (sq8_mfma, tune "sq8_mfma_min"
+Every test runs five times: batches scanned by the wide int8 MFMA kernel (sq8_wide, 256 queries per launch),
+by the int8 MFMA kernel (sq8_mfma, tune "sq8_mfma_min"
 2, the default) with 32 and with 16 queries per launch (rows ≤ 256 dims streamed by the LDS-DMA ring,
 the default), with 32 queries and register row loads ("sq8_mfma_ring" 0), and by the VALU kernel
 (sq8_scan, "sq8_mfma_min" 0).
@@ -23,17 +24,21 @@ SIMS = [LU.VectorSimilarityFunction(s) for s in range(4)]
 COS = LU.VectorSimilarityFunction.COSINE
 
 
-@pytest.fixture(autouse=True, params=["mfma32", "mfma16", "mfma32reg", "valu"])
+@pytest.fixture(autouse=True, params=["mfma32", "mfma16", "mfma32reg", "valu", "wide"])
 def scan_kernel(request):
     """The int8 scan kernel of batched prefilter searches (single queries always take sq8_scan):
-    sq8_mfma with 32 or 16 queries per launch (LDS-DMA ring), with register row loads, or sq8_scan."""
+    sq8_mfma with 32 or 16 queries per launch (LDS-DMA ring), with register row loads, sq8_scan, or the
+    wide kernel (osk_sq8w.hip, 256 queries per launch; unfiltered batches of rows ≤ 256 dims, the others
+    fall back to sq8_mfma)."""
     _lib.tune("sq8_mfma_min", 0 if request.param == "valu" else 2)
     _lib.tune("sq8_mfma_queries", 16 if request.param == "mfma16" else 32)
     _lib.tune("sq8_mfma_ring", 0 if request.param == "mfma32reg" else -1)
+    _lib.tune("sq8_wide_min", 2 if request.param == "wide" else 0)
     yield request.param
     _lib.tune("sq8_mfma_min", 2)
     _lib.tune("sq8_mfma_queries", 32)
     _lib.tune("sq8_mfma_ring", -1)
+    _lib.tune("sq8_wide_min", 0)
 
 
 def corpus(n, dim, sim, seed):

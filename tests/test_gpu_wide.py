@@ -1,0 +1,192 @@
+"""GPU parity of the wide int8 MFMA prefilter (osk_sq8w.hip, 256 queries per launch).
+
+Large unfiltered batches of float32 rows of ≤ 256 dims read the int8 corpus once per 256 queries.  Its
+quick test is relaxed to per-step row maxima and its lists are per (quarter, query), so every result must
+still equal the fp32 streaming scan (tune "sq8" 0), sq8_mfma (tune "sq8_wide_min" 0) and the oracle's
+device-order exactSearch + TopDocs.merge bit for bit: docs, score bits, tie order, shard indices.
+Covered: every similarity, dims 1…256 (KS = 2 and 4), batches that are not multiples of 16, 64 or 256
+(partial query blocks, idle waves, several launches), k 1…12, ragged multi-segment multi-shard views with
+partial 16-row groups and 1-row segments, heavy ties, zero and constant rows, a zero query, and the
+pilot floor on data where most rows tie.
+"""
+import numpy as np
+import pytest
+
+from opensearch_amd import _lib, lucene as LU
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SIMS = [LU.VectorSimilarityFunction(s) for s in range(4)]
+
+
+def corpus(n, dim, sim, seed):
+    dist = {0: 1, 1: 3, 2: 3, 3: 2}[int(sim)]
+    return O.synth(0, n, dim, seed, dist)
+
+
+def bits(a):
+    return np.asarray(a, np.float32).view(np.uint32)
+
+
+def assert_same(a, b):
+    for x, y in zip(a, b):
+        x, y = np.asarray(x), np.asarray(y)
+        if x.dtype == np.float32:
+            assert np.array_equal(bits(x), bits(y)), (x, y)
+        else:
+            assert np.array_equal(x, y), (x, y)
+
+
+def tuned(key, value, default, fn):
+    _lib.tune(key, value)
+    try:
+        return fn()
+    finally:
+        _lib.tune(key, default)
+
+
+def view_of(rows_list, sim, shard_of, shard_index=None):
+    n_shards = max(shard_of) + 1
+    leaves = [[] for _ in range(n_shards)]
+    readers, bases = [], [0] * n_shards
+    for rows, s in zip(rows_list, shard_of):
+        r = LU.GpuFlatVectorsReader("v", rows, sim)
+        readers.append(r)
+        leaves[s].append(LU.LeafReaderContext(len(leaves[s]), bases[s], r))
+        bases[s] += len(rows)
+    return LU.DeviceShardSet(leaves, shard_index), readers
+
+
+def close_all(ds, readers):
+    ds.close()
+    for r in readers:
+        r.close()
+
+
+def three_ways(ds, queries, k, from_=0, size=None):
+    """wide vs sq8_mfma vs fp32 scan; returns the wide result and checks the wide kernel ran."""
+    size = size or k
+    w0 = ds.counter("sq8_wide_calls")
+    wide = ds.search(queries, k, from_, size)
+    assert ds.counter("sq8_wide_calls") == w0 + 1
+    narrow = tuned("sq8_wide_min", 0, WIDE_MIN, lambda: ds.search(queries, k, from_, size))
+    fp32 = tuned("sq8", 0, 1, lambda: ds.search(queries, k, from_, size))
+    assert_same(wide, narrow)
+    assert_same(wide, fp32)
+    return wide
+
+
+def oracle_merge(rows_list, shard_of, shard_index, q, k, sim):
+    n_shards = max(shard_of) + 1
+    lists = []
+    for s in range(n_shards):
+        segs = [i for i, t in enumerate(shard_of) if t == s]
+        rows = np.concatenate([rows_list[i] for i in segs])
+        lists.append(O.exact_search(rows, q, k, int(sim))[:2])
+    return O.topdocs_merge(lists, 0, k, shard_index)
+
+
+WIDE_MIN = 48   # the batches these tests send to the wide kernel
+
+
+@pytest.fixture(autouse=True)
+def defaults():
+    _lib.tune("sq8_wide_min", WIDE_MIN)
+    yield
+    _lib.tune("sq8_wide_min", 0)
+
+
+@pytest.mark.parametrize("dim", [1, 17, 64, 96, 100, 128, 129, 200, 256])
+@pytest.mark.parametrize("sim", SIMS, ids=lambda s: s.name)
+def test_wide_equals_mfma_scan_and_oracle(dim, sim):
+    sizes = [7001, 1, 2999, 16, 4100]
+    rows_list = [corpus(n, dim, sim, 10 + i) for i, n in enumerate(sizes)]
+    shard_of, shard_index = [0, 0, 1, 2, 2], [2, 0, 1]
+    queries = corpus(77, dim, sim, 20)
+    ds, readers = view_of(rows_list, sim, shard_of, shard_index)
+    try:
+        s, d, sh, c, _, _ = three_ways(ds, queries, 10)
+        for i in range(0, 77, 19):
+            es, ed, esh, _, _ = oracle_merge(rows_list, shard_of, shard_index, queries[i], 10, sim)
+            assert np.array_equal(d[i, :c[i]], ed) and np.array_equal(sh[i, :c[i]], esh)
+            assert np.array_equal(bits(s[i, :c[i]]), bits(es))
+    finally:
+        close_all(ds, readers)
+
+
+@pytest.mark.parametrize("nq", [48, 63, 64, 65, 200, 256, 257, 520])
+def test_wide_batch_shapes(nq):
+    """Partial 16-query blocks, waves with no query, several launches of 256."""
+    sim = LU.VectorSimilarityFunction.DOT_PRODUCT
+    rows_list = [corpus(n, 96, sim, 30 + i) for i, n in enumerate([12000, 5003])]
+    queries = corpus(nq, 96, sim, 40)
+    ds, readers = view_of(rows_list, sim, [0, 1])
+    try:
+        three_ways(ds, queries, 10)
+    finally:
+        close_all(ds, readers)
+
+
+@pytest.mark.parametrize("k", [1, 5, 12])
+@pytest.mark.parametrize("sim", SIMS, ids=lambda s: s.name)
+def test_wide_k_and_from_size(k, sim):
+    rows_list = [corpus(n, 128, sim, 50 + i) for i, n in enumerate([9000, 3000, 6001])]
+    queries = corpus(100, 128, sim, 60)
+    ds, readers = view_of(rows_list, sim, [0, 1, 1], [1, 0])
+    try:
+        three_ways(ds, queries, k, 0, k)
+        if k > 2:
+            three_ways(ds, queries, k, 2, k - 2)
+    finally:
+        close_all(ds, readers)
+
+
+@pytest.mark.parametrize("sim", SIMS, ids=lambda s: s.name)
+def test_wide_ties_zero_rows_and_zero_query(sim):
+    """Duplicated rows (exact ties broken by doc), zero and constant rows, and a zero query: the relaxed
+    quick test passes every pair of a zero query or a zero row, the precise bound decides."""
+    rng = np.random.default_rng(3)
+    base = corpus(400, 64, sim, 70)
+    rows = base[rng.integers(0, 400, 6000)].copy()
+    rows[::97] = 0.0
+    rows[5::101] = 0.25
+    queries = corpus(80, 64, sim, 71)
+    queries[3] = 0.0
+    queries[40] = rows[10]
+    ds, readers = view_of([rows[:3500], rows[3500:]], sim, [0, 1])
+    try:
+        three_ways(ds, queries, 10)
+    finally:
+        close_all(ds, readers)
+
+
+def test_wide_many_tiles_at_size():
+    """A device-generated 3.2M × 96 DOT view over 4 shards (thousands of quarters): the wide path (one
+    launch of 256 after its pilot) equals sq8_mfma and the oracle on a sample of queries."""
+    sim, rps, dim = LU.VectorSimilarityFunction.DOT_PRODUCT, 800_000, 96
+    readers = [LU.GpuFlatVectorsReader.synthetic("v", rps, dim, sim, seed=91, dist=_lib.DIST_NORMALISH_UNIT,
+                                                 row0=s * rps) for s in range(4)]
+    ds = LU.DeviceShardSet([[LU.LeafReaderContext(0, 0, r)] for r in readers], [3, 1, 0, 2])
+    try:
+        q = O.synth(0, 256, dim, 92, _lib.DIST_NORMALISH_UNIT)
+        w0 = ds.counter("sq8_wide_calls")
+        out = ds.search(q, 10, 0, 10)
+        assert ds.counter("sq8_wide_calls") == w0 + 1
+        assert ds.counter("sq8_fallback_queries") == 0
+        assert_same(out, tuned("sq8_wide_min", 0, WIDE_MIN, lambda: ds.search(q, 10, 0, 10)))
+        samp = [0, 77, 200, 255]
+        lists = [[] for _ in samp]
+        for s in range(4):
+            rows = O.synth(s * rps, rps, dim, 91, _lib.DIST_NORMALISH_UNIT)
+            sc, dc, cc = O.knn_batch(rows, q[samp], 10, int(sim), O.ORDER_DEVICE, 16)
+            for j in range(len(samp)):
+                lists[j].append((sc[j, :cc[j]], dc[j, :cc[j]]))
+        for j, i in enumerate(samp):
+            es, ed, esh, _, _ = O.topdocs_merge(lists[j], 0, 10, [3, 1, 0, 2])
+            assert np.array_equal(out[1][i], ed) and np.array_equal(out[2][i], esh)
+            assert np.array_equal(bits(out[0][i]), bits(es))
+    finally:
+        ds.close()
+        for r in readers:
+            r.close()

@@ -147,11 +147,18 @@ def run_slots(view, queries, batch, steps, warmup, accept_ptrs, k, slots):
     return dt / steps * 1e3, tot / max(1, n)
 
 
+PATH_COUNTERS = ("sq8_calls", "sq8_wide_calls", "sq6_calls", "mfma_calls", "select_calls")
+PATH = {}
+
+
 def run(view, queries, batch, steps, warmup, accept_ptrs=None, k=10):
     """(ms per batch with INFLIGHT queries in flight, the scan's isolated mean launch duration)."""
+    before = {c: counter(view, c) for c in PATH_COUNTERS}
     ms, km = run_slots(view, queries, batch, steps, warmup, accept_ptrs, k, INFLIGHT)
     global HOST_ISSUE
     HOST_ISSUE = HOST_MS
+    PATH.clear()
+    PATH.update({c: counter(view, c) - before[c] for c in PATH_COUNTERS if counter(view, c) != before[c]})
     if INFLIGHT > 1:   # overlapped launches share HBM: the kernel's own duration from a one-in-flight pass
         _, km = run_slots(view, queries, batch, max(3, steps // 2), 2, accept_ptrs, k, 1)
     return ms, km
@@ -170,7 +177,8 @@ def emit(name, view, batch, ms_step, kernel_ms, bytes_per_launch, extra=None):
     rec = {"config": name, "batch": batch, "inflight": INFLIGHT, "qps": batch / (ms_step * 1e-3),
            "ms_per_batch": ms_step, "host_issue_ms_per_batch": HOST_ISSUE,
            "kernel_ms": kernel_ms, "fp32_equiv_GBps": bytes_per_launch / (kernel_ms * 1e-3) / 1e9,
-           "rows": view.n_shards * view.rows, "dim": view.dim, "shards": view.n_shards}
+           "rows": view.n_shards * view.rows, "dim": view.dim, "shards": view.n_shards,
+           "path_calls": dict(PATH)}
     rows = view.n_shards * view.rows
     if view.enc == _lib.FLOAT32 and batch < 96 and not (extra or {}).get("selectivity"):
         # the certified int8 prefilter's own bytes: int8 rows (16-B units) + 16-B bound terms, read

@@ -46,6 +46,61 @@ __global__ __launch_bounds__(256) void read_stream(const int4* __restrict__ src,
     if (x == 0x12345678) sink[threadIdx.x] = x;   // practically never: keeps the loads live
 }
 
+// The 6-bit tier's load shape (osk_sq6.hip): blocks of 1536 B read as one 16-B-per-lane instruction (1 KiB)
+// and one 8-B-per-lane instruction (512 B), U blocks per wave-iteration, non-temporal — against the pure
+// 16-B stream, to tell whether the 8-B half of the pattern costs bandwidth.
+template <int U>
+__global__ __launch_bounds__(256) void read_mixed(const char* __restrict__ src, int64_t n_blocks, int64_t chunk,
+                                                  int* __restrict__ sink) {
+    typedef int i4v __attribute__((ext_vector_type(4)));
+    typedef int i2v __attribute__((ext_vector_type(2)));
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t begin = (int64_t)blockIdx.x * chunk;
+    const int64_t end = begin + chunk < n_blocks ? begin + chunk : n_blocks;
+    i4v acc = {0, 0, 0, 0};
+    for (int64_t b = begin + wave; b < end; b += (int64_t)4 * U) {
+        i4v h[U];
+        i2v l[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t j = b + (int64_t)u * 4;
+            const int64_t jj = j < end ? j : begin;
+            const char* blk = src + jj * 1536;
+            h[u] = __builtin_nontemporal_load(reinterpret_cast<const i4v*>(blk) + lane);
+            l[u] = __builtin_nontemporal_load(reinterpret_cast<const i2v*>(blk + 1024) + lane);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            acc ^= h[u];
+            acc.x ^= l[u].x;
+            acc.y ^= l[u].y;
+        }
+    }
+    const int x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+    if (x == 0x12345678) sink[threadIdx.x] = x;
+}
+
+template <int U>
+double run_mixed(const char* src, int64_t bytes, int blocks, int* sink, int reps) {
+    const int64_t n_blocks = bytes / 1536;
+    const int64_t chunk = (n_blocks + blocks - 1) / blocks;
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    hipLaunchKernelGGL((read_mixed<U>), dim3(blocks), dim3(256), 0, 0, src, n_blocks, chunk, sink);
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(a, 0));
+    for (int r = 0; r < reps; ++r)
+        hipLaunchKernelGGL((read_mixed<U>), dim3(blocks), dim3(256), 0, 0, src, n_blocks, chunk, sink);
+    CHECK(hipEventRecord(b, 0));
+    CHECK(hipEventSynchronize(b));
+    float ms = 0.f;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    CHECK(hipEventDestroy(a));
+    CHECK(hipEventDestroy(b));
+    return (double)n_blocks * 1536.0 * reps / (ms * 1e-3) / 1e12;   // TB/s
+}
+
 template <int U, bool NT>
 double run(const int4* src, int64_t n_units, int blocks, int* sink, int reps) {
     const int64_t chunk = (n_units + blocks - 1) / blocks;
@@ -90,6 +145,19 @@ int main(int argc, char** argv) {
         for (int i = 0; i < 6; ++i) {
             std::printf("%s {\"blocks_per_cu\": %d, \"loads_in_flight\": %d, \"nt\": %s, \"TBps\": %.3f}", first ? "" : ",\n",
                         per_cu, us[i % 3], i >= 3 ? "true" : "false", r[i]);
+            first = false;
+        }
+    }
+    std::printf("\n], \"mixed_16B_8B\": [\n");
+    first = true;
+    for (int per_cu : {4, 8}) {
+        const int blocks = cus * per_cu;
+        const double r[3] = {run_mixed<2>(reinterpret_cast<const char*>(src), n_units * 16, blocks, sink, reps),
+                             run_mixed<3>(reinterpret_cast<const char*>(src), n_units * 16, blocks, sink, reps),
+                             run_mixed<4>(reinterpret_cast<const char*>(src), n_units * 16, blocks, sink, reps)};
+        for (int i = 0; i < 3; ++i) {
+            std::printf("%s {\"blocks_per_cu\": %d, \"blocks_in_flight_per_wave\": %d, \"TBps\": %.3f}",
+                        first ? "" : ",\n", per_cu, i + 2, r[i]);
             first = false;
         }
     }

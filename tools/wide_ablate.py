@@ -1,0 +1,66 @@
+"""A/B timing of the wide int8 MFMA prefilter (osk_sq8w.hip) and its insertion-event counts.
+
+    python tools/wide_ablate.py [C4|C2|C3] [batch]      (ABLATE="0,1,2,3" sq8_mfma_ablate values)
+
+C4: 8 × 12.5M × 96 DOT_PRODUCT unit rows; C2: 1 × 1M × 128 EUCLIDEAN U[0,1)·128.  Runs on the testing build
+(ablations; the kernel's event counters).  Reports per search: pilot + merge + main pass time
+(osk_view_scan_time), insertion events (queries with a passing pair per 16-row group and wave) and
+quick-test passes (pairs), each also per (query, quarter)."""
+import os
+os.environ.setdefault("OSK_TESTING_LIB", "1")
+import ctypes as C
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from opensearch_amd import _lib, distributed as D  # noqa: E402
+from opensearch_amd._lib import check, lib  # noqa: E402
+from opensearch_amd.lucene import synth_host  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "C4"
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+K = 10
+NS, RPS, DIM, SIM, DIST = {"C4": (8, 12_500_000, 96, _lib.DOT_PRODUCT, _lib.DIST_NORMALISH_UNIT),
+                           "C2": (1, 1_000_000, 128, _lib.EUCLIDEAN, _lib.DIST_UNIFORM01_X128),
+                           "C3": (8, 1_250_000, 768, _lib.COSINE, _lib.DIST_NORMALISH_UNIT)}[cfg]
+_lib.tune("sq8_wide_min", 2)   # (the wide path is opt-in while it is tuned)
+for kv in filter(None, os.environ.get("TUNE", "").split(",")):
+    _lib.tune(kv.split("=")[0], int(kv.split("=")[1]))
+torch.cuda.set_device(0)
+s = torch.cuda.Stream()
+torch.cuda.set_stream(s)
+st = s.cuda_stream
+shards = D.LocalShards(0, 1, NS, RPS, DIM, SIM, _lib.FLOAT32, 42, DIST, 0)
+q = torch.from_numpy(synth_host(0, B, DIM, 43, DIST)).cuda()
+kk = torch.empty((B, NS, K), dtype=torch.int64, device="cuda")
+cc = torch.empty((B, NS), dtype=torch.int32, device="cuda")
+
+
+def counter(name):
+    v = C.c_int64()
+    check(lib().osk_view_counter(shards.view, name.encode(), C.byref(v)))
+    return v.value
+
+
+tiles = C.c_int64()
+for ab in [int(x) for x in os.environ.get("ABLATE", "0,1,2,3").split(",")]:
+    _lib.tune("sq8_mfma_ablate", ab)
+    for _ in range(2):
+        shards.search(q.data_ptr(), B, K, kk, cc, st)
+    torch.cuda.synchronize()
+    e0, p0, w0 = counter("sq8_wide_events"), counter("sq8_wide_pairs"), counter("sq8_wide_calls")
+    check(lib().osk_view_profile(shards.view, 1))
+    n = 5
+    for _ in range(n):
+        shards.search(q.data_ptr(), B, K, kk, cc, st)
+    torch.cuda.synchronize()
+    ms, calls = C.c_double(), C.c_int64()
+    check(lib().osk_view_scan_time(shards.view, C.byref(ms), C.byref(calls)))
+    check(lib().osk_view_profile(shards.view, 0))
+    ev, pr, wc = counter("sq8_wide_events") - e0, counter("sq8_wide_pairs") - p0, counter("sq8_wide_calls") - w0
+    launches = max(1, wc) * ((B + 255) // 256)
+    print(f"{cfg} b{B} ablate={ab}: {ms.value / max(1, calls.value):.3f} ms per search (pilot+merge+main), "
+          f"wide calls {wc}/{n}, events/search {ev / n:.0f}, pairs/search {pr / n:.0f}", flush=True)
+_lib.tune("sq8_mfma_ablate", 0)
+shards.close()
