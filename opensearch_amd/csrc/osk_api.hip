@@ -150,7 +150,7 @@ osk_seg::~osk_seg() {
     if (d_q8) (void)hipFree(d_q8);
     if (d_q8aux) (void)hipFree(d_q8aux);
     if (d_q8t) (void)hipFree(d_q8t);
-    if (d_q8bmax) (void)hipFree(d_q8bmax);
+    if (d_q8auxt) (void)hipFree(d_q8auxt);
     if (d_q6) (void)hipFree(d_q6);
     if (d_q6aux) (void)hipFree(d_q6aux);
 }
@@ -164,7 +164,7 @@ int64_t osk_seg::hbm_bytes() const {
     if (d_split) b += std::max<int64_t>(1, (n_rows + 127) / 128) * 8 * split_KS * 2 * 1024 + n * 4 + 4;
     if (d_q8) b += n * units8 * 16 + n * 16;
     if (d_q8t) b += std::max<int64_t>(1, (n_rows + 15) / 16) * sq8_mfma_ks(units8) * 1024;
-    if (d_q8bmax) b += std::max<int64_t>(1, (n_rows + 15) / 16) * 16;
+    if (d_q8auxt) b += std::max<int64_t>(1, (n_rows + 15) / 16) * kAuxGroupF4 * 16;
     if (d_q6) b += sq6_bytes(n_rows, dim);
     return b;
 }
@@ -304,6 +304,8 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         {"sq8_mfma_queries", &g_tuning.sq8_mfma_queries, 16, 32, false},
         {"sq8_mfma_min", &g_tuning.sq8_mfma_min, 0, 1 << 20, false},
         {"sq8_wide_min", &g_tuning.sq8_wide_min, 0, 1 << 20, false},
+        {"sq8_wide_force", &g_tuning.sq8_wide_force, 0, 1, false},
+        {"sq8_wide_phase", &g_tuning.sq8_wide_phase, 0, 1 << 16, false},
         {"sq8_mfma_ring", &g_tuning.sq8_mfma_ring, -1, 8, false},
         {"i8_stream", &g_tuning.i8_stream, 0, 1, false},
         {"call_timing", &g_tuning.call_timing, 0, 1, false},
@@ -697,8 +699,8 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
     OSK_HIP(v->d_tile_coff.reserve(sizeof(int32_t) * tile_coff.size()));
     OSK_HIP(v->d_tile_order.reserve(sizeof(int32_t) * tile_order.size()));
     OSK_HIP(v->d_seg_vrow.reserve(sizeof(int64_t) * n_segs));
-    OSK_HIP(v->d_counters.reserve(sizeof(unsigned long long) * 8));
-    OSK_HIP(hipMemsetAsync(v->d_counters.p, 0, sizeof(unsigned long long) * 8, st));
+    OSK_HIP(v->d_counters.reserve(sizeof(unsigned long long) * 16));
+    OSK_HIP(hipMemsetAsync(v->d_counters.p, 0, sizeof(unsigned long long) * 16, st));
     OSK_HIP(hipMemcpyAsync(v->d_seg_vrow.p, vrow.data(), sizeof(int64_t) * n_segs, hipMemcpyHostToDevice, st));
     OSK_HIP(hipMemcpyAsync(v->d_segs.p, sd.data(), sizeof(SegDev) * n_segs, hipMemcpyHostToDevice, st));
     if (!tiles.empty())
@@ -1092,8 +1094,9 @@ int32_t ensure_sq8_seg(osk_seg* s, hipStream_t st) {
 }
 
 // The segment's int8 copy in sq8_mfma's tiled layout: blocks of 16 rows, per 64-dim k-step one
-// contiguous 1 KiB slab (row r of the block at r·64 B), so each of the scan's load instructions
-// reads 1 KiB contiguous.  Built once, from the row-major int8 copy.
+// contiguous 1 KiB slab (chunk-major: 16-dim chunk c of row r at c·256 + r·16 B), so each of the scan's
+// load instructions reads 1 KiB contiguous and a 32-dim tail is the slab's first 512 B.  Built once, from
+// the row-major int8 copy.
 int32_t ensure_sq8t_seg(osk_seg* s, hipStream_t st) {
     std::lock_guard<std::mutex> lk(s->mu);
     if (s->d_q8t) return OSK_OK;
@@ -1107,41 +1110,46 @@ int32_t ensure_sq8t_seg(osk_seg* s, hipStream_t st) {
         return OSK_ERR_OOM;
     }
     OSK_HIP(launch_sq8_tile(s->d_q8, s->n_rows, u8, ks, q8t, st));
-    float4* bmax = nullptr;   // the wide kernel's per-block maxima of the bound terms (16 B per 16 rows)
+    float4* auxt = nullptr;   // the wide kernel's tiled bound terms (352 B per 16 rows)
     if (sq8_wide_supported(u8)) {
-        e = hipMalloc(&bmax, (size_t)blocks * sizeof(float4));
+        e = hipMalloc(&auxt, (size_t)blocks * kAuxGroupF4 * sizeof(float4));
         if (e != hipSuccess) {
             (void)hipFree(q8t);
-            set_error(std::string("hipMalloc of the block maxima failed: ") + hipGetErrorString(e));
+            set_error(std::string("hipMalloc of the tiled bound terms failed: ") + hipGetErrorString(e));
             return OSK_ERR_OOM;
         }
-        OSK_HIP(launch_sq8_block_max(s->d_q8aux, s->n_rows, bmax, st));
+        OSK_HIP(launch_sq8_aux_tile(s->d_q8aux, s->sim == SIM_COSINE ? s->d_xnorm_f : nullptr, s->n_rows, auxt, st));
     }
     OSK_HIP(hipStreamSynchronize(st));
     s->d_q8t = q8t;
-    s->d_q8bmax = bmax;
+    s->d_q8auxt = auxt;
     return OSK_OK;
 }
 
 int32_t ensure_sq8t(osk_view* v, hipStream_t st) {
     if (v->sq8t_ready) return OSK_OK;
     const int ns = (int)v->segs.size();
-    std::vector<const void*> rows(ns), bmax(ns);
+    std::vector<const void*> rows(ns), auxt(ns);
     for (int i = 0; i < ns; ++i) {
         int32_t rc = ensure_sq8t_seg(v->segs[i], st);
         if (rc) return rc;
         rows[i] = v->segs[i]->d_q8t;
-        bmax[i] = v->segs[i]->d_q8bmax;
+        auxt[i] = v->segs[i]->d_q8auxt;
     }
     std::vector<int32_t> sqb(v->shard_tile_begin.size());
     for (size_t i = 0; i < sqb.size(); ++i) sqb[i] = 4 * v->shard_tile_begin[i];   // the wide kernel's quarters
     OSK_HIP(v->d_sq8_rows_t.reserve(sizeof(void*) * ns));
-    OSK_HIP(v->d_sq8_bmax.reserve(sizeof(void*) * ns));
+    OSK_HIP(v->d_sq8_auxt.reserve(sizeof(void*) * ns));
     OSK_HIP(v->d_shard_quarter_begin.reserve(sizeof(int32_t) * sqb.size()));
     OSK_HIP(hipMemcpyAsync(v->d_sq8_rows_t.p, rows.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
-    OSK_HIP(hipMemcpyAsync(v->d_sq8_bmax.p, bmax.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
+    OSK_HIP(hipMemcpyAsync(v->d_sq8_auxt.p, auxt.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
     OSK_HIP(hipMemcpyAsync(v->d_shard_quarter_begin.p, sqb.data(), sizeof(int32_t) * sqb.size(), hipMemcpyHostToDevice,
                            st));
+    if (sq8_wide_supported((v->segs.empty() ? 0 : v->segs[0]->units8)) && v->n_tiles > 0) {
+        OSK_HIP(v->d_quarter_bm.reserve(sizeof(float4) * 4 * (size_t)v->n_tiles));
+        OSK_HIP(launch_wide_quarter_max(v->d_tiles.as<TileDev>(), v->n_tiles, v->d_sq8_auxt.as<const float4*>(),
+                                        v->d_quarter_bm.as<float4>(), st));
+    }
     OSK_HIP(hipStreamSynchronize(st));
     v->sq8t_ready = true;
     return OSK_OK;
@@ -1313,6 +1321,29 @@ void fold_probe(osk_view* v) {
     }
 }
 
+// The prefilter's two int8 MFMA kernels, in µs for this view's R rows (measured end to end on MI355X,
+// DESIGN.md §3c): sq8_mfma per launch of ≤ 32 queries streams R·(int8 row + 16-B bound terms) at ≈ 4.3 TB/s
+// + ≈ 165 µs + 0.28 µs per dim (pilot, merge, settle, re-score); the wide kernel per launch of ≤ 256 queries
+// ≈ R·KS·0.0475 ns (it is issue-bound, not HBM-bound: C4 9.8 ms per 256) + ≈ 600 µs (pilot, two passes,
+// floors, settle: C2 0.58 ms per 256).
+double sq8_narrow_us(double R, int nq, int u8, int dim) {
+    return (double)((nq + 31) / 32) * (R * (16.0 * u8 + 16.0) / 4.3e6 + 165.0 + 0.28 * dim);
+}
+double sq8_wide_us(double R, int nq, int u8) {
+    return (double)((nq + kWideQ - 1) / kWideQ) * (R * (u8 <= 8 ? 2.0 : 4.0) * 0.0475e-3 + 600.0);
+}
+// the wide kernel takes an unfiltered batch of ≥ sq8_wide_min queries of ≤ 256 dims when the model has it
+// cheaper than sq8_mfma (C4: from about 96 queries)
+bool sq8_wide_pick(const osk_view* v, int nq, bool filtered) {
+    const int u8 = (v->dim + 15) / 16;
+    if (filtered || !sq8_wide_supported(u8) || g_tuning.sq8_wide_min <= 0 || nq < g_tuning.sq8_wide_min ||
+        g_tuning.sq8_mfma_min <= 0 || nq < g_tuning.sq8_mfma_min)
+        return false;
+    double R = 0.0;
+    for (const osk_seg* sg : v->segs) R += (double)sg->n_rows;
+    return g_tuning.sq8_wide_force || sq8_wide_us(R, nq, u8) <= sq8_narrow_us(R, nq, u8, v->dim);
+}
+
 // Certified int8 prefilter search (float32, k ≤ kKQ): int8 scan → settle per slice of tiles (exact
 // re-score of the rows the certificate cannot exclude; a tile whose list overflowed is re-scanned
 // exactly inside the settle) → per-shard merge.  Nothing waits on the host.
@@ -1328,8 +1359,7 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     // unfiltered query scans the 6-bit tier where the view has one.
     const bool use_mfma = g_tuning.sq8_mfma_min > 0 && nq >= g_tuning.sq8_mfma_min && sq8_mfma_supported(u8);
     // large unfiltered batches of ≤ 256-dim rows: one corpus pass per kWideQ queries (osk_sq8w.hip)
-    const bool use_wide = use_mfma && !d_accept && g_tuning.sq8_wide_min > 0 && nq >= g_tuning.sq8_wide_min &&
-                          sq8_wide_supported(u8);
+    const bool use_wide = use_mfma && sq8_wide_pick(v, nq, d_accept != nullptr);
     // the 6-bit tier: single unfiltered queries, every segment's calibration probing or on.  The shared
     // lock keeps a segment's copy alive from this check to the launches (fold_probe frees it under the
     // exclusive one after a device synchronisation)
@@ -1424,11 +1454,12 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
         rc = ensure_sq8t(v, st);
         if (rc) return rc;
         p.rows8t = v->d_sq8_rows_t.as<const int4*>();
-        p.bmax = v->d_sq8_bmax.as<const float4*>();
+        p.auxt = v->d_sq8_auxt.as<const float4*>();
         const size_t qmax = use_wide ? kWideQ : kMfmaQueries;
         OSK_HIP(v->ws_pilot.reserve(sizeof(uint64_t) * qmax * v->n_tiles * (use_wide ? 4 : 64)));
         OSK_HIP(v->ws_thr.reserve(sizeof(uint64_t) * qmax * S * 64));
         OSK_HIP(v->ws_thr_counts.reserve(sizeof(int32_t) * qmax * S));
+        if (use_wide) OSK_HIP(v->ws_wfloor.reserve(sizeof(uint32_t) * 2 * kWideQ * S));
     }
     for (int q0 = 0; q0 < nq; q0 += chunk) {
         p.q0 = q0;
@@ -1453,13 +1484,37 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             p.counters = v->d_counters.as<unsigned long long>();   // (testing build: event counts)
             p.pilot = 1;
             p.pilot_keys = v->ws_pilot.as<uint64_t>();
+            p.quarter_begin = 0;
+            p.quarter_end = 0;
+            p.floors = nullptr;
+            p.quarter_bm = v->d_quarter_bm.as<const float4>();
             OSK_HIP(launch_sq8_wide(p, st, e0, nullptr));
-            OSK_HIP(launch_merge_shards(v->ws_pilot.as<uint64_t>(), 4 * v->n_tiles,
-                                        v->d_shard_quarter_begin.as<int32_t>(), S, p.q_count, k,
+            const int nql = 4 * v->n_tiles;
+            const int32_t* sqb = v->d_shard_quarter_begin.as<int32_t>();
+            OSK_HIP(launch_merge_shards(v->ws_pilot.as<uint64_t>(), nql, sqb, S, p.q_count, k,
                                         v->ws_thr.as<uint64_t>(), v->ws_thr_counts.as<int32_t>(), st, 1));
+            uint32_t* floor_a = v->ws_wfloor.as<uint32_t>();
+            uint32_t* floor_b = floor_a + (size_t)kWideQ * S;
+            OSK_HIP(launch_wide_floor(nullptr, nql, sqb, S, p.q_count, k, v->ws_thr.as<uint64_t>(),
+                                      v->ws_thr_counts.as<int32_t>(), floor_a, st));
             p.pilot = 0;
-            p.thr_keys = v->ws_thr.as<uint64_t>();
-            p.thr_counts = v->ws_thr_counts.as<int32_t>();
+            p.floors = floor_a;
+            // two passes: the first 1/phase of the quarters (tile order: every shard) under the pilot's floors,
+            // then the rest under floors raised by the first pass's list maxima (the lists of the second pass
+            // read as empty until it writes them)
+            const int phase = g_tuning.sq8_wide_phase;
+            const int n_a = phase > 1 ? nql / phase : 0;
+            if (n_a > 0) {
+                uint32_t* lbm = p.list_lbmax + (size_t)q0 * nql;
+                OSK_HIP(hipMemsetAsync(lbm, 0, sizeof(uint32_t) * (size_t)p.q_count * nql, st));
+                p.quarter_end = n_a;
+                OSK_HIP(launch_sq8_wide(p, st, nullptr, nullptr));
+                OSK_HIP(launch_wide_floor(lbm, nql, sqb, S, p.q_count, k, v->ws_thr.as<uint64_t>(),
+                                          v->ws_thr_counts.as<int32_t>(), floor_b, st));
+                p.quarter_begin = n_a;
+                p.quarter_end = 0;
+                p.floors = floor_b;
+            }
             OSK_HIP(launch_sq8_wide(p, st, nullptr, e1));
         } else if (use_mfma) {
             // pilot: 16 sampled rows per wave → per (query, tile) the top k sampled lower bounds →
@@ -1742,8 +1797,7 @@ int32_t view_search_device(osk_view* v, const void* d_queries, int nq, int k,
     OSK_HIP(v->ws_q.reserve((size_t)nq_pad * UP * 16));
     OSK_HIP(v->ws_qnorm.reserve(sizeof(float) * nq_pad));
     // Path cost model, measured end to end on MI355X, in µs for this view's rows R:
-    //   int8 prefilter, per launch of ≤ 32 queries: R·(int8 row + 16-B bound terms) at ≈ 4.3 TB/s + ≈ 165 µs
-    //     + 0.28 µs per dim (pilot, pilot merge, settle and re-score: C3 2.2 ms, C4 2.7 ms, C2 0.20 ms per launch);
+    //   int8 prefilter: the cheaper of its kernels (sq8_narrow_us, sq8_wide_us);
     //   bf16×3, per block of ≤ 256 queries: R·(0.153 + 0.00119·dim) ns + ≈ 325 µs (C3 11.0, C4 27.1, C2 0.63 ms;
     //     fitted to those three, profiles/r02q/c2_batches_*.jsonl, c3_batches_*.jsonl).
     // 96-dim rows stay on the prefilter at any batch, 768-dim rows move to bf16×3 blocks from about 160
@@ -1753,15 +1807,11 @@ int32_t view_search_device(osk_view* v, const void* d_queries, int nq, int k,
     double R = 0.0;
     for (const osk_seg* sg : v->segs) R += (double)sg->n_rows;
     const int u8v = (v->dim + 15) / 16;
-    const bool wide_ok = sq8_wide_supported(u8v) && !d_accept && g_tuning.sq8_wide_min > 0 &&
-                         nq >= g_tuning.sq8_wide_min && g_tuning.sq8_mfma_min > 0 && nq >= g_tuning.sq8_mfma_min;
-    // the wide int8 MFMA kernel (osk_sq8w.hip), per launch of ≤ 256 queries: the tiled rows (64 B per 64-dim
-    // k-step), their 16-B bound terms and the block maxima at ≈ 5 TB/s, plus pilot, merges and settle
-    const double sq8_us =
-        wide_ok ? (double)((nq + kWideQ - 1) / kWideQ) * (R * (64.0 * sq8_mfma_ks(u8v) + 17.0) / 5.0e6 + 100.0)
-                : (double)((nq + 31) / 32) * (R * (16.0 * u8v + 16.0) / 4.3e6 + 165.0 + 0.28 * v->dim);
+    const double sq8_us = sq8_wide_pick(v, nq, d_accept != nullptr) ? sq8_wide_us(R, nq, u8v)
+                                                                      : sq8_narrow_us(R, nq, u8v, v->dim);
     const double bf_us = (double)((nq + 255) / 256) * (R * (0.153 + 0.00119 * v->dim) * 1e-3 + 325.0);
-    const bool blocks_cheaper = bf_us * 100.0 <= sq8_us * (double)g_tuning.sq8_cost_pct;
+    const bool blocks_cheaper = bf_us * 100.0 <= sq8_us * (double)g_tuning.sq8_cost_pct &&
+                                !(g_tuning.sq8_wide_force && sq8_wide_pick(v, nq, d_accept != nullptr));
     const bool batched = v->enc == ENC_FLOAT32 && g_tuning.mfma_min_batch > 0 &&
                          nq >= g_tuning.mfma_min_batch && k <= kKC - 4 && (!sq8_ok || blocks_cheaper);
     // k ≤ kKQ − 4: a tile list holds 4 more rows than k, so it rarely overflows past the certificate
@@ -1964,7 +2014,9 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
         return OSK_OK;
     }
     const bool dev = n == "sq8_fallback_queries" || n == "sq8_rescored_rows" || n == "sq8_exact_tiles" ||
-                     n == "sq6_rebound_rows" || n == "sq8_wide_events" || n == "sq8_wide_pairs";
+                     n == "sq6_rebound_rows" || n == "sq8_wide_events" || n == "sq8_wide_pairs" ||
+                     n == "sq8_wide_wait_cycles" || n == "sq8_wide_issue_cycles" || n == "sq8_wide_loop_cycles" ||
+                     n == "sq8_wide_quarter_cycles" || n == "sq8_wide_consts_cycles";
     OSK_REQUIRE(dev || n == "mfma_calls" || n == "mfma_fallback_queries" || n == "sq8_calls" || n == "sq6_calls" ||
                     n == "select_calls" || n == "sq8_wide_calls",
                 "unknown counter: " + n);
@@ -1974,13 +2026,16 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
         std::lock_guard<std::mutex> lk(s->mu);
         if (dev) {
             if (!s->d_counters.p) continue;
-            unsigned long long c[8];
+            unsigned long long c[16];
             OSK_HIP(hipDeviceSynchronize());   // the last search may be on any stream
             OSK_HIP(hipMemcpy(c, s->d_counters.p, sizeof(c), hipMemcpyDeviceToHost));
-            // [4], [5]: the wide kernel's insertion events and quick-test passes (testing build only)
+            // [4] … [8]: the wide kernel's insertion events, quick-test passes and wave 0's shader clocks in
+            // the step loop's wait / issue / whole loop (testing build only)
             sum += (int64_t)(n == "sq8_fallback_queries" ? c[0] : n == "sq8_rescored_rows" ? c[1]
                              : n == "sq8_exact_tiles" ? c[2] : n == "sq6_rebound_rows" ? c[3]
-                             : n == "sq8_wide_events" ? c[4] : c[5]);
+                             : n == "sq8_wide_events" ? c[4] : n == "sq8_wide_pairs" ? c[5]
+                             : n == "sq8_wide_wait_cycles" ? c[6] : n == "sq8_wide_issue_cycles" ? c[7]
+                             : n == "sq8_wide_loop_cycles" ? c[8] : n == "sq8_wide_quarter_cycles" ? c[9] : c[10]);
         } else {
             sum += n == "mfma_calls" ? s->mfma_calls : n == "mfma_fallback_queries" ? s->mfma_fallback_queries
                  : n == "sq8_calls" ? s->sq8_calls : n == "sq6_calls" ? s->sq6_calls

@@ -179,8 +179,11 @@ struct Sq8Params {
     uint32_t* cand6;                 // sq6_scan → sq6_rebound: per list, the rows that passed the 6-bit test
     int32_t* cnt6;                   // [q][n_lists] their count (> cap6: overflowed)
     int cap6;
-    const float4* const* bmax;       // sq8_wide: per segment, the 16-row block maxima (launch_sq8_block_max)
+    const float4* const* auxt;       // sq8_wide: per segment, the 16-row groups' bound terms (launch_sq8_aux_tile)
     int wide_grid;                   // sq8_wide: persistent workgroups (the device's CUs)
+    int quarter_begin, quarter_end;  // sq8_wide: the launch's quarters in tile order (end 0: all)
+    const uint32_t* floors;          // sq8_wide: [q_count][n_shards] floor score (sortable bits; 0 = none)
+    const float4* quarter_bm;        // sq8_wide: [4·n_tiles] the quarters' row maxima (launch_wide_quarter_max)
 };
 
 struct SettleParams {
@@ -337,19 +340,35 @@ int sq8_ring_slots(int units8, int qb, int want);   // sq8_mfma LDS-DMA ring dep
 hipError_t launch_sq8_tile(const void* q8, int64_t n_rows, int units8, int ks, void* out, hipStream_t s);
 hipError_t launch_sq8_mfma(const Sq8Params& p, hipStream_t s, hipEvent_t ev_start = nullptr,
                            hipEvent_t ev_stop = nullptr);
-// int8 MFMA prefilter for large batches (osk_sq8w.hip): kWideQ queries per launch, 64 per wave, rows
-// ≤ 256 int8 dims, unfiltered.  One workgroup per (tile, quarter) — the settle's list of a scan wave with
-// scan_R = kMfmaScanR — whose 4 waves share the quarter's rows, staged once through an LDS-DMA ring, and
-// each own 64 of the queries (lists per (quarter, query) in LDS).  pilot = 1: each workgroup bounds only
-// its quarter's first 64 rows and writes, per query, the best lower-bound key of them to
+// int8 MFMA prefilter for large batches (osk_sq8w.hip): kWideQ queries per launch, 32 per wave, rows
+// ≤ 256 int8 dims, unfiltered.  Persistent: one workgroup of 8 waves per CU streams its share of the
+// (tile, quarter) row ranges — the settle's list of a scan wave with scan_R = kMfmaScanR — through an
+// LDS-DMA ring once; every wave scores its 32 queries against every staged row (lists per (quarter, query)
+// in LDS).  pilot = 1: each quarter's first 64 rows only, and per query the best lower-bound key of them to
 // pilot_keys [q][4·n_tiles].
-constexpr int kWideQB = 4;                      // 16-query MFMA blocks per wave
-constexpr int kWideQ = 4 * 16 * kWideQB;        // queries per launch
+constexpr int kWideQB = 2;                      // 16-query MFMA blocks per wave
+constexpr int kWideWaves = 8;                   // two per SIMD
+constexpr int kWideQ = kWideWaves * 16 * kWideQB;   // queries per launch
+constexpr int kAuxGroupF4 = 22;                 // float4 per 16-row group of the tiled bound terms
 int sq8_wide_supported(int units8);
 hipError_t launch_sq8_wide(const Sq8Params& p, hipStream_t s, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
-// per 16-row block of a segment's int8 copy: {max s·|q|, max |δ|, max |x|², min |x|²} of its rows (zeros past
-// the last row), the wide kernel's per-step quick-test terms
-hipError_t launch_sq8_block_max(const float4* aux, int64_t n_rows, float4* out, hipStream_t s);
+// The wide kernel's bound terms, tiled per 16-row group of a segment (kAuxGroupF4 float4 = 352 B): s_x[16],
+// (s_x|q_x|)[16], |δ_x|[16], |x|²[16] (struct of arrays: a lane reads its 4 rows' terms in one ds_read_b128),
+// {max s|q|, max |δ|, max |x|², min |x|²} and {max s_x, min s_x, 0, 0} of the group's rows, then (COSINE) the
+// rows' device-order |x|² (xnorm; zeros without).  Rows past the last: zero terms, not in the extrema.  The
+// kernel stages the first 18 float4 (COSINE all 22) with the rows.
+hipError_t launch_sq8_aux_tile(const float4* aux, const float* xnorm, int64_t n_rows, float4* out, hipStream_t s);
+// Per (tile, quarter) of a view: {max s|q|, max |δ|, max |x|², min |x|²} over its rows (the wide kernel's
+// quick-test terms, from the tiled bound terms' group maxima), out [4·n_tiles]
+hipError_t launch_wide_quarter_max(const TileDev* tiles, int n_tiles, const float4* const* auxt, float4* out,
+                                   hipStream_t s);
+// The wide kernel's per-(query, shard) floors [nq][n_shards]: the pilot's (the k-th of thr_keys when
+// thr_counts reaches k), raised to the k-th best list maximum lower bound among the shard's lists
+// (list_lbmax [nq][n_lists], lists of shard s at [shard_list_begin[s], [s + 1]); 0 = not written) when
+// list_lbmax is given.  Sortable score bits; a floor at or below score 0 is dropped (ties at the clamp).
+hipError_t launch_wide_floor(const uint32_t* list_lbmax, int n_lists, const int32_t* shard_list_begin, int n_shards,
+                             int nq, int k, const uint64_t* thr_keys, const int32_t* thr_counts, uint32_t* floors,
+                             hipStream_t s);
 // The 6-bit tier's share of the query prep (C = 0: none): the nibble-split query [nq_pad][64·C dwords],
 // its bound terms, and the floor buckets [nq_pad][floor_n] zeroed
 struct Sq6Prep {
@@ -416,7 +435,11 @@ struct Tuning {
     std::atomic<int> sq8_mfma_queries{32};    // queries per sq8_mfma launch: 16 or 32 (two MFMA chains per row operand)
     std::atomic<int> sq8_mfma_ablate{0};  // TESTING. A/B timing only: 1 skip sq8_mfma's epilogue, 2 its MFMAs (results wrong)
     std::atomic<int> sq8_mfma_min{2};     // prefilter batches ≥ this scan on int8 MFMA, 16 queries per launch (0 = never)
-    std::atomic<int> sq8_wide_min{0};     // ...and unfiltered batches ≥ this on the wide kernel, kWideQ per launch (0 = never)
+    std::atomic<int> sq8_wide_min{64};    // ...and unfiltered batches ≥ this on the wide kernel, kWideQ per launch, when
+                                          // its cost model beats sq8_mfma's (0 = never)
+    std::atomic<int> sq8_wide_force{0};   // (tests) the wide kernel for every eligible batch, whatever the model says
+    std::atomic<int> sq8_wide_phase{8};   // the wide kernel's first pass covers 1/this of the quarters, whose lists
+                                          // raise the floors of the rest (0: one pass)
     std::atomic<int> sq8_force_fallback{0};   // TESTING. tests: every list of a prefiltered search is re-scanned exactly
     std::atomic<int> settle_trace{0};     // TESTING. A/B only: record settle phase timestamps (debug copy "settle_trace")
     std::atomic<int> mfma_ablate{0};      // TESTING. A/B only: 1 skip the epilogue, 2 skip query staging, 4 skip corpus staging,

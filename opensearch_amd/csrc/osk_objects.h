@@ -136,7 +136,7 @@ struct osk_seg {
     void* d_q8 = nullptr;
     float4* d_q8aux = nullptr;
     void* d_q8t = nullptr;    // the int8 rows in sq8_mfma's tiled layout (osk_seg_warm / first batched prefilter)
-    float4* d_q8bmax = nullptr;   // per 16-row block: maxima of the bound terms (sq8_wide's quick test), with d_q8t
+    float4* d_q8auxt = nullptr;   // per 16-row group: the bound terms tiled for sq8_wide (launch_sq8_aux_tile), with d_q8t
     void* d_q6 = nullptr;     // the 6-bit tier (dims with sq6_supported, tune sq6 on at staging): tiled codes,
     float4* d_q6aux = nullptr;   // built with the int8 copy; freed when the segment's calibration turns it off
     // The 6-bit tier's calibration, per segment: every view over the segment (a searcher's view, its
@@ -186,7 +186,8 @@ struct osk_view {
     float sq8_gam = 0.f, sq8_g2 = 0.f, sq8_cos_slack = 0.f;
     osk::DevBuf d_sq8_rows, d_sq8_aux, d_counters;   // counters: SettleParams::counters
     osk::DevBuf d_sq8_rows_t;                         // per segment: tiled int8 copy (sq8_mfma)
-    osk::DevBuf d_sq8_bmax, d_shard_quarter_begin;    // per segment: its block maxima (sq8_wide); 4·shard_tile_begin
+    osk::DevBuf d_sq8_auxt, d_shard_quarter_begin;    // per segment: its tiled bound terms (sq8_wide); 4·shard_tile_begin
+    osk::DevBuf d_quarter_bm;                         // per (tile, quarter): its rows' bound-term maxima (sq8_wide)
     bool sq8t_ready = false;
     osk::DevBuf d_sq6_rows, d_sq6_aux;                // per segment: the 6-bit tier (every segment has one or
     bool sq6_ready = false;                           // the view does not use it)
@@ -206,6 +207,7 @@ struct osk_view {
     int n_slices = 0;
     osk::DevBuf d_slices, d_shard_slice_begin, ws_part;
     osk::DevBuf ws_pilot, ws_thr, ws_thr_counts;   // int8 MFMA prefilter: pilot keys, per-(query, shard) floors
+    osk::DevBuf ws_wfloor;                          // sq8_wide: the two passes' floors [2][kWideQ][S]
     int64_t sq8_calls = 0, sq8w_calls = 0;
     int n_cus = 0;                         // the device's CUs (cached; the wide kernel's persistent grid)   // prefiltered searches; those whose batch took sq8_wide
     // filter pushdown by compaction (osk_filter.hip): gather tiles over the compacted accepted ordinals

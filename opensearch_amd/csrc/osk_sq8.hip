@@ -689,7 +689,7 @@ __global__ __launch_bounds__(kBlock, QB == 1 || (NS && KS == 2) ? 4 : (NS ? 2 : 
     const int col = lane & 15, grp = lane >> 4;
     const TileDev tile = p.tiles[blockIdx.x];
     const SegDev seg = p.segs[tile.seg];
-    const int4* __restrict__ XT = p.rows8t[tile.seg];   // tiled: [row / 16][KS][16 rows][4 chunks]
+    const int4* __restrict__ XT = p.rows8t[tile.seg];   // tiled: [row / 16][KS][4 chunks][16 rows]
     const float4* __restrict__ AX = p.aux[tile.seg];
     const uint32_t vbase = (uint32_t)p.seg_vrow[tile.seg];
     const int u8 = p.units8;
@@ -789,7 +789,7 @@ __global__ __launch_bounds__(kBlock, QB == 1 || (NS && KS == 2) ? 4 : (NS ? 2 : 
     auto load_group = [&](int64_t rowA, bool vA, i32x4 (&a)[KS]) {
         // row rowA's chunk grp of slab s: an aligned 16-row group reads 1 KiB contiguous per slab
         const int64_t ra = vA ? rowA : tile.row_begin;
-        const int4* xr = XT + (ra >> 4) * (KS * 64) + (ra & 15) * 4 + grp;
+        const int4* xr = XT + (ra >> 4) * (KS * 64) + grp * 16 + (ra & 15);
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             const int4 v = vA ? load_i4_g(xr + s * 64, p.nt) : make_int4(0, 0, 0, 0);
@@ -1190,12 +1190,14 @@ int sq8_mfma_ks(int u8) {
 
 __global__ __launch_bounds__(kBlock) void sq8_tile(const int4* __restrict__ q8, int64_t n_rows, int u8, int ks,
                                                    int4* __restrict__ out) {
-    // one thread per 16-B unit of the tiled copy: block b, slab s, row r, chunk c
+    // one thread per 16-B unit of the tiled copy: block b, slab s, chunk c, row r (chunk-major in the slab:
+    // a lane's MFMA fragment — row lane & 15, chunk lane >> 4 — is lane-linear, and the slab's first two
+    // chunks, a K = 32 tail, are its first 512 B)
     const int64_t n_units = ((n_rows + 15) / 16) * ks * 64;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n_units; i += (int64_t)gridDim.x * kBlock) {
         const int64_t b = i / (ks * 64);
         const int rem = (int)(i - b * ks * 64);
-        const int s = rem >> 6, r = (rem >> 2) & 15, c = rem & 3;
+        const int s = rem >> 6, c = (rem >> 4) & 3, r = rem & 15;
         const int64_t row = b * 16 + r;
         const int f = s * 4 + c;
         out[i] = (row < n_rows && f < u8) ? q8[row * u8 + f] : make_int4(0, 0, 0, 0);

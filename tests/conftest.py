@@ -20,3 +20,23 @@ def _built():
     from oracle import oracle
     build.build(verbose=False)
     oracle.build()
+
+
+_torch_cuda_ready = False
+
+
+@pytest.fixture(autouse=True)
+def _torch_cuda_first(request):
+    """Initialise torch's HIP context before a GPU test's first native call: torch reports "No HIP GPUs are
+    available" when libosknn initialised the device first in the process (seen when a torch-using GPU test
+    runs on its own, -k), whereas the other order works."""
+    global _torch_cuda_ready
+    if not _torch_cuda_ready and request.node.get_closest_marker("gpu") is not None:
+        try:
+            import torch
+            if torch.cuda.device_count() > 0:
+                torch.cuda.init()
+        except Exception:   # pragma: no cover - a GPU test then fails on its own terms
+            pass
+        _torch_cuda_ready = True
+    yield

@@ -80,10 +80,24 @@ def _sample(n, m, seed):
 
 
 # ---- the library's path cost model, restated (osk_api.hip view_search_device) -------
+def _wide_us(rows, dim, nq):
+    u8 = (dim + 15) // 16
+    return ((nq + 255) // 256) * (rows * (2.0 if u8 <= 8 else 4.0) * 0.0475e-3 + 600.0)
+
+
+def _narrow_us(rows, dim, nq):
+    return ((nq + 31) // 32) * (rows * (16.0 * ((dim + 15) // 16) + 16.0) / 4.3e6 + 165.0 + 0.28 * dim)
+
+
+def _takes_wide(rows, dim, nq):
+    """osk_api.hip sq8_wide_pick: unfiltered batches of >= 64 queries of <= 256 dims, when cheaper."""
+    return dim <= 256 and nq >= 64 and _wide_us(rows, dim, nq) <= _narrow_us(rows, dim, nq)
+
+
 def _takes_bf16x3(rows, dim, nq, k=10):
     if nq < 96 or k > 12:
         return False
-    sq8_us = ((nq + 31) // 32) * (rows * (16.0 * ((dim + 15) // 16) + 16.0) / 4.3e6 + 165.0 + 0.28 * dim)
+    sq8_us = _wide_us(rows, dim, nq) if _takes_wide(rows, dim, nq) else _narrow_us(rows, dim, nq)
     bf_us = ((nq + 255) // 256) * (rows * (0.153 + 0.00119 * dim) * 1e-3 + 325.0)
     return bf_us <= sq8_us
 
@@ -176,30 +190,35 @@ C4_RPS, C4_DIM = 812_500, 96
 
 @pytest.mark.parametrize("sim,dist", [(SIM.DOT_PRODUCT, _lib.DIST_NORMALISH_UNIT),
                                       (SIM.MAXIMUM_INNER_PRODUCT, _lib.DIST_NORMALISH)])
-def test_c4_ring_prefilter_b32_and_b1024(sim, dist):
+def test_c4_prefilter_b32_sq8_mfma_b1024_wide(sim, dist):
+    """C4 shape: b32 on sq8_mfma (the LDS-DMA ring), b1024 on the wide kernel (four launches of 256, each one
+    corpus pass) — the cost model's picks at this size and at C4's own 100M rows — and b1024 forced onto
+    bf16×3; all equal the oracle bit for bit."""
     seed = 9600 + int(sim)
     readers = _readers(C4_RPS, C4_DIM, sim, seed, dist)
     ds = LU.DeviceShardSet([[LU.LeafReaderContext(0, 0, r)] for r in readers], SHARD_INDEX)
+    counters = ("sq8_calls", "mfma_calls", "sq8_wide_calls")
     try:
         q32 = O.synth(0, 32, C4_DIM, 601, dist)
         q1024 = O.synth(0, 1024, C4_DIM, 602, dist)
         s1024 = list(_sample(1024, 32, 5))
         want32, want1024 = _oracle(C4_RPS, C4_DIM, sim, seed, dist, [q32, q1024[s1024]], 10)
-        out, d = _search_counted(ds, q32)
-        assert d == {"sq8_calls": 1, "mfma_calls": 0}
+        out, d = _search_counted(ds, q32, counters=counters)
+        assert d == {"sq8_calls": 1, "mfma_calls": 0, "sq8_wide_calls": 0}, d
         _check(out, want32, range(32), 10)
-        # b1024 on the ring prefilter (forced: at 6.5M rows the cost model prefers bf16x3 here, at the
-        # 100M rows of C4 itself it keeps the prefilter) and on whichever path the cost model picks
-        _lib.tune("sq8_cost_pct", 1)
+        for rows in (N_SHARDS * C4_RPS, 100_000_000):
+            assert _takes_wide(rows, C4_DIM, 1024) and not _takes_bf16x3(rows, C4_DIM, 1024)
+        assert not _takes_wide(100_000_000, C4_DIM, 32)
+        out, d = _search_counted(ds, q1024, counters=counters)
+        assert d == {"sq8_calls": 1, "mfma_calls": 0, "sq8_wide_calls": 1}, d
+        assert ds.counter("sq8_fallback_queries") == 0
+        _check(out, want1024, s1024, 10)
+        _lib.tune("sq8_cost_pct", 100000)   # the prefilter priced out: bf16×3 blocks
         try:
-            out, d = _search_counted(ds, q1024)
+            out, d = _search_counted(ds, q1024, counters=counters)
         finally:
             _lib.tune("sq8_cost_pct", 100)
-        assert d["mfma_calls"] == 0 and d["sq8_calls"] >= 1
-        _check(out, want1024, s1024, 10)
-        assert _takes_bf16x3(N_SHARDS * C4_RPS, C4_DIM, 1024) and not _takes_bf16x3(100_000_000, C4_DIM, 1024)
-        out, d = _search_counted(ds, q1024)
-        assert d == {"sq8_calls": 0, "mfma_calls": 1}
+        assert d == {"sq8_calls": 0, "mfma_calls": 1, "sq8_wide_calls": 0}, d
         _check(out, want1024, s1024, 10)
     finally:
         ds.close()

@@ -34,11 +34,13 @@ def scan_kernel(request):
     _lib.tune("sq8_mfma_queries", 16 if request.param == "mfma16" else 32)
     _lib.tune("sq8_mfma_ring", 0 if request.param == "mfma32reg" else -1)
     _lib.tune("sq8_wide_min", 2 if request.param == "wide" else 0)
+    _lib.tune("sq8_wide_force", 1 if request.param == "wide" else 0)
     yield request.param
     _lib.tune("sq8_mfma_min", 2)
     _lib.tune("sq8_mfma_queries", 32)
     _lib.tune("sq8_mfma_ring", -1)
-    _lib.tune("sq8_wide_min", 0)
+    _lib.tune("sq8_wide_min", 64)
+    _lib.tune("sq8_wide_force", 0)
 
 
 def corpus(n, dim, sim, seed):

@@ -316,12 +316,15 @@ def test_calibration_is_per_segment_and_shared_by_views(sim):
         out2 = one_by_one(lambda q: ds2.search(q, 10, 0, 10), queries[:5])
         assert ds2.counter("sq6_calls") == (5 if keeps else 0)
         assert_same(out, out2)
-        # concurrent host calls lease replicas of the first view: every slot follows the segments' state
+        # concurrent host calls lease replicas of the first view: every slot follows the segments' state.
+        # Each call asks a distinct (from, size) page, so the host entry's opportunistic batching (which
+        # merges concurrent calls of equal k, from, size into one launch chain) keeps them single queries.
         res, errs = {}, []
+        page = [(i % 4, 1 + i // 4) for i in range(16)]
 
         def worker(i):
             try:
-                res[i] = ds.search(queries[5 + i % 7:6 + i % 7], 10, 0, 10)
+                res[i] = ds.search(queries[5 + i % 7:6 + i % 7], 10, page[i][0], page[i][1])
             except Exception as e:   # pragma: no cover - reported below
                 errs.append(e)
         ts = [threading.Thread(target=worker, args=(i,)) for i in range(16)]
@@ -331,9 +334,9 @@ def test_calibration_is_per_segment_and_shared_by_views(sim):
             t.join()
         assert not errs, errs
         assert ds.counter("sq6_calls") - c1 == (16 if keeps else 0)
-        want = tuned("sq6", 0, lambda: one_by_one(lambda q: ds.search(q, 10, 0, 10), queries[5:12]))
         for i in range(16):
-            assert_same(res[i], tuple(w[i % 7:i % 7 + 1] for w in want))
+            want = tuned("sq6", 0, lambda: ds.search(queries[5 + i % 7:6 + i % 7], 10, page[i][0], page[i][1]))
+            assert_same(res[i], want)
     finally:
         if ds2 is not None:
             ds2.close()

@@ -93,8 +93,10 @@ WIDE_MIN = 48   # the batches these tests send to the wide kernel
 @pytest.fixture(autouse=True)
 def defaults():
     _lib.tune("sq8_wide_min", WIDE_MIN)
+    _lib.tune("sq8_wide_force", 1)   # (these views are small: the cost model alone would keep sq8_mfma)
     yield
-    _lib.tune("sq8_wide_min", 0)
+    _lib.tune("sq8_wide_min", 64)
+    _lib.tune("sq8_wide_force", 0)
 
 
 @pytest.mark.parametrize("dim", [1, 17, 64, 96, 100, 128, 129, 200, 256])

@@ -50,6 +50,7 @@ for ab in [int(x) for x in os.environ.get("ABLATE", "0,1,2,3").split(",")]:
         shards.search(q.data_ptr(), B, K, kk, cc, st)
     torch.cuda.synchronize()
     e0, p0, w0 = counter("sq8_wide_events"), counter("sq8_wide_pairs"), counter("sq8_wide_calls")
+    cyc0 = [counter("sq8_wide_" + c + "_cycles") for c in ("wait", "loop")]
     check(lib().osk_view_profile(shards.view, 1))
     n = 5
     for _ in range(n):
@@ -62,5 +63,10 @@ for ab in [int(x) for x in os.environ.get("ABLATE", "0,1,2,3").split(",")]:
     launches = max(1, wc) * ((B + 255) // 256)
     print(f"{cfg} b{B} ablate={ab}: {ms.value / max(1, calls.value):.3f} ms per search (pilot+merge+main), "
           f"wide calls {wc}/{n}, events/search {ev / n:.0f}, pairs/search {pr / n:.0f}", flush=True)
+    cyc = [counter("sq8_wide_" + c + "_cycles") - c0 for c0, c in zip(cyc0, ("wait", "loop"))]
+    # wave 0's shader clocks summed over workgroups (pilot + main): per workgroup per search, and the split
+    wgs = 256 * 2 * n
+    print(f"   clocks per wg-launch (wave 0): loop {cyc[1] / wgs:.0f}, wait+barrier {cyc[0] / wgs:.0f} "
+          f"({cyc[0] / max(1, cyc[1]):.2f})", flush=True)
 _lib.tune("sq8_mfma_ablate", 0)
 shards.close()
