@@ -1136,18 +1136,63 @@ int32_t ensure_sq8t(osk_view* v, hipStream_t st) {
         rows[i] = v->segs[i]->d_q8t;
         auxt[i] = v->segs[i]->d_q8auxt;
     }
-    std::vector<int32_t> sqb(v->shard_tile_begin.size());
-    for (size_t i = 0; i < sqb.size(); ++i) sqb[i] = 4 * v->shard_tile_begin[i];   // the wide kernel's quarters
     OSK_HIP(v->d_sq8_rows_t.reserve(sizeof(void*) * ns));
     OSK_HIP(v->d_sq8_auxt.reserve(sizeof(void*) * ns));
-    OSK_HIP(v->d_shard_quarter_begin.reserve(sizeof(int32_t) * sqb.size()));
     OSK_HIP(hipMemcpyAsync(v->d_sq8_rows_t.p, rows.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
     OSK_HIP(hipMemcpyAsync(v->d_sq8_auxt.p, auxt.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
-    OSK_HIP(hipMemcpyAsync(v->d_shard_quarter_begin.p, sqb.data(), sizeof(int32_t) * sqb.size(), hipMemcpyHostToDevice,
-                           st));
     if (sq8_wide_supported((v->segs.empty() ? 0 : v->segs[0]->units8)) && v->n_tiles > 0) {
-        OSK_HIP(v->d_quarter_bm.reserve(sizeof(float4) * 4 * (size_t)v->n_tiles));
-        OSK_HIP(launch_wide_quarter_max(v->d_tiles.as<TileDev>(), v->n_tiles, v->d_sq8_auxt.as<const float4*>(),
+        // The wide kernel's own tiles: its lists are per (tile, quarter) and every quarter's lists are
+        // written for all 256 queries, so quarters of the scan tiles (≈ 244 rows at C2) would make the list
+        // traffic rival the corpus.  Quarters here hold ≈ R / (2·CUs) rows, 256 … 16,384 (C2 ≈ 2k, C4 16k;
+        // two to a few dozen per persistent workgroup), tiles never span segments, cut at multiples of 16.
+        if (v->n_cus <= 0 &&
+            (hipDeviceGetAttribute(&v->n_cus, hipDeviceAttributeMultiprocessorCount, v->device) != hipSuccess ||
+             v->n_cus <= 0))
+            v->n_cus = 256;
+        double R = 0.0;
+        for (const osk_seg* sg : v->segs) R += (double)sg->n_rows;
+        const int64_t qr = std::min<int64_t>(16384, std::max<int64_t>(256, (int64_t)(R / (2.0 * v->n_cus)) + 15 & ~15ll));
+        const int64_t trows = 4 * qr;
+        std::vector<TileDev> wt;
+        v->wshard_tile_begin.assign(v->n_shards + 1, 0);
+        for (int sh = 0; sh < v->n_shards; ++sh) {
+            v->wshard_tile_begin[sh] = (int32_t)wt.size();
+            for (int i = 0; i < ns; ++i) {
+                if ((v->seg_shard.empty() ? 0 : v->seg_shard[i]) != sh) continue;
+                const int64_t n = v->segs[i]->n_rows;
+                if (n == 0) continue;
+                const int64_t nt = (n + trows - 1) / trows;
+                auto cut = [&](int64_t t) { return t >= nt ? n : (n * t / nt) & ~(int64_t)15; };
+                for (int64_t t = 0; t < nt; ++t)
+                    if (cut(t + 1) > cut(t)) wt.push_back(TileDev{i, sh, cut(t), cut(t + 1)});
+            }
+        }
+        v->wshard_tile_begin[v->n_shards] = (int32_t)wt.size();
+        v->n_wtiles = (int)wt.size();
+        std::vector<int32_t> order(std::max<size_t>(1, wt.size()), 0), sqb(v->n_shards + 1);
+        {   // interleaved over shards (as the scan tiles' order)
+            std::vector<std::pair<double, int>> key;
+            for (int sh = 0; sh < v->n_shards; ++sh) {
+                const int t0 = v->wshard_tile_begin[sh], n = v->wshard_tile_begin[sh + 1] - t0;
+                for (int j = 0; j < n; ++j) key.push_back({(j + 0.5) / n, t0 + j});
+            }
+            std::stable_sort(key.begin(), key.end(), [](auto& a, auto& b) { return a.first < b.first; });
+            for (size_t i = 0; i < key.size(); ++i) order[i] = key[i].second;
+        }
+        for (int i = 0; i <= v->n_shards; ++i) sqb[i] = 4 * v->wshard_tile_begin[i];
+        OSK_HIP(v->d_wtiles.reserve(sizeof(TileDev) * std::max<size_t>(1, wt.size())));
+        OSK_HIP(v->d_wtile_order.reserve(sizeof(int32_t) * order.size()));
+        OSK_HIP(v->d_wshard_tile_begin.reserve(sizeof(int32_t) * (v->n_shards + 1)));
+        OSK_HIP(v->d_shard_quarter_begin.reserve(sizeof(int32_t) * sqb.size()));
+        if (!wt.empty())
+            OSK_HIP(hipMemcpyAsync(v->d_wtiles.p, wt.data(), sizeof(TileDev) * wt.size(), hipMemcpyHostToDevice, st));
+        OSK_HIP(hipMemcpyAsync(v->d_wtile_order.p, order.data(), sizeof(int32_t) * order.size(), hipMemcpyHostToDevice, st));
+        OSK_HIP(hipMemcpyAsync(v->d_wshard_tile_begin.p, v->wshard_tile_begin.data(), sizeof(int32_t) * (v->n_shards + 1),
+                               hipMemcpyHostToDevice, st));
+        OSK_HIP(hipMemcpyAsync(v->d_shard_quarter_begin.p, sqb.data(), sizeof(int32_t) * sqb.size(), hipMemcpyHostToDevice,
+                               st));
+        OSK_HIP(v->d_quarter_bm.reserve(sizeof(float4) * 4 * std::max<size_t>(1, wt.size())));
+        OSK_HIP(launch_wide_quarter_max(v->d_wtiles.as<TileDev>(), v->n_wtiles, v->d_sq8_auxt.as<const float4*>(),
                                         v->d_quarter_bm.as<float4>(), st));
     }
     OSK_HIP(hipStreamSynchronize(st));
@@ -1324,13 +1369,13 @@ void fold_probe(osk_view* v) {
 // The prefilter's two int8 MFMA kernels, in µs for this view's R rows (measured end to end on MI355X,
 // DESIGN.md §3c): sq8_mfma per launch of ≤ 32 queries streams R·(int8 row + 16-B bound terms) at ≈ 4.3 TB/s
 // + ≈ 165 µs + 0.28 µs per dim (pilot, merge, settle, re-score); the wide kernel per launch of ≤ 256 queries
-// ≈ R·KS·0.0475 ns (it is issue-bound, not HBM-bound: C4 9.8 ms per 256) + ≈ 600 µs (pilot, two passes,
-// floors, settle: C2 0.58 ms per 256).
+// ≈ R·KS·0.0454 ns (it is issue-bound, not HBM-bound: C4 9.4 ms per 256) + ≈ 300 µs (pilot, two passes,
+// floors, settle: C2 0.39 ms per 256).
 double sq8_narrow_us(double R, int nq, int u8, int dim) {
     return (double)((nq + 31) / 32) * (R * (16.0 * u8 + 16.0) / 4.3e6 + 165.0 + 0.28 * dim);
 }
 double sq8_wide_us(double R, int nq, int u8) {
-    return (double)((nq + kWideQ - 1) / kWideQ) * (R * (u8 <= 8 ? 2.0 : 4.0) * 0.0475e-3 + 600.0);
+    return (double)((nq + kWideQ - 1) / kWideQ) * (R * (u8 <= 8 ? 2.0 : 4.0) * 0.0454e-3 + 300.0);
 }
 // the wide kernel takes an unfiltered batch of ≥ sq8_wide_min queries of ≤ 256 dims when the model has it
 // cheaper than sq8_mfma (C4: from about 96 queries)
@@ -1359,7 +1404,7 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     // unfiltered query scans the 6-bit tier where the view has one.
     const bool use_mfma = g_tuning.sq8_mfma_min > 0 && nq >= g_tuning.sq8_mfma_min && sq8_mfma_supported(u8);
     // large unfiltered batches of ≤ 256-dim rows: one corpus pass per kWideQ queries (osk_sq8w.hip)
-    const bool use_wide = use_mfma && sq8_wide_pick(v, nq, d_accept != nullptr);
+    const bool use_wide = use_mfma && !g_tuning.sq8_force_fallback && sq8_wide_pick(v, nq, d_accept != nullptr);
     // the 6-bit tier: single unfiltered queries, every segment's calibration probing or on.  The shared
     // lock keeps a segment's copy alive from this check to the launches (fold_probe frees it under the
     // exclusive one after a device synchronisation)
@@ -1408,7 +1453,12 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
         rc = ensure_gather(v, st);
         if (rc) return rc;
     }
-    const int n_scan_tiles = gather ? v->n_gtiles : v->n_tiles;
+    int n_scan_tiles = gather ? v->n_gtiles : v->n_tiles;
+    if (use_wide) {   // its own tile table (ensure_sq8t)
+        rc = ensure_sq8t(v, st);
+        if (rc) return rc;
+        n_scan_tiles = v->n_wtiles;
+    }
     const size_t nl = (size_t)nq * 4 * n_scan_tiles * kKQ;
     OSK_HIP(v->ws_sq8cand.reserve(sizeof(uint64_t) * nl));
     OSK_HIP(v->ws_sq8lb.reserve(sizeof(uint32_t) * nl));
@@ -1477,7 +1527,8 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
                  v->n_cus <= 0))
                 v->n_cus = 256;
             p.wide_grid = v->n_cus;
-            p.tile_order = v->d_tile_order.as<int32_t>();
+            p.tiles = v->d_wtiles.as<TileDev>();
+            p.tile_order = v->d_wtile_order.as<int32_t>();
             p.k = k;
             p.n_shards = S;
             p.ablate = g_tuning.sq8_mfma_ablate;
@@ -1489,7 +1540,7 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             p.floors = nullptr;
             p.quarter_bm = v->d_quarter_bm.as<const float4>();
             OSK_HIP(launch_sq8_wide(p, st, e0, nullptr));
-            const int nql = 4 * v->n_tiles;
+            const int nql = 4 * v->n_wtiles;
             const int32_t* sqb = v->d_shard_quarter_begin.as<int32_t>();
             OSK_HIP(launch_merge_shards(v->ws_pilot.as<uint64_t>(), nql, sqb, S, p.q_count, k,
                                         v->ws_thr.as<uint64_t>(), v->ws_thr_counts.as<int32_t>(), st, 1));
@@ -1503,7 +1554,10 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             // then the rest under floors raised by the first pass's list maxima (the lists of the second pass
             // read as empty until it writes them)
             const int phase = g_tuning.sq8_wide_phase;
-            const int n_a = phase > 1 ? nql / phase : 0;
+            // (the first pass takes whole rounds of the persistent grid, at least one: a small view's 1/phase
+            // would idle the chip, and a partial round leaves a tail)
+            const int rounds = std::max(1, (int)std::lround((double)nql / ((double)phase * v->n_cus)));
+            const int n_a = phase > 1 ? std::min(nql / 2, rounds * v->n_cus) : 0;
             if (n_a > 0) {
                 uint32_t* lbm = p.list_lbmax + (size_t)q0 * nql;
                 OSK_HIP(hipMemsetAsync(lbm, 0, sizeof(uint32_t) * (size_t)p.q_count * nql, st));
@@ -1594,8 +1648,9 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
         OSK_HIP(v->ws_trace.reserve(sizeof(unsigned long long) * 8 * (size_t)nq * n_slices));
         sp.trace = v->ws_trace.as<unsigned long long>();
     }
-    if (use_wide && !sp.force_fail) {   // (forced exact lists are the per-slice settle's test knob)
-        sp.shard_tile_begin = v->d_shard_tile_begin.as<int32_t>();
+    if (use_wide) {
+        sp.tiles = v->d_wtiles.as<TileDev>();
+        sp.shard_tile_begin = v->d_wshard_tile_begin.as<int32_t>();
         OSK_HIP(launch_sq8_settle_wide(v->cfg, nq, sp, st));
     } else {
         OSK_HIP(launch_sq8_settle(v->cfg, nq, sp, st));

@@ -187,7 +187,11 @@ struct osk_view {
     osk::DevBuf d_sq8_rows, d_sq8_aux, d_counters;   // counters: SettleParams::counters
     osk::DevBuf d_sq8_rows_t;                         // per segment: tiled int8 copy (sq8_mfma)
     osk::DevBuf d_sq8_auxt, d_shard_quarter_begin;    // per segment: its tiled bound terms (sq8_wide); 4·shard_tile_begin
-    osk::DevBuf d_quarter_bm;                         // per (tile, quarter): its rows' bound-term maxima (sq8_wide)
+    osk::DevBuf d_quarter_bm;                         // per (wide tile, quarter): its rows' bound-term maxima
+    // sq8_wide's own tiles (ensure_sq8t: quarters of ≈ R / (2·CUs) rows), their shard ranges and dispatch order
+    osk::DevBuf d_wtiles, d_wtile_order, d_wshard_tile_begin;
+    std::vector<int32_t> wshard_tile_begin;
+    int n_wtiles = 0;
     bool sq8t_ready = false;
     osk::DevBuf d_sq6_rows, d_sq6_aux;                // per segment: the 6-bit tier (every segment has one or
     bool sq6_ready = false;                           // the view does not use it)

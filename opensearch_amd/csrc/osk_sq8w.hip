@@ -20,7 +20,7 @@
 //     than sq8_bounds' upper side (derivation at quick_consts).  A passing pair takes the precise bound in
 //     its own lane and, above the floor, is appended to its (quarter, query) list by an LDS atomic; lists
 //     that would fill go through sq8_mfma's ordered insertion (sorted once, best kKQ kept);
-//   * floors: pilot = 1 bounds each quarter's first 64 rows (the best lower-bound key per query; their k-th
+//   * floors: pilot = 1 bounds each quarter's first step of rows (the best lower-bound key per query; their k-th
 //     per (query, shard) floors the main pass); the main pass runs in two launches — 1/phase of the quarters
 //     first, then the rest under floors raised to the k-th best list maximum of the first (launch_wide_floor;
 //     the sq8_mfma pilot argument: k distinct rows score ≥ T, a row with ub < T cannot enter or tie into the
@@ -231,7 +231,7 @@ struct WideQuarter {
     const int4* xt;       // the tiled int8 rows from the quarter's first 16-row group
     const float4* at;     // the tiled bound terms from its first group (kAuxGroupF4 float4 per group)
     uint32_t vrow0;       // view row of its first row
-    int32_t nrows;        // (the pilot: its first 64 rows at most)
+    int32_t nrows;        // (the pilot: its first step's rows at most)
     int32_t list;         // tile·4 + quarter: the settle's list, the pilot's slot
     int32_t shard;
     int32_t seg;
@@ -311,7 +311,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
         d.xt = p.rows8t[tile.seg] + (rb >> 4) * (KS * 64);
         d.at = p.auxt[tile.seg] + (rb >> 4) * kAuxGroupF4;
         d.vrow0 = (uint32_t)(p.seg_vrow[tile.seg] + rb);
-        d.nrows = (int32_t)(pilot ? min<int64_t>(64, re - rb) : re - rb);   // the pilot: one 64-row step
+        d.nrows = (int32_t)(pilot ? min<int64_t>(16 * GPS, re - rb) : re - rb);   // the pilot: one step
         d.list = tix * 4 + quarter;
         d.shard = tile.shard;
         d.seg = tile.seg;

@@ -82,7 +82,7 @@ def _sample(n, m, seed):
 # ---- the library's path cost model, restated (osk_api.hip view_search_device) -------
 def _wide_us(rows, dim, nq):
     u8 = (dim + 15) // 16
-    return ((nq + 255) // 256) * (rows * (2.0 if u8 <= 8 else 4.0) * 0.0475e-3 + 600.0)
+    return ((nq + 255) // 256) * (rows * (2.0 if u8 <= 8 else 4.0) * 0.0454e-3 + 300.0)
 
 
 def _narrow_us(rows, dim, nq):
@@ -229,18 +229,28 @@ def test_c4_prefilter_b32_sq8_mfma_b1024_wide(sim, dist):
 # ---------------------------------------------------------------------------------------------------
 # C2: SIFT-shaped 1M × 128 EUCLIDEAN, one shard, batch 256 on bf16×3
 # ---------------------------------------------------------------------------------------------------
-def test_c2_b256_bf16x3():
+def test_c2_b256_wide_and_bf16x3():
+    """C2 b256: the cost model's pick is the wide int8 prefilter (one corpus pass, 0.39 ms against bf16×3's
+    0.46); bf16×3 forced (the prefilter priced out) equals the oracle too."""
     rows_n, dim, seed = 1_000_000, 128, 1280
     r = LU.GpuFlatVectorsReader.synthetic("v", rows_n, dim, SIM.EUCLIDEAN, seed=seed, dist=_lib.DIST_UNIFORM01_X128)
     ds = LU.DeviceShardSet([[LU.LeafReaderContext(0, 0, r)]], [0])
+    counters = ("sq8_calls", "mfma_calls", "sq8_wide_calls")
     try:
         q = O.synth(0, 256, dim, 701, _lib.DIST_UNIFORM01_X128)
         samp = list(_sample(256, 16, 6))
-        assert _takes_bf16x3(rows_n, dim, 256)
+        assert _takes_wide(rows_n, dim, 256) and not _takes_bf16x3(rows_n, dim, 256)
         want = _oracle(rows_n, dim, SIM.EUCLIDEAN, seed, _lib.DIST_UNIFORM01_X128, [q[samp]], 10, n_shards=1,
                        shard_index=[0])[0]
-        out, d = _search_counted(ds, q)
-        assert d == {"sq8_calls": 0, "mfma_calls": 1}
+        out, d = _search_counted(ds, q, counters=counters)
+        assert d == {"sq8_calls": 1, "mfma_calls": 0, "sq8_wide_calls": 1}, d
+        _check(out, want, samp, 10)
+        _lib.tune("sq8_cost_pct", 100000)
+        try:
+            out, d = _search_counted(ds, q, counters=counters)
+        finally:
+            _lib.tune("sq8_cost_pct", 100)
+        assert d == {"sq8_calls": 0, "mfma_calls": 1, "sq8_wide_calls": 0}, d
         _check(out, want, samp, 10)
     finally:
         ds.close()

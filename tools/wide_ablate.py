@@ -24,7 +24,8 @@ K = 10
 NS, RPS, DIM, SIM, DIST = {"C4": (8, 12_500_000, 96, _lib.DOT_PRODUCT, _lib.DIST_NORMALISH_UNIT),
                            "C2": (1, 1_000_000, 128, _lib.EUCLIDEAN, _lib.DIST_UNIFORM01_X128),
                            "C3": (8, 1_250_000, 768, _lib.COSINE, _lib.DIST_NORMALISH_UNIT)}[cfg]
-_lib.tune("sq8_wide_min", 2)   # (the wide path is opt-in while it is tuned)
+_lib.tune("sq8_wide_min", 2)
+_lib.tune("sq8_wide_force", 1)
 for kv in filter(None, os.environ.get("TUNE", "").split(",")):
     _lib.tune(kv.split("=")[0], int(kv.split("=")[1]))
 torch.cuda.set_device(0)
@@ -50,6 +51,7 @@ for ab in [int(x) for x in os.environ.get("ABLATE", "0,1,2,3").split(",")]:
         shards.search(q.data_ptr(), B, K, kk, cc, st)
     torch.cuda.synchronize()
     e0, p0, w0 = counter("sq8_wide_events"), counter("sq8_wide_pairs"), counter("sq8_wide_calls")
+    x0 = [counter(c) for c in ("sq8_fallback_queries", "sq8_exact_tiles", "sq8_rescored_rows")]
     cyc0 = [counter("sq8_wide_" + c + "_cycles") for c in ("wait", "loop")]
     check(lib().osk_view_profile(shards.view, 1))
     n = 5
@@ -63,6 +65,9 @@ for ab in [int(x) for x in os.environ.get("ABLATE", "0,1,2,3").split(",")]:
     launches = max(1, wc) * ((B + 255) // 256)
     print(f"{cfg} b{B} ablate={ab}: {ms.value / max(1, calls.value):.3f} ms per search (pilot+merge+main), "
           f"wide calls {wc}/{n}, events/search {ev / n:.0f}, pairs/search {pr / n:.0f}", flush=True)
+    x1 = [counter(c) - c0 for c0, c in zip(x0, ("sq8_fallback_queries", "sq8_exact_tiles", "sq8_rescored_rows"))]
+    print(f"   settle per search: fallback queries {x1[0] / n:.1f}, exactly re-scanned lists {x1[1] / n:.1f}, "
+          f"re-scored rows {x1[2] / n:.0f}", flush=True)
     cyc = [counter("sq8_wide_" + c + "_cycles") - c0 for c0, c in zip(cyc0, ("wait", "loop"))]
     # wave 0's shader clocks summed over workgroups (pilot + main): per workgroup per search, and the split
     wgs = 256 * 2 * n
