@@ -1606,17 +1606,34 @@ __global__ __launch_bounds__(kSettleThreads) void sq8_settle_wide(SettleParams p
     };
     for (int c0 = l0; c0 < l1; c0 += kWideChunk) {
         const int c1 = min(c0 + kWideChunk, l1);
-        // (b) 4 lists per wave-iteration, 16 lanes each: entry e = lane & 15 of list c0 + 4i + (lane >> 4)
-        for (int i = wave; 4 * i < c1 - c0; i += kSettleWaves) {
-            const int l = c0 + 4 * i + (lane >> 4), e = lane & 15;
-            const bool in = l < c1;
-            const bool rows = in && lm[in ? l : c0] != 0u;   // an empty list has best lb 0: keys not read
-            const uint64_t key = rows ? p.cand[((size_t)q * p.n_lists + l) * kKQ + e] : 0ull;
-            const bool reach = key && (uint32_t)(key >> 32) >= Lb;
-            const uint64_t full = __ballot(reach && e == kKQ - 1);   // the list's 16th key reaches L
-            const bool exact = (full >> (lane | 15)) & 1ull;
-            if (reach && e == kKQ - 1) s_exact[atomicAdd(&s_ne, 1)] = l;
-            if (reach && !exact) s_cand[atomicAdd(&s_nc, 1)] = 0xFFFFFFFFu - (uint32_t)key;
+        // (b) 4 lists per wave-iteration, 16 lanes each: entry e = lane & 15 of list c0 + 4i + (lane >> 4);
+        // kWideUnroll iterations' best bounds and keys are loaded together (one round trip, not two per
+        // iteration: the walk was latency-bound, 39 µs per C2 b256 search), an empty list's (best lb 0)
+        // keys masked to 0 after the load
+        constexpr int kWideUnroll = 4;
+        const int e = lane & 15;
+        for (int i0 = wave; 4 * i0 < c1 - c0; i0 += kSettleWaves * kWideUnroll) {
+            uint32_t lmv[kWideUnroll];
+            uint64_t kv[kWideUnroll];
+            bool in[kWideUnroll];
+#pragma unroll
+            for (int u = 0; u < kWideUnroll; ++u) {
+                const int l = c0 + 4 * (i0 + u * kSettleWaves) + (lane >> 4);
+                in[u] = l < c1;
+                const int lc = in[u] ? l : c0;
+                lmv[u] = lm[lc];
+                kv[u] = p.cand[((size_t)q * p.n_lists + lc) * kKQ + e];
+            }
+#pragma unroll
+            for (int u = 0; u < kWideUnroll; ++u) {
+                const int l = c0 + 4 * (i0 + u * kSettleWaves) + (lane >> 4);
+                const uint64_t key = (in[u] && lmv[u] != 0u) ? kv[u] : 0ull;
+                const bool reach = key && (uint32_t)(key >> 32) >= Lb;
+                const uint64_t full = __ballot(reach && e == kKQ - 1);   // the list's 16th key reaches L
+                const bool exact = (full >> (lane | 15)) & 1ull;
+                if (reach && e == kKQ - 1) s_exact[atomicAdd(&s_ne, 1)] = l;
+                if (reach && !exact) s_cand[atomicAdd(&s_nc, 1)] = 0xFFFFFFFFu - (uint32_t)key;
+            }
         }
         __syncthreads();
         const int nc = s_nc, ne = s_ne;
