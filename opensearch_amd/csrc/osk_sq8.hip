@@ -1540,21 +1540,24 @@ __global__ __launch_bounds__(kSettleThreads) void sq8_settle_merge(SettleParams 
 //   (b) the lists in chunks of 256: a list with no row (best lb 0) is skipped without reading its keys;
 //       a full list whose 16th upper bound reaches L (it may have dropped a qualifying row) is re-scanned
 //       exactly; the other lists' rows with ub ≥ L are re-scored exactly (scan_f32's arithmetic);
-//   (c) the 4 waves' top k → shard_keys / shard_counts.
+//   (c) the 16 waves' top k → shard_keys / shard_counts.
 // Exactness is sq8_settle's: every row of the shard's top k has ub ≥ exact ≥ T ≥ L, so it is re-scored or
 // lies in a re-scanned list.
 // ------------------------------------------------------------------------------------------------
 constexpr int kWideChunk = 256;   // lists per chunk of the list walk
+// 16 waves per (shard, query): a wide batch has few of these workgroups (C2 b256: 256, one per CU), and
+// the walk and the re-score are latency-bound chains, so more waves per workgroup hide more of them
+constexpr int kWideSettleWaves = 16, kWideSettleThreads = kWideSettleWaves * 64;
 template <int L, int V, bool L2K>
-__global__ __launch_bounds__(kSettleThreads) void sq8_settle_wide(SettleParams p) {
+__global__ __launch_bounds__(kWideSettleThreads) void sq8_settle_wide(SettleParams p) {
     constexpr int R = 64 / L, UP = L * V;
-    __shared__ uint32_t s_bm[kSettleWaves][64];
+    __shared__ uint32_t s_bm[kWideSettleWaves][64];
     __shared__ uint64_t s_keys[64];
     __shared__ uint32_t s_L;
     __shared__ uint32_t s_cand[kWideChunk * kKQ];
     __shared__ int32_t s_exact[kWideChunk];
     __shared__ int s_nc, s_ne;
-    __shared__ uint64_t s_lists[kSettleWaves * 64];
+    __shared__ uint64_t s_lists[kWideSettleWaves * 64];
     __shared__ uint64_t s_top[64];
     const int sh = blockIdx.x, q = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1562,9 +1565,9 @@ __global__ __launch_bounds__(kSettleThreads) void sq8_settle_wide(SettleParams p
     const int k = p.k, sim = p.sim;
     const int l0 = 4 * p.shard_tile_begin[sh], l1 = 4 * p.shard_tile_begin[sh + 1];
     const uint32_t* __restrict__ lm = p.list_lbmax + (size_t)q * p.n_lists;
-    // (a) bucket maxima: thread t takes lists l0 + t + 256j (bucket t mod 64, four threads per bucket)
+    // (a) bucket maxima: thread t takes lists l0 + t + 1024j (bucket t mod 64, 16 threads per bucket)
     uint32_t mx = 0u;
-    for (int l = l0 + tid; l < l1; l += kSettleThreads) mx = max(mx, lm[l]);
+    for (int l = l0 + tid; l < l1; l += kWideSettleThreads) mx = max(mx, lm[l]);
     s_bm[wave][lane] = mx;
     const float4* __restrict__ Q = reinterpret_cast<const float4*>(p.q) + (size_t)q * UP;
     float4 qf[V];
@@ -1573,7 +1576,9 @@ __global__ __launch_bounds__(kSettleThreads) void sq8_settle_wide(SettleParams p
     const float qn = (!L2K && sim == SIM_COSINE) ? p.qnorm[q] : 0.0f;
     __syncthreads();
     if (tid < 64) {
-        const uint32_t m = max(max(s_bm[0][tid], s_bm[1][tid]), max(s_bm[2][tid], s_bm[3][tid]));
+        uint32_t m = 0u;
+#pragma unroll
+        for (int w = 0; w < kWideSettleWaves; ++w) m = max(m, s_bm[w][tid]);
         s_keys[tid] = ((uint64_t)m << 32) | (uint32_t)tid;   // distinct
     }
     __syncthreads();
@@ -1612,13 +1617,13 @@ __global__ __launch_bounds__(kSettleThreads) void sq8_settle_wide(SettleParams p
         // keys masked to 0 after the load
         constexpr int kWideUnroll = 4;
         const int e = lane & 15;
-        for (int i0 = wave; 4 * i0 < c1 - c0; i0 += kSettleWaves * kWideUnroll) {
+        for (int i0 = wave; 4 * i0 < c1 - c0; i0 += kWideSettleWaves * kWideUnroll) {
             uint32_t lmv[kWideUnroll];
             uint64_t kv[kWideUnroll];
             bool in[kWideUnroll];
 #pragma unroll
             for (int u = 0; u < kWideUnroll; ++u) {
-                const int l = c0 + 4 * (i0 + u * kSettleWaves) + (lane >> 4);
+                const int l = c0 + 4 * (i0 + u * kWideSettleWaves) + (lane >> 4);
                 in[u] = l < c1;
                 const int lc = in[u] ? l : c0;
                 lmv[u] = lm[lc];
@@ -1626,7 +1631,7 @@ __global__ __launch_bounds__(kSettleThreads) void sq8_settle_wide(SettleParams p
             }
 #pragma unroll
             for (int u = 0; u < kWideUnroll; ++u) {
-                const int l = c0 + 4 * (i0 + u * kSettleWaves) + (lane >> 4);
+                const int l = c0 + 4 * (i0 + u * kWideSettleWaves) + (lane >> 4);
                 const uint64_t key = (in[u] && lmv[u] != 0u) ? kv[u] : 0ull;
                 const bool reach = key && (uint32_t)(key >> 32) >= Lb;
                 const uint64_t full = __ballot(reach && e == kKQ - 1);   // the list's 16th key reaches L
@@ -1639,7 +1644,7 @@ __global__ __launch_bounds__(kSettleThreads) void sq8_settle_wide(SettleParams p
         const int nc = s_nc, ne = s_ne;
         n_res += nc;
         n_exact += ne;
-        for (int i0 = wave * R; i0 < nc; i0 += kSettleWaves * R) {
+        for (int i0 = wave * R; i0 < nc; i0 += kWideSettleWaves * R) {
             const int ci = i0 + gr;
             rescore(s_cand[ci < nc ? ci : 0], ci < nc);
         }
@@ -1652,7 +1657,7 @@ __global__ __launch_bounds__(kSettleThreads) void sq8_settle_wide(SettleParams p
             const int64_t spw = ((trows + 4 * p.scan_R - 1) / (4 * p.scan_R)) * p.scan_R;
             const int64_t lb0 = min(td.row_begin + (list & 3) * spw, td.row_end);
             const int64_t lb1 = min(lb0 + spw, td.row_end);
-            const int64_t per_wave = ((lb1 - lb0 + kSettleWaves * R - 1) / (kSettleWaves * R)) * R;
+            const int64_t per_wave = ((lb1 - lb0 + kWideSettleWaves * R - 1) / (kWideSettleWaves * R)) * R;
             const int64_t wb = lb0 + wave * per_wave, we = min(wb + per_wave, lb1);
             const float4* X = static_cast<const float4*>(seg.rows);
             for (int64_t r0 = wb; r0 < we; r0 += R) {
@@ -1682,7 +1687,7 @@ __global__ __launch_bounds__(kSettleThreads) void sq8_settle_wide(SettleParams p
     s_lists[wave * 64 + lane] = lane < k ? lk : 0ull;
     if (tid < 64) s_top[tid] = 0ull;
     __syncthreads();
-    block_rank_topk<kSettleWaves>(s_lists, k, tid, s_top);
+    block_rank_topk<kWideSettleWaves>(s_lists, k, tid, s_top);
     __syncthreads();
     if (wave == 0) {
         const uint64_t key = lane < k ? s_top[lane] : 0ull;
@@ -1699,16 +1704,14 @@ static const SettleFn kSettle[9][2] = {OSK_SETTLE_ROW(4, 2),  OSK_SETTLE_ROW(8, 
                                        OSK_SETTLE_ROW(16, 4), OSK_SETTLE_ROW(16, 8), OSK_SETTLE_ROW(16, 12),
                                        OSK_SETTLE_ROW(32, 8), OSK_SETTLE_ROW(64, 8), OSK_SETTLE_ROW(64, 16)};
 
-static const SettleFn kSettleWide[9][2] = {
+// (the wide kernel takes rows of ≤ 256 dims, sq8_wide_supported: settle configs 0–3 only)
+static const SettleFn kSettleWide[4][2] = {
     {sq8_settle_wide<4, 2, false>, sq8_settle_wide<4, 2, true>},    {sq8_settle_wide<8, 2, false>, sq8_settle_wide<8, 2, true>},
-    {sq8_settle_wide<8, 4, false>, sq8_settle_wide<8, 4, true>},    {sq8_settle_wide<16, 4, false>, sq8_settle_wide<16, 4, true>},
-    {sq8_settle_wide<16, 8, false>, sq8_settle_wide<16, 8, true>},  {sq8_settle_wide<16, 12, false>, sq8_settle_wide<16, 12, true>},
-    {sq8_settle_wide<32, 8, false>, sq8_settle_wide<32, 8, true>},  {sq8_settle_wide<64, 8, false>, sq8_settle_wide<64, 8, true>},
-    {sq8_settle_wide<64, 16, false>, sq8_settle_wide<64, 16, true>}};
+    {sq8_settle_wide<8, 4, false>, sq8_settle_wide<8, 4, true>},    {sq8_settle_wide<16, 4, false>, sq8_settle_wide<16, 4, true>}};
 
 hipError_t launch_sq8_settle_wide(int cfg, int nq, const SettleParams& p, hipStream_t s) {
-    if (p.accept || p.gtiles || !p.shard_tile_begin || p.k < 1 || p.k > 64) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(kSettleWide[cfg][p.sim == SIM_EUCLIDEAN ? 1 : 0], dim3(p.n_shards, nq), dim3(kSettleThreads), 0,
+    if (p.accept || p.gtiles || !p.shard_tile_begin || p.k < 1 || p.k > 64 || cfg < 0 || cfg > 3) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(kSettleWide[cfg][p.sim == SIM_EUCLIDEAN ? 1 : 0], dim3(p.n_shards, nq), dim3(kWideSettleThreads), 0,
                        s, p);
     return hipGetLastError();
 }
