@@ -1520,8 +1520,8 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
         hipEvent_t e0 = v->profile && q0 == 0 ? v->ev0 : nullptr;
         hipEvent_t e1 = v->profile && q0 + chunk >= nq ? v->ev1 : nullptr;
         if (use_wide) {
-            // pilot: the first 16 rows of every quarter → per (query, quarter) the best lower-bound key →
-            // per (query, shard) the top k (one key per quarter); its k-th floors the main pass
+            // pilot: the first step of every quarter → per (query, quarter) the best lower-bound key (and the
+            // quarter's list maximum zeroed) → per (query, shard) the k-th best of them floors the main pass
             if (v->n_cus <= 0 &&
                 (hipDeviceGetAttribute(&v->n_cus, hipDeviceAttributeMultiprocessorCount, v->device) != hipSuccess ||
                  v->n_cus <= 0))
@@ -1542,12 +1542,10 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             OSK_HIP(launch_sq8_wide(p, st, e0, nullptr));
             const int nql = 4 * v->n_wtiles;
             const int32_t* sqb = v->d_shard_quarter_begin.as<int32_t>();
-            OSK_HIP(launch_merge_shards(v->ws_pilot.as<uint64_t>(), nql, sqb, S, p.q_count, k,
-                                        v->ws_thr.as<uint64_t>(), v->ws_thr_counts.as<int32_t>(), st, 1));
             uint32_t* floor_a = v->ws_wfloor.as<uint32_t>();
             uint32_t* floor_b = floor_a + (size_t)kWideQ * S;
-            OSK_HIP(launch_wide_floor(nullptr, nql, sqb, S, p.q_count, k, v->ws_thr.as<uint64_t>(),
-                                      v->ws_thr_counts.as<int32_t>(), floor_a, st));
+            OSK_HIP(launch_wide_floor(nullptr, v->ws_pilot.as<uint64_t>(), nql, sqb, S, p.q_count, k, nullptr, floor_a,
+                                      st));
             p.pilot = 0;
             p.floors = floor_a;
             // two passes: the first 1/phase of the quarters (tile order: every shard) under the pilot's floors,
@@ -1558,13 +1556,11 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             // would idle the chip, and a partial round leaves a tail)
             const int rounds = std::max(1, (int)std::lround((double)nql / ((double)phase * v->n_cus)));
             const int n_a = phase > 1 ? std::min(nql / 2, rounds * v->n_cus) : 0;
-            if (n_a > 0) {
+            if (n_a > 0) {   // (the pilot zeroed every list maximum: the second pass's read as empty)
                 uint32_t* lbm = p.list_lbmax + (size_t)q0 * nql;
-                OSK_HIP(hipMemsetAsync(lbm, 0, sizeof(uint32_t) * (size_t)p.q_count * nql, st));
                 p.quarter_end = n_a;
                 OSK_HIP(launch_sq8_wide(p, st, nullptr, nullptr));
-                OSK_HIP(launch_wide_floor(lbm, nql, sqb, S, p.q_count, k, v->ws_thr.as<uint64_t>(),
-                                          v->ws_thr_counts.as<int32_t>(), floor_b, st));
+                OSK_HIP(launch_wide_floor(lbm, nullptr, nql, sqb, S, p.q_count, k, floor_a, floor_b, st));
                 p.quarter_begin = n_a;
                 p.quarter_end = 0;
                 p.floors = floor_b;

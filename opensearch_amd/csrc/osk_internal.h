@@ -362,13 +362,13 @@ hipError_t launch_sq8_aux_tile(const float4* aux, const float* xnorm, int64_t n_
 // quick-test terms, from the tiled bound terms' group maxima), out [4·n_tiles]
 hipError_t launch_wide_quarter_max(const TileDev* tiles, int n_tiles, const float4* const* auxt, float4* out,
                                    hipStream_t s);
-// The wide kernel's per-(query, shard) floors [nq][n_shards]: the pilot's (the k-th of thr_keys when
-// thr_counts reaches k), raised to the k-th best list maximum lower bound among the shard's lists
-// (list_lbmax [nq][n_lists], lists of shard s at [shard_list_begin[s], [s + 1]); 0 = not written) when
-// list_lbmax is given.  Sortable score bits; a floor at or below score 0 is dropped (ties at the clamp).
-hipError_t launch_wide_floor(const uint32_t* list_lbmax, int n_lists, const int32_t* shard_list_begin, int n_shards,
-                             int nq, int k, const uint64_t* thr_keys, const int32_t* thr_counts, uint32_t* floors,
-                             hipStream_t s);
+// The wide kernel's per-(query, shard) floors [nq][n_shards]: base (or 0), raised to the k-th best of the
+// shard's pilot keys (pilot_keys [nq][n_lists], one per quarter) or of its lists' maximum lower bounds
+// (list_lbmax [nq][n_lists]; 0 = not written); the shard's quarters / lists are [shard_list_begin[s], [s + 1]).
+// Sortable score bits; a floor at or below score 0 is dropped (ties at the clamp).
+hipError_t launch_wide_floor(const uint32_t* list_lbmax, const uint64_t* pilot_keys, int n_lists,
+                             const int32_t* shard_list_begin, int n_shards, int nq, int k, const uint32_t* base,
+                             uint32_t* floors, hipStream_t s);
 // The 6-bit tier's share of the query prep (C = 0: none): the nibble-split query [nq_pad][64·C dwords],
 // its bound terms, and the floor buckets [nq_pad][floor_n] zeroed
 struct Sq6Prep {

@@ -121,50 +121,50 @@ hipError_t launch_wide_quarter_max(const TileDev* tiles, int n_tiles, const floa
     return hipGetLastError();
 }
 
-// The floors of launch_wide_floor (osk_internal.h): one workgroup per (shard, query).  A list maximum is the
-// lower bound of one row of its list, and lists hold distinct rows, so k lists with maxima ≥ T are k rows
-// scoring ≥ T (the sq8_mfma pilot argument): a row whose upper bound is below T cannot enter or tie into
-// the shard's top k.
-__global__ __launch_bounds__(kBlock) void wide_floor(const uint32_t* __restrict__ list_lbmax, int n_lists,
+// The floors of launch_wide_floor (osk_internal.h): one workgroup per (shard, query), the k-th best of the
+// shard's pilot keys (one per quarter: its first step's best lower-bound key) or of its lists' maxima, raised
+// from a base floor.  A pilot key is one row's lower bound, and so is a list maximum (lists hold distinct
+// rows): k quarters or lists with a value ≥ T are k distinct rows scoring ≥ T (the sq8_mfma pilot argument),
+// so a row whose upper bound is below T cannot enter or tie into the shard's top k.
+__global__ __launch_bounds__(kBlock) void wide_floor(const uint32_t* __restrict__ list_lbmax,
+                                                     const uint64_t* __restrict__ pilot_keys, int n_lists,
                                                      const int32_t* __restrict__ shard_list_begin, int n_shards,
-                                                     int k, const uint64_t* __restrict__ thr_keys,
-                                                     const int32_t* __restrict__ thr_counts,
+                                                     int k, const uint32_t* __restrict__ base,
                                                      uint32_t* __restrict__ floors) {
     __shared__ uint64_t lists[4 * 64];
     const int s = blockIdx.x, b = blockIdx.y;
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const size_t o = (size_t)b * n_shards + s;
-    uint32_t f = 0u;   // the pilot's floor
-    if (thr_counts[o] >= k) {
-        const uint64_t t = thr_keys[o * k + k - 1];
-        f = key_score(t) > 0.0f ? (uint32_t)(t >> 32) : 0u;
-    }
-    if (list_lbmax) {
-        const int l0 = shard_list_begin[s], l1 = shard_list_begin[s + 1];
-        const uint32_t* m = list_lbmax + (size_t)b * n_lists;
-        uint64_t lk = 0ull, thr = 0ull;
-        for (int base = l0 + wave * 64; base < l1; base += kBlock) {
-            const int l = base + lane;
-            const uint32_t v = l < l1 ? m[l] : 0u;
-            wave_offer(v ? ((uint64_t)v << 32) | (uint32_t)(l + 1) : 0ull, true, lk, thr, lane, k);
+    uint32_t f = base ? base[o] : 0u;
+    const int l0 = shard_list_begin[s], l1 = shard_list_begin[s + 1];
+    uint64_t lk = 0ull, thr = 0ull;
+    for (int i0 = l0 + wave * 64; i0 < l1; i0 += kBlock) {
+        const int l = i0 + lane;
+        uint64_t key = 0ull;
+        if (pilot_keys) {
+            key = l < l1 ? pilot_keys[(size_t)b * n_lists + l] : 0ull;   // (distinct: they carry the row)
+        } else if (list_lbmax) {
+            const uint32_t v = l < l1 ? list_lbmax[(size_t)b * n_lists + l] : 0u;
+            key = v ? ((uint64_t)v << 32) | (uint32_t)(l + 1) : 0ull;
         }
-        lists[wave * 64 + lane] = lane < k ? lk : 0ull;
-        __syncthreads();
-        if (wave != 0) return;
-        block_fold(lists, lk, thr, lane, k);
-        const uint64_t kth = readlane64(lk, k - 1);
-        const uint32_t t = (uint32_t)(kth >> 32);
-        if (kth && sortable_to_float(t) > 0.0f && t > f) f = t;
+        wave_offer(key, true, lk, thr, lane, k);
     }
+    lists[wave * 64 + lane] = lane < k ? lk : 0ull;
+    __syncthreads();
+    if (wave != 0) return;
+    block_fold(lists, lk, thr, lane, k);
+    const uint64_t kth = readlane64(lk, k - 1);
+    const uint32_t t = (uint32_t)(kth >> 32);
+    if (kth && sortable_to_float(t) > 0.0f && t > f) f = t;
     if (threadIdx.x == 0) floors[o] = f;
 }
 
-hipError_t launch_wide_floor(const uint32_t* list_lbmax, int n_lists, const int32_t* shard_list_begin, int n_shards,
-                             int nq, int k, const uint64_t* thr_keys, const int32_t* thr_counts, uint32_t* floors,
-                             hipStream_t s) {
+hipError_t launch_wide_floor(const uint32_t* list_lbmax, const uint64_t* pilot_keys, int n_lists,
+                             const int32_t* shard_list_begin, int n_shards, int nq, int k, const uint32_t* base,
+                             uint32_t* floors, hipStream_t s) {
     if (n_shards < 1 || nq < 1 || k < 1 || k > 64) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(wide_floor, dim3(n_shards, nq), dim3(kBlock), 0, s, list_lbmax, n_lists, shard_list_begin,
-                       n_shards, k, thr_keys, thr_counts, floors);
+    hipLaunchKernelGGL(wide_floor, dim3(n_shards, nq), dim3(kBlock), 0, s, list_lbmax, pilot_keys, n_lists,
+                       shard_list_begin, n_shards, k, base, floors);
     return hipGetLastError();
 }
 
@@ -500,7 +500,10 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
 #pragma unroll
             for (int qb = 0; qb < QB; ++qb) {
                 const int qi = wq0 + qb * 16 + col;
-                if (grp == 0 && qi < p.q_count) p.pilot_keys[(size_t)qi * n_quarters + d.list] = 0ull;
+                if (grp == 0 && qi < p.q_count) {
+                    p.pilot_keys[(size_t)qi * n_quarters + d.list] = 0ull;
+                    p.list_lbmax[(size_t)(p.q0 + qi) * p.n_lists + d.list] = 0u;   // (read as empty until written)
+                }
             }
         } else {
             flush(d);   // (the LDS lists are all zero here)
@@ -786,6 +789,8 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                     const int qi = wq0 + qb * 16 + col;
                     if (grp == 0 && qi < p.q_count && !(ablate & 16))
                         p.pilot_keys[(size_t)qi * n_quarters + hd.list] = pbest[qb];
+                    // the two-pass main pass reads the second pass's list maxima as empty until it writes them
+                    if (grp == 0 && qi < p.q_count) p.list_lbmax[(size_t)(p.q0 + qi) * p.n_lists + hd.list] = 0u;
                 }
             }
                 continue;
