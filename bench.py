@@ -80,8 +80,8 @@ def pmc_traffic(rows_local: int, batch: int, prefilter: bool, six: bool = False)
 
 
 READ_CEILING = os.path.join(ROOT, "profiles", "r02j", "hbm_read_ceiling.json")
-# the 6-bit tier's pass (tools/pmc_round3.sh: FETCH_SIZE / WRITE_SIZE of this bench at N = 1)
-PMC_SUMMARY_SQ6 = os.path.join(ROOT, "profiles", "r03d", "pmc", "pmc_c3b1.json")
+# the 6-bit tier's pass (tools/gpu_run.sh pmc: FETCH_SIZE / WRITE_SIZE of this bench at N = 1, round 4)
+PMC_SUMMARY_SQ6 = os.path.join(ROOT, "profiles", "r04f", "pmc", "pmc_traffic.json")
 
 
 def read_ceiling():
@@ -410,7 +410,7 @@ def main():
         bytes_per_launch = rows_local * (((DIM + 255) // 256) * 192 + 16)
         kernel_name = ("sq6_scan<C=3,U=3> the 6-bit pass of the certified prefilter (bytes = 6-bit codes + 16-B "
                        "bound terms per row, one query per launch; its pilot and int8 re-bound kernels read "
-                       "≈ 2-3 % more, profiles/r03d/pmc/)")
+                       "≈ 2 % more: sq6_pilot 0.041 GB, sq6_rebound 0.092 GB per launch, profiles/r04f/pmc/)")
     elif prefilter:
         passes = (B + 7) // 8
         bytes_per_launch = rows_local * (u8 * 16 + 16) * passes
