@@ -20,16 +20,21 @@ stream with its own view (workspace) over the shared segments, round-robin — o
 and exchange run under the next one's scan instead of idling the chip.  The same run also times the
 steps strictly one after another ("one_in_flight": per-query latency).
 
-Path: batches below 16 take the certified int8 prefilter (sq8_scan over an int8 copy of the rows,
-exact fp32 re-score of the rows the bound cannot exclude; results bit-identical to the fp32 scan,
-which the bench re-runs on the same queries and compares); batches ≥ 16 the batched MFMA path.
-roofline: the dominant kernel is HBM-bound; algorithmic bytes per launch = rows scanned × (768 + 16) B
-for sq8_scan (int8 row + 16-B bound terms; rows × 768 × 4 B for the fp32 scan), each read once per
-launch of ≤ 8 queries.  Its average duration is measured live from the kernel's own dispatch-packet
-timestamps (hipExtLaunchKernelGGL events, osk_view_profile) in the one-in-flight timed pass (overlapped
-launches share HBM with their neighbours, so their individual durations overstate the kernel's time);
-the whole step's sustained rate (bytes per step ÷ ms per step of the headline pass) is reported beside
-it.
+Path (the library's own choice): a single unfiltered query — the headline —
+takes the certified prefilter's 6-bit tier (sq6_pilot seeds per-shard floors from 1 % of the rows on the int8
+copy, sq6_scan streams 6-bit codes + 16-B bound terms and keeps the rows whose upper bound reaches the floor,
+sq6_rebound re-bounds them on the int8 copy, the settle re-scores the surviving candidates exactly in fp32);
+results are bit-identical to the fp32 streaming scan, which the bench re-runs on the same queries and
+compares.  Batches of 2…~160 take the int8 MFMA prefilter (sq8_mfma, 32 queries per corpus pass), larger ones
+the wide int8 prefilter (≤ 256 dims, 256 queries per pass) or the bf16×3 MFMA path, by the library's cost model.
+roofline: the dominant kernel is HBM-bound; algorithmic bytes per launch = rows scanned × (576 + 16) B for
+sq6_scan (6-bit codes + 16-B bound terms, one query per launch; rows × (768 + 16) B for sq8_scan's int8 tier;
+rows × 768 × 4 B for the fp32 scan).  Its average duration is measured live from the kernel's own
+dispatch-packet timestamps (hipExtLaunchKernelGGL events, osk_view_profile) in the one-in-flight timed pass
+(overlapped launches share HBM with their neighbours, so their individual durations overstate the kernel's
+time); the whole step's sustained rate (bytes per step ÷ ms per step of the headline pass) is reported
+beside it.  `--rank-share R/W` stages only the shards rank R of a W-GPU run owns (one shard of 1.25M rows
+at W = 8) on this one GPU: the per-GPU share of that run, without its all-gather.
 cpu_baseline: rank 0 at N = 1 only — the oracle's Lucene-equivalent restatement (Panama-512 order,
 not Lucene: no JDK/jar on the box) on a bounded sample, scaled to the full corpus by rows.
 """
@@ -220,6 +225,10 @@ def main():
     ap.add_argument("--k", type=int, default=K, help="k (and size); the headline is k = 10. k > 12 takes the "
                     "select path (osk_select.hip), k ≤ 12 the prefilter's wave lists")
     ap.add_argument("--rows-per-shard", type=int, default=ROWS_PER_SHARD)
+    ap.add_argument("--rank-share", default="", metavar="R/W",
+                    help="stage only the shards rank R of a W-GPU run owns (shard s on rank s·W/8), on this one GPU: "
+                         "the per-GPU share of an N = W run measured without its collective (e.g. 0/8: one shard "
+                         "of 1.25M rows)")
     ap.add_argument("--inflight", type=int, default=4,
                     help="queries in flight: search threads issuing round-robin, each on its own stream with its "
                          "own view (workspace) over the shared segments; 1 = strictly one query after another")
@@ -271,7 +280,12 @@ def main():
     sq8_mfma_min = 2 if a.sq8_mfma_min < 0 else a.sq8_mfma_min
     _lib.tune("sq8_mfma_min", sq8_mfma_min)
     t0 = time.perf_counter()
-    shards = D.LocalShards(rank, world, N_SHARDS, a.rows_per_shard, DIM, _lib.COSINE, _lib.FLOAT32, 42,
+    s_rank, s_world = rank, world
+    if a.rank_share:
+        if world != 1:
+            raise SystemExit("--rank-share emulates one rank's share on one GPU: run it with --gpus 1")
+        s_rank, s_world = (int(x) for x in a.rank_share.split("/"))
+    shards = D.LocalShards(s_rank, s_world, N_SHARDS, a.rows_per_shard, DIM, _lib.COSINE, _lib.FLOAT32, 42,
                            _lib.DIST_NORMALISH_UNIT, local_rank)
     torch.cuda.synchronize()
     rows_local = len(shards.shards) * a.rows_per_shard
@@ -493,6 +507,8 @@ def main():
             "config": {"workload": f"C3 Cohere-shaped exact k-NN: 10M×768 fp32 COSINE, 8 shards, k={K}, from=0, size={SIZE}",
                        "batch": B, "rows": N_SHARDS * a.rows_per_shard, "dim": DIM, "shards": N_SHARDS,
                        "k": K,
+                       "rank_share": (f"rank {s_rank} of {s_world}: shards {shards.shards} only, no collective "
+                                      f"(the per-GPU share of an N = {s_world} run)") if a.rank_share else None,
                        "path": ("prefilter" if prefilter else "select" if select else "mfma" if batched
                                 else "fp32_stream"),
                        "parallelism": (f"8 shards over {world} GPU(s); " + (

@@ -151,8 +151,15 @@ osk_seg::~osk_seg() {
     if (d_q8aux) (void)hipFree(d_q8aux);
     if (d_q8t) (void)hipFree(d_q8t);
     if (d_q8auxt) (void)hipFree(d_q8auxt);
-    if (d_q6) (void)hipFree(d_q6);
-    if (d_q6aux) (void)hipFree(d_q6aux);
+    if (d_q6 || d_q6aux) {   // stream-ordered pool allocations (ensure_sq8_seg); the hipFree calls above
+        int cur = -1;         // synchronised the device, so nothing reads them any more
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(device);
+        if (d_q6) (void)hipFreeAsync(d_q6, nullptr);
+        if (d_q6aux) (void)hipFreeAsync(d_q6aux, nullptr);
+        (void)hipStreamSynchronize(nullptr);
+        if (cur >= 0) (void)hipSetDevice(cur);
+    }
 }
 
 int64_t osk_seg::hbm_bytes() const {
@@ -306,6 +313,8 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         {"sq8_wide_min", &g_tuning.sq8_wide_min, 0, 1 << 20, false},
         {"sq8_wide_force", &g_tuning.sq8_wide_force, 0, 1, false},
         {"sq8_wide_phase", &g_tuning.sq8_wide_phase, 0, 1 << 16, false},
+        {"sq8_wide_grid", &g_tuning.sq8_wide_grid, 0, 1 << 16, false},
+        {"sq8_wide_quarter_rows", &g_tuning.sq8_wide_quarter_rows, 0, 1 << 20, false},
         {"sq8_mfma_ring", &g_tuning.sq8_mfma_ring, -1, 8, false},
         {"i8_stream", &g_tuning.i8_stream, 0, 1, false},
         {"call_timing", &g_tuning.call_timing, 0, 1, false},
@@ -1072,11 +1081,14 @@ int32_t ensure_sq8_seg(osk_seg* s, hipStream_t st) {
     void* q6 = nullptr;
     float4* aux6 = nullptr;
     if (sq6_supported(s->dim) && g_tuning.sq6.load(std::memory_order_relaxed)) {
+        // (stream-ordered allocations: the calibration frees them with hipFreeAsync behind the events of the
+        // launches that read them, no device-wide wait — fold_probe)
         const int64_t b6 = sq6_bytes(s->n_rows, s->dim), ba = std::max<int64_t>(1, s->n_rows) * 16;
-        e = hipMalloc(&q6, (size_t)(b6 - ba));
-        if (e == hipSuccess) e = hipMalloc(&aux6, (size_t)ba);
+        e = hipMallocAsync(&q6, (size_t)(b6 - ba), st);
+        if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&aux6), (size_t)ba, st);
         if (e != hipSuccess) {
-            if (q6) (void)hipFree(q6);
+            if (q6) (void)hipFreeAsync(q6, st);
+            (void)hipStreamSynchronize(st);
             (void)hipFree(q8);
             (void)hipFree(aux);
             set_error(std::string("hipMalloc of the 6-bit prefilter tier failed: ") + hipGetErrorString(e));
@@ -1151,7 +1163,9 @@ int32_t ensure_sq8t(osk_view* v, hipStream_t st) {
             v->n_cus = 256;
         double R = 0.0;
         for (const osk_seg* sg : v->segs) R += (double)sg->n_rows;
-        const int64_t qr = std::min<int64_t>(16384, std::max<int64_t>(256, (int64_t)(R / (2.0 * v->n_cus)) + 15 & ~15ll));
+        const int64_t qr = g_tuning.sq8_wide_quarter_rows > 0
+                               ? std::max<int64_t>(16, (int64_t)g_tuning.sq8_wide_quarter_rows & ~15ll)
+                               : std::min<int64_t>(16384, std::max<int64_t>(256, (int64_t)(R / (2.0 * v->n_cus)) + 15 & ~15ll));
         const int64_t trows = 4 * qr;
         std::vector<TileDev> wt;
         v->wshard_tile_begin.assign(v->n_shards + 1, 0);
@@ -1333,12 +1347,60 @@ int32_t ensure_sq8(osk_view* v, hipStream_t st) {
 // The 6-bit tier's calibration, folded without waiting: when this view's last probe has
 // landed (its event completed), its per-segment int8 re-bound counts join the segments' calibration; a
 // segment with kSq6Probes probes keeps the tier, or turns it off (re-bounds above sq6_probe_pct % of the
-// rows probed) and frees its 6-bit copy.  The free is the only wait, once per segment: every launch that
-// may read the copy was issued under the shared side of g_sq6_free_mu, so the exclusive side plus a device
-// synchronisation retire them all, and no later call launches it (state off).
+// rows probed) and frees its 6-bit copy — stream-ordered, with no host or device-wide wait:
+//  * only a probing segment (state 0) can turn off, so only launches issued while some segment of the view
+//    probes register an event (sq6_track_launch); a kept segment (state 1) never frees its copy early;
+//  * a search holds the shared side of g_sq6_free_mu from its state check to that registration, so once the
+//    freeing call holds the exclusive side (briefly: no waiting under it) every launch that may read the
+//    copy is registered, and every later search sees state 2 and leaves the tier alone;
+//  * the freeing call's stream waits on the events of the registered launches still in flight over the
+//    segment (other views' streams included), then hipFreeAsync releases the copy on that stream.
 std::shared_mutex g_sq6_free_mu;
-void fold_probe(osk_view* v) {
-    if (!v->probe_pending || hipEventQuery(v->ev_probe) != hipSuccess) return;
+struct Sq6Inflight {
+    int device;
+    hipEvent_t ev;
+    std::vector<const osk_seg*> segs;
+};
+std::mutex g_sq6_inflight_mu;                       // (inner to g_sq6_free_mu)
+std::vector<Sq6Inflight> g_sq6_inflight;            // launches over probing segments, not yet seen complete
+std::vector<std::pair<int, hipEvent_t>> g_sq6_ev_pool;
+
+// (g_sq6_inflight_mu held) drop the entries whose launches have completed; their events go back to the pool
+void sq6_prune_locked() {
+    size_t j = 0;
+    for (size_t i = 0; i < g_sq6_inflight.size(); ++i) {
+        if (hipEventQuery(g_sq6_inflight[i].ev) == hipSuccess)
+            g_sq6_ev_pool.push_back({g_sq6_inflight[i].device, g_sq6_inflight[i].ev});
+        else
+            g_sq6_inflight[j++] = std::move(g_sq6_inflight[i]);
+    }
+    g_sq6_inflight.resize(j);
+}
+
+// A 6-bit launch over a view with a probing segment: record its completion (caller holds the shared side
+// of g_sq6_free_mu, and the view's device is current).
+int32_t sq6_track_launch(const osk_view* v, hipStream_t st) {
+    std::lock_guard<std::mutex> lk(g_sq6_inflight_mu);
+    sq6_prune_locked();
+    hipEvent_t ev = nullptr;
+    for (size_t i = 0; i < g_sq6_ev_pool.size(); ++i)
+        if (g_sq6_ev_pool[i].first == v->device) {
+            ev = g_sq6_ev_pool[i].second;
+            g_sq6_ev_pool.erase(g_sq6_ev_pool.begin() + (ptrdiff_t)i);
+            break;
+        }
+    if (!ev) OSK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    hipError_t e = hipEventRecord(ev, st);
+    if (e != hipSuccess) {
+        g_sq6_ev_pool.push_back({v->device, ev});
+        OSK_HIP(e);
+    }
+    g_sq6_inflight.push_back(Sq6Inflight{v->device, ev, std::vector<const osk_seg*>(v->segs.begin(), v->segs.end())});
+    return OSK_OK;
+}
+
+int32_t fold_probe(osk_view* v, hipStream_t st) {
+    if (!v->probe_pending || hipEventQuery(v->ev_probe) != hipSuccess) return OSK_OK;
     v->probe_pending = false;
     const unsigned long long* rb = static_cast<const unsigned long long*>(v->h_seg_rebound.p);
     std::vector<osk_seg*> off;
@@ -1354,16 +1416,23 @@ void fold_probe(osk_view* v) {
         sg->sq6_state.store(keep ? 1 : 2, std::memory_order_release);
         if (!keep) off.push_back(sg);
     }
-    if (off.empty()) return;
+    if (off.empty()) return OSK_OK;
     std::unique_lock<std::shared_mutex> ex(g_sq6_free_mu);
-    if (hipDeviceSynchronize() != hipSuccess) return;   // (keep the copies: a later release frees them)
+    std::lock_guard<std::mutex> lk(g_sq6_inflight_mu);
+    sq6_prune_locked();
+    for (const Sq6Inflight& f : g_sq6_inflight) {
+        bool reads = false;
+        for (const osk_seg* sg : off) reads = reads || std::find(f.segs.begin(), f.segs.end(), sg) != f.segs.end();
+        if (reads) OSK_HIP(hipStreamWaitEvent(st, f.ev, 0));
+    }
     for (osk_seg* sg : off) {
-        std::lock_guard<std::mutex> lk(sg->mu);
-        if (sg->d_q6) (void)hipFree(sg->d_q6);
-        if (sg->d_q6aux) (void)hipFree(sg->d_q6aux);
+        std::lock_guard<std::mutex> sl(sg->mu);
+        if (sg->d_q6) OSK_HIP(hipFreeAsync(sg->d_q6, st));
+        if (sg->d_q6aux) OSK_HIP(hipFreeAsync(sg->d_q6aux, st));
         sg->d_q6 = nullptr;
         sg->d_q6aux = nullptr;
     }
+    return OSK_OK;
 }
 
 // The prefilter's two int8 MFMA kernels, in µs for this view's R rows (measured end to end on MI355X,
@@ -1408,7 +1477,8 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     // the 6-bit tier: single unfiltered queries, every segment's calibration probing or on.  The shared
     // lock keeps a segment's copy alive from this check to the launches (fold_probe frees it under the
     // exclusive one after a device synchronisation)
-    fold_probe(v);
+    rc = fold_probe(v, st);
+    if (rc) return rc;
     std::shared_lock<std::shared_mutex> tier_lock(g_sq6_free_mu, std::defer_lock);
     bool use6 = nq == 1 && !d_accept && !use_mfma && v->sq6_ready && g_tuning.sq6;
     bool probing = false;
@@ -1506,7 +1576,12 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
         p.rows8t = v->d_sq8_rows_t.as<const int4*>();
         p.auxt = v->d_sq8_auxt.as<const float4*>();
         const size_t qmax = use_wide ? kWideQ : kMfmaQueries;
-        OSK_HIP(v->ws_pilot.reserve(sizeof(uint64_t) * qmax * v->n_tiles * (use_wide ? 4 : 64)));
+        // pilot keys: per (query, list) of the table the launch walks — the wide kernel's own quarters
+        // (4 per wide tile, qi·4·n_wtiles + list) or the scan tiles' (64 sampled keys per tile); the two
+        // tables differ in size (tiles_target, views past ≈ 400M rows), so size by the one in use
+        const size_t pilot_keys = use_wide ? qmax * 4 * (size_t)std::max(1, v->n_wtiles)
+                                           : qmax * 64 * (size_t)std::max(1, v->n_tiles);
+        OSK_HIP(v->ws_pilot.reserve(sizeof(uint64_t) * pilot_keys));
         OSK_HIP(v->ws_thr.reserve(sizeof(uint64_t) * qmax * S * 64));
         OSK_HIP(v->ws_thr_counts.reserve(sizeof(int32_t) * qmax * S));
         if (use_wide) OSK_HIP(v->ws_wfloor.reserve(sizeof(uint32_t) * 2 * kWideQ * S));
@@ -1526,7 +1601,9 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
                 (hipDeviceGetAttribute(&v->n_cus, hipDeviceAttributeMultiprocessorCount, v->device) != hipSuccess ||
                  v->n_cus <= 0))
                 v->n_cus = 256;
-            p.wide_grid = v->n_cus;
+            // persistent workgroups: one per CU (sq8_wide_grid overrides it: the tests' LDS-cap grid doubling)
+            const int wgrid = g_tuning.sq8_wide_grid > 0 ? (int)g_tuning.sq8_wide_grid : v->n_cus;
+            p.wide_grid = wgrid;
             p.tiles = v->d_wtiles.as<TileDev>();
             p.tile_order = v->d_wtile_order.as<int32_t>();
             p.k = k;
@@ -1554,8 +1631,8 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             const int phase = g_tuning.sq8_wide_phase;
             // (the first pass takes whole rounds of the persistent grid, at least one: a small view's 1/phase
             // would idle the chip, and a partial round leaves a tail)
-            const int rounds = std::max(1, (int)std::lround((double)nql / ((double)phase * v->n_cus)));
-            const int n_a = phase > 1 ? std::min(nql / 2, rounds * v->n_cus) : 0;
+            const int rounds = std::max(1, (int)std::lround((double)nql / ((double)phase * wgrid)));
+            const int n_a = phase > 1 ? std::min(nql / 2, rounds * wgrid) : 0;
             if (n_a > 0) {   // (the pilot zeroed every list maximum: the second pass's read as empty)
                 uint32_t* lbm = p.list_lbmax + (size_t)q0 * nql;
                 p.quarter_end = n_a;
@@ -1602,6 +1679,10 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             p.cap6 = kSq6Cap;
             p.seg_rebound = probe6 ? v->d_seg_rebound.as<unsigned long long>() : nullptr;
             OSK_HIP(launch_sq6_scan(p, v->dim, st, e0, e1));
+            if (probing) {   // a segment may still turn the tier off: its free waits for this launch
+                rc = sq6_track_launch(v, st);
+                if (rc) return rc;
+            }
         } else {
             OSK_HIP(launch_sq8_scan(p.q_count, p, st, e0, e1));
         }

@@ -437,6 +437,8 @@ struct Tuning {
     std::atomic<int> sq8_mfma_min{2};     // prefilter batches ≥ this scan on int8 MFMA, 16 queries per launch (0 = never)
     std::atomic<int> sq8_wide_min{64};    // ...and unfiltered batches ≥ this on the wide kernel, kWideQ per launch, when
                                           // its cost model beats sq8_mfma's (0 = never)
+    std::atomic<int> sq8_wide_grid{0};    // wide kernel's persistent workgroups (0 = one per CU)
+    std::atomic<int> sq8_wide_quarter_rows{0};   // rows per wide quarter, read when a view builds its table (0 = auto)
     std::atomic<int> sq8_wide_force{0};   // (tests) the wide kernel for every eligible batch, whatever the model says
     std::atomic<int> sq8_wide_phase{8};   // the wide kernel's first pass covers 1/this of the quarters, whose lists
                                           // raise the floors of the rest (0: one pass)

@@ -94,6 +94,22 @@ def synth(row0: int, n: int, dim: int, seed: int, dist: int) -> np.ndarray:
     return out
 
 
+def synth_par(row0: int, n: int, dim: int, seed: int, dist: int, nthreads: int = 8) -> np.ndarray:
+    """synth() in row chunks on `nthreads` threads (the generator is a counter hash of the global row
+    index, so chunking does not change a byte; ctypes drops the GIL for each call)."""
+    from concurrent.futures import ThreadPoolExecutor
+    out = np.empty((n, dim), np.int8 if dist == 4 else np.float32)
+    step = max(1, -(-n // max(1, nthreads)))
+    L = lib()
+
+    def run(i0):
+        L.orc_synth(out.ctypes.data + i0 * out.strides[0], row0 + i0, min(step, n - i0), dim, seed, dist)
+
+    with ThreadPoolExecutor(max(1, nthreads)) as ex:
+        list(ex.map(run, range(0, n, step)))
+    return out
+
+
 def score(q: np.ndarray, x: np.ndarray, sim: int, order: int = ORDER_DEVICE) -> float:
     if q.dtype == np.int8:
         return float(lib().orc_score_i8(_p(np.ascontiguousarray(q)), _p(np.ascontiguousarray(x)), len(q), sim))

@@ -373,3 +373,53 @@ def test_first_device_call_returns_before_its_work_completes():
         ds.close()
         for r in readers:
             r.close()
+
+
+def test_tier_off_frees_its_copy_without_waiting_for_other_streams():
+    """A segment whose calibration turns the tier off frees its 6-bit copy stream-ordered (hipFreeAsync behind
+    the events of the launches that read it), not with a device-wide synchronisation: while a neighbouring
+    view's searches are queued on another stream, the call that folds the last probe and frees the copy
+    returns before that stream's work completes.  Results stay exact after the free (int8 tier)."""
+    import torch
+    sim = LU.VectorSimilarityFunction.EUCLIDEAN   # uniform rows: the probes turn the tier off
+    rows = corpus(120_000, 768, sim, 130)
+    queries = corpus(8, 768, sim, 131)
+    ds, readers = view_of([rows[:60_000], rows[60_000:]], sim, [0, 1])
+    rps = 2_000_000
+    big = [LU.GpuFlatVectorsReader.synthetic("v", rps, 768, COS, seed=33, dist=3, row0=s * rps) for s in range(2)]
+    dsb = LU.DeviceShardSet([[LU.LeafReaderContext(0, 0, r)] for r in big])
+    try:
+        fp0 = [_footprint(r) for r in readers]
+        first = one_by_one(lambda q: ds.search(q, 10, 0, 10), queries[:4])   # the 4 probes (not yet folded)
+        assert ds.counter("sq6_calls") == 4
+        qb = torch.from_numpy(O.synth(0, 1, 768, 34, 3)).cuda()
+        keys = torch.zeros((1, 2, 10), dtype=torch.int64, device="cuda")
+        counts = torch.zeros((1, 2), dtype=torch.int32, device="cuda")
+        st = torch.cuda.Stream()
+        L = _lib.lib()
+        for _ in range(6):   # the neighbour's own probes and builds, done before the timed part
+            _lib.check(L.osk_view_search_device(dsb.handle, qb.data_ptr(), 1, 10, None, keys.data_ptr(),
+                                                counts.data_ptr(), None, st.cuda_stream))
+        torch.cuda.synchronize()
+        with torch.cuda.stream(st):
+            for _ in range(60):   # ≈ 60 × 0.1 ms of queued work on the neighbour's stream
+                _lib.check(L.osk_view_search_device(dsb.handle, qb.data_ptr(), 1, 10, None, keys.data_ptr(),
+                                                    counts.data_ptr(), None, st.cuda_stream))
+        out5 = ds.search(queries[4:5], 10, 0, 10)   # folds the 4th probe: the tier turns off, the copy is freed
+        neighbour_pending = not st.query()
+        st.synchronize()
+        assert neighbour_pending, "the call that freed the 6-bit copy waited for another stream's work"
+        assert ds.counter("sq6_calls") == 4
+        sq6 = [((60_000 + 7) // 8) * 3 * 1536 + 60_000 * 16] * 2
+        assert [_footprint(r) for r in readers] == [a - b for a, b in zip(fp0, sq6)]
+        assert counts.cpu().numpy().tolist() == [[10, 10]]
+        rest = one_by_one(lambda q: ds.search(q, 10, 0, 10), queries[5:])
+        assert ds.counter("sq6_calls") == 4
+        want = tuned("sq6", 0, lambda: one_by_one(lambda q: ds.search(q, 10, 0, 10), queries))
+        got = tuple(np.concatenate([a, b, c]) for a, b, c in zip(first, out5, rest))
+        assert_same(got, want)
+    finally:
+        dsb.close()
+        for r in big:
+            r.close()
+        close_all(ds, readers)

@@ -192,3 +192,56 @@ def test_wide_many_tiles_at_size():
         ds.close()
         for r in readers:
             r.close()
+
+
+def _oracle_check(out, rows_list, shard_of, shard_index, queries, k, sim, every=1):
+    s, d, sh, c, _, _ = out
+    for i in range(0, len(queries), every):
+        es, ed, esh, _, _ = oracle_merge(rows_list, shard_of, shard_index, queries[i], k, sim)
+        assert c[i] == len(ed)
+        assert np.array_equal(d[i, :c[i]], ed) and np.array_equal(sh[i, :c[i]], esh), i
+        assert np.array_equal(bits(s[i, :c[i]]), bits(es)), i
+
+
+def test_wide_with_few_scan_tiles():
+    """tiles_target far below the wide kernel's quarter table (the scan tiles and the wide quarters are two
+    tables): the pilot's key buffer is sized by the wide table, so results equal the oracle."""
+    sim = LU.VectorSimilarityFunction.DOT_PRODUCT
+    rows_list = [corpus(n, 96, sim, 80 + i) for i, n in enumerate([150_000, 90_001])]
+    queries = corpus(256, 96, sim, 81)
+    _lib.tune("tiles_target", 16)
+    try:
+        ds, readers = view_of(rows_list, sim, [0, 1], [1, 0])
+    finally:
+        _lib.tune("tiles_target", 0)
+    try:
+        out = three_ways(ds, queries, 10)
+        _oracle_check(out, rows_list, [0, 1], [1, 0], queries, 10, sim, every=37)
+    finally:
+        close_all(ds, readers)
+
+
+@pytest.mark.parametrize("sim", [LU.VectorSimilarityFunction.COSINE, LU.VectorSimilarityFunction.EUCLIDEAN],
+                         ids=lambda s: s.name)
+def test_wide_many_shards_global_floors_and_grid_doubling(sim):
+    """20 shards (> kWideMaxFloorShards = 16: the per-(shard, query) floors live in global memory, not LDS),
+    256-row quarters and a 1-workgroup grid, so one workgroup's quarter descriptors overflow the LDS cap and
+    launch_sq8_wide doubles the grid until they fit; a second view keeps the default grid."""
+    sizes = [9000 + 517 * i for i in range(20)]
+    rows_list = [corpus(n, 128, sim, 200 + i) for i, n in enumerate(sizes)]
+    shard_of = list(range(20))
+    shard_index = list(np.random.default_rng(5).permutation(20))
+    queries = corpus(130, 128, sim, 201)
+    _lib.tune("sq8_wide_quarter_rows", 256)
+    try:
+        ds, readers = view_of(rows_list, sim, shard_of, shard_index)
+        ds.search(queries[:64], 10, 0, 10)   # builds the wide table under the knob
+    finally:
+        _lib.tune("sq8_wide_quarter_rows", 0)
+    try:
+        default_grid = three_ways(ds, queries, 10)
+        small = tuned("sq8_wide_grid", 1, 0, lambda: ds.search(queries, 10, 0, 10))
+        assert_same(small, default_grid)
+        _oracle_check(small, rows_list, shard_of, shard_index, queries, 10, sim, every=29)
+    finally:
+        close_all(ds, readers)
