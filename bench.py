@@ -310,6 +310,7 @@ def main():
         # libosknn's own RCCL communicator (world 1: no collective runs, the local lists are the image)
         comm = (D.DeviceComm.from_process_group(local_rank) if world > 1
                 else D.DeviceComm.init_rank(local_rank, 0, 1, D.DeviceComm.unique_id()))
+        comm.set_device_limits(B, K, shards.s_pad)   # (every rank: the exchange block's fixed size)
         xsteps = [D.ShardSearchMerge(comm, v, shards.s_pad, B, K, FROM, SIZE, device=local_rank) for v in views]
     else:
         xchg = D.ShardExchange(world, shards.s_pad, B, K, FROM, SIZE, shards.global_shard_index, device=local_rank)

@@ -370,13 +370,25 @@ int32_t osk_comm_all_gather(osk_comm* comm, const void* d_send, void* d_recv, in
  * returns OSK_ERR_INVALID (release and re-create the communicator).  The batch, k and shards per rank size
  * the all-gather, and RCCL requires every rank to pass the same count: the host entry agrees on a
  * fixed-size call header first and refuses on every rank together when they differ; the device entry
- * cannot (it never waits on the host), so its callers must pass the same n_queries, k and
- * shards_per_rank on every rank — its header check catches calls that differ in anything else (sequence,
- * queries, from/size).  osk_comm_status reports the flag (OSK_ERR_INVALID + message) without
+ * never waits on the host, so at world > 1 its all-gather moves a block of the communicator's FIXED size
+ * (osk_comm_set_device_limits) whatever the call's batch, k and shards per rank, and its header check
+ * catches every difference — batch, k and shards per rank included.  osk_comm_status reports the flag (OSK_ERR_INVALID + message) without
  * synchronising: synchronise the call's stream first.  info (optional, 4 values): [flag, rank 0's call
  * number, first differing rank, its call number].  (A rank that never issues its call leaves the others
  * blocked inside RCCL, as the coordinator would wait on a shard that never answers.) */
 int32_t osk_comm_status(const osk_comm* comm, int64_t* info);
+/* The device entry's exchange limits (osk_shards_search_merge_device at world > 1): its all-gather moves
+ * max_queries × max_shards_per_rank × max_k keys plus the header per rank and call, so the RCCL count is a
+ * property of the communicator, equal on every rank by construction, and ranks whose calls differ in
+ * batch, k or shards per rank get count −1 from the header check instead of an all-gather of mismatched
+ * counts (undefined under RCCL: a hang).  Set them once, identically on every rank (like world and id),
+ * before the first device call, to the largest batch, k and shards per rank the node will issue (the
+ * block size is the price of every call: 1 × 10 × 1 keys for single-query k = 10 search at one shard per
+ * GPU).  Defaults: 1 query, k 100, 8 shards per rank.  A call beyond the limits still issues its
+ * collective with a refusal header (the other ranks must not wait alone): every rank's reduce reports
+ * count −1, the communicator is poisoned, and this rank's call returns OSK_ERR_INVALID.  World 1 runs no
+ * collective; the limits do not apply there. */
+int32_t osk_comm_set_device_limits(osk_comm* comm, int32_t max_queries, int32_t max_k, int32_t max_shards_per_rank);
 /* Testing build only (libosknn_testing.so; the shipped library returns OSK_ERR_UNSUPPORTED): a
  * communicator of `world` processes that may share ONE device (RCCL refuses that), whose all-gather
  * goes through the POSIX shared-memory segment named by id (a NUL-terminated "/name"), at most
@@ -403,9 +415,9 @@ int32_t osk_shards_search_merge(osk_comm* comm, osk_view* const* views, int32_t 
 /* The same for one GPU per process with device buffers, asynchronous on `stream`: d_queries
  * n_queries × dim on the view's device, d_accept as osk_view_search_device, shards_per_rank the
  * number of list slots per rank (≥ the view's shards; slots past them are empty), outputs as
- * osk_merge_device.  shards_per_rank must be the same on every rank (the caller knows the shard
- * layout, e.g. the largest shard count of any rank): it sizes the all-gather, and RCCL cannot pair
- * gathers of different sizes. */
+ * osk_merge_device.  shards_per_rank should be the same on every rank (the caller knows the shard
+ * layout, e.g. the largest shard count of any rank); at world > 1 the all-gather moves the communicator's
+ * fixed block (osk_comm_set_device_limits), so a rank that differs gets count −1, never a hang. */
 int32_t osk_shards_search_merge_device(osk_comm* comm, osk_view* view, const void* d_queries, int32_t n_queries,
                                        int32_t k, const uint64_t* const* d_accept, int32_t shards_per_rank,
                                        int32_t from, int32_t size, float* d_scores, int32_t* d_docs,

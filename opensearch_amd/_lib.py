@@ -76,6 +76,7 @@ SIGNATURES = {
     "osk_comm_info": (_I32, [_P, _PI32, _PI32, _PI32]),
     "osk_comm_all_gather": (_I32, [_P, _P, _P, _I64, _P]),
     "osk_comm_status": (_I32, [_P, _PI64]),
+    "osk_comm_set_device_limits": (_I32, [_P, _I32, _I32, _I32]),
     "osk_comm_init_loopback": (_I32, [_I32, _I32, _I32, _P, _I64, C.POINTER(_P)]),
     "osk_comm_init_all_loopback": (_I32, [_P, _I32, C.POINTER(_P)]),
     "osk_shards_search_merge": (_I32, [_P, _P, _I32, _P, _I32, _I32, _P, _I32, _I32, _P, _P, _P, _P, _P, _P]),

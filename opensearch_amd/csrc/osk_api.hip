@@ -151,6 +151,7 @@ osk_seg::~osk_seg() {
     if (d_q8aux) (void)hipFree(d_q8aux);
     if (d_q8t) (void)hipFree(d_q8t);
     if (d_q8auxt) (void)hipFree(d_q8auxt);
+    if (d_q8w) (void)hipFree(d_q8w);
     if (d_q6 || d_q6aux) {   // stream-ordered pool allocations (ensure_sq8_seg); the hipFree calls above
         int cur = -1;         // synchronised the device, so nothing reads them any more
         (void)hipGetDevice(&cur);
@@ -172,6 +173,7 @@ int64_t osk_seg::hbm_bytes() const {
     if (d_q8) b += n * units8 * 16 + n * 16;
     if (d_q8t) b += std::max<int64_t>(1, (n_rows + 15) / 16) * sq8_mfma_ks(units8) * 1024;
     if (d_q8auxt) b += std::max<int64_t>(1, (n_rows + 15) / 16) * kAuxGroupF4 * 16;
+    if (d_q8w) b += std::max<int64_t>(1, (n_rows + 15) / 16) * sq8_wide_ks(units8) * 1024;
     if (d_q6) b += sq6_bytes(n_rows, dim);
     return b;
 }
@@ -1122,18 +1124,26 @@ int32_t ensure_sq8t_seg(osk_seg* s, hipStream_t st) {
         return OSK_ERR_OOM;
     }
     OSK_HIP(launch_sq8_tile(s->d_q8, s->n_rows, u8, ks, q8t, st));
-    float4* auxt = nullptr;   // the wide kernel's tiled bound terms (352 B per 16 rows)
+    // the wide kernel's own copy (osk_sq8w.hip launch_sq8w_build): codes with one scale per 16-row group,
+    // tiled, and their bound terms per group (352 B per 16 rows)
+    void* q8w = nullptr;
+    float4* auxt = nullptr;
     if (sq8_wide_supported(u8)) {
-        e = hipMalloc(&auxt, (size_t)blocks * kAuxGroupF4 * sizeof(float4));
+        e = hipMalloc(&q8w, (size_t)blocks * sq8_wide_ks(u8) * 1024);
+        if (e == hipSuccess) e = hipMalloc(&auxt, (size_t)blocks * kAuxGroupF4 * sizeof(float4));
         if (e != hipSuccess) {
+            if (q8w) (void)hipFree(q8w);
             (void)hipFree(q8t);
-            set_error(std::string("hipMalloc of the tiled bound terms failed: ") + hipGetErrorString(e));
+            set_error(std::string("hipMalloc of the wide prefilter copy failed: ") + hipGetErrorString(e));
             return OSK_ERR_OOM;
         }
-        OSK_HIP(launch_sq8_aux_tile(s->d_q8aux, s->sim == SIM_COSINE ? s->d_xnorm_f : nullptr, s->n_rows, auxt, st));
+        OSK_HIP(launch_sq8w_build(static_cast<const float4*>(s->d_rows), s->n_rows, s->units, u8,
+                                  s->sim == SIM_COSINE ? s->d_xnorm_f : nullptr, s->sim == SIM_COSINE ? 1 : 0, q8w, auxt,
+                                  st));
     }
     OSK_HIP(hipStreamSynchronize(st));
     s->d_q8t = q8t;
+    s->d_q8w = q8w;
     s->d_q8auxt = auxt;
     return OSK_OK;
 }
@@ -1141,16 +1151,19 @@ int32_t ensure_sq8t_seg(osk_seg* s, hipStream_t st) {
 int32_t ensure_sq8t(osk_view* v, hipStream_t st) {
     if (v->sq8t_ready) return OSK_OK;
     const int ns = (int)v->segs.size();
-    std::vector<const void*> rows(ns), auxt(ns);
+    std::vector<const void*> rows(ns), rows_w(ns), auxt(ns);
     for (int i = 0; i < ns; ++i) {
         int32_t rc = ensure_sq8t_seg(v->segs[i], st);
         if (rc) return rc;
         rows[i] = v->segs[i]->d_q8t;
+        rows_w[i] = v->segs[i]->d_q8w;
         auxt[i] = v->segs[i]->d_q8auxt;
     }
     OSK_HIP(v->d_sq8_rows_t.reserve(sizeof(void*) * ns));
+    OSK_HIP(v->d_sq8_rows_w.reserve(sizeof(void*) * ns));
     OSK_HIP(v->d_sq8_auxt.reserve(sizeof(void*) * ns));
     OSK_HIP(hipMemcpyAsync(v->d_sq8_rows_t.p, rows.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
+    OSK_HIP(hipMemcpyAsync(v->d_sq8_rows_w.p, rows_w.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
     OSK_HIP(hipMemcpyAsync(v->d_sq8_auxt.p, auxt.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
     if (sq8_wide_supported((v->segs.empty() ? 0 : v->segs[0]->units8)) && v->n_tiles > 0) {
         // The wide kernel's own tiles: its lists are per (tile, quarter) and every quarter's lists are
@@ -1163,9 +1176,13 @@ int32_t ensure_sq8t(osk_view* v, hipStream_t st) {
             v->n_cus = 256;
         double R = 0.0;
         for (const osk_seg* sg : v->segs) R += (double)sg->n_rows;
+        // (≥ 512 dims: quarters of R / (8·CUs), so the first pass — one round of the persistent grid — covers
+        // 1/8 of the rows, not 1/2, and the second pass's floors come early; list traffic is small beside
+        // rows of ≥ 512 B)
+        const int qdiv = sq8_wide_ks(v->segs.empty() ? 1 : v->segs[0]->units8) >= 8 ? 8 : 2;
         const int64_t qr = g_tuning.sq8_wide_quarter_rows > 0
                                ? std::max<int64_t>(16, (int64_t)g_tuning.sq8_wide_quarter_rows & ~15ll)
-                               : std::min<int64_t>(16384, std::max<int64_t>(256, (int64_t)(R / (2.0 * v->n_cus)) + 15 & ~15ll));
+                               : std::min<int64_t>(16384, std::max<int64_t>(256, (int64_t)(R / ((double)qdiv * v->n_cus)) + 15 & ~15ll));
         const int64_t trows = 4 * qr;
         std::vector<TileDev> wt;
         v->wshard_tile_begin.assign(v->n_shards + 1, 0);
@@ -1444,7 +1461,7 @@ double sq8_narrow_us(double R, int nq, int u8, int dim) {
     return (double)((nq + 31) / 32) * (R * (16.0 * u8 + 16.0) / 4.3e6 + 165.0 + 0.28 * dim);
 }
 double sq8_wide_us(double R, int nq, int u8) {
-    return (double)((nq + kWideQ - 1) / kWideQ) * (R * (u8 <= 8 ? 2.0 : 4.0) * 0.0454e-3 + 300.0);
+    return (double)((nq + kWideQ - 1) / kWideQ) * (R * sq8_wide_ks(u8) * 0.0454e-3 + 300.0);
 }
 // the wide kernel takes an unfiltered batch of ≥ sq8_wide_min queries of ≤ 256 dims when the model has it
 // cheaper than sq8_mfma (C4: from about 96 queries)
@@ -1604,6 +1621,7 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             // persistent workgroups: one per CU (sq8_wide_grid overrides it: the tests' LDS-cap grid doubling)
             const int wgrid = g_tuning.sq8_wide_grid > 0 ? (int)g_tuning.sq8_wide_grid : v->n_cus;
             p.wide_grid = wgrid;
+            p.rows8t = v->d_sq8_rows_w.as<const int4*>();   // (the wide copy: one scale per 16-row group)
             p.tiles = v->d_wtiles.as<TileDev>();
             p.tile_order = v->d_wtile_order.as<int32_t>();
             p.k = k;
@@ -2147,7 +2165,7 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
     }
     const bool dev = n == "sq8_fallback_queries" || n == "sq8_rescored_rows" || n == "sq8_exact_tiles" ||
                      n == "sq6_rebound_rows" || n == "sq8_wide_events" || n == "sq8_wide_pairs" ||
-                     n == "sq8_wide_wait_cycles" || n == "sq8_wide_issue_cycles" || n == "sq8_wide_loop_cycles" ||
+                     n == "sq8_wide_wait_cycles" || n == "sq8_wide_slow_steps" || n == "sq8_wide_loop_cycles" ||
                      n == "sq8_wide_quarter_cycles" || n == "sq8_wide_consts_cycles";
     OSK_REQUIRE(dev || n == "mfma_calls" || n == "mfma_fallback_queries" || n == "sq8_calls" || n == "sq6_calls" ||
                     n == "select_calls" || n == "sq8_wide_calls",
@@ -2161,12 +2179,12 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
             unsigned long long c[16];
             OSK_HIP(hipDeviceSynchronize());   // the last search may be on any stream
             OSK_HIP(hipMemcpy(c, s->d_counters.p, sizeof(c), hipMemcpyDeviceToHost));
-            // [4] … [8]: the wide kernel's insertion events, quick-test passes and wave 0's shader clocks in
-            // the step loop's wait / issue / whole loop (testing build only)
+            // [4] … [8]: the wide kernel's insertion events, quick-test passes, wave 0's shader clocks in the
+            // step loop's waits [6] and whole loop [8], and the wave-steps that took the slow path [7] (testing build)
             sum += (int64_t)(n == "sq8_fallback_queries" ? c[0] : n == "sq8_rescored_rows" ? c[1]
                              : n == "sq8_exact_tiles" ? c[2] : n == "sq6_rebound_rows" ? c[3]
                              : n == "sq8_wide_events" ? c[4] : n == "sq8_wide_pairs" ? c[5]
-                             : n == "sq8_wide_wait_cycles" ? c[6] : n == "sq8_wide_issue_cycles" ? c[7]
+                             : n == "sq8_wide_wait_cycles" ? c[6] : n == "sq8_wide_slow_steps" ? c[7]
                              : n == "sq8_wide_loop_cycles" ? c[8] : n == "sq8_wide_quarter_cycles" ? c[9] : c[10]);
         } else {
             sum += n == "mfma_calls" ? s->mfma_calls : n == "mfma_fallback_queries" ? s->mfma_fallback_queries

@@ -60,6 +60,8 @@ struct osk_comm {
     // the reduce kernel (pinned host memory); a set flag makes the communicator refuse further calls
     osk::HostPinned h_err;
     osk::HostPinned h_spr;               // the host entry's call agreement (agree_call)
+    // the device entry's exchange limits (osk_comm_set_device_limits): its world > 1 block has this fixed size
+    int dev_max_nq = 1, dev_max_k = 100, dev_max_spr = 8;
     void* lb = nullptr;                  // testing build: loopback transport instead of RCCL
     bool lb_local = false;               // testing build: init_all's local devices exchange by device copies
     void (*lb_free)(void*) = nullptr;
@@ -209,7 +211,7 @@ Block block_of(int nq, int k, int spr) {
     return {keys, keys + kXHdrWords + (size_t)(spr + 1) / 2};
 }
 
-constexpr uint64_t kXMagic = 0x4F534B5800000001ull;   // "OSKX", block format 1
+// ("OSKX" block format 1: kXMagic, osk_internal.h; kXRefused marks a refusing rank's block)
 
 // Header words of this call (w[5], the query fingerprint, is computed on the device).
 void header_words(uint64_t (&w)[kXHdrWords], uint64_t seq, int nq, int k, int from, int size, int spr, int dim,
@@ -358,13 +360,20 @@ int32_t gather_blocks(osk_comm* c, osk_view* const* views, size_t words, const h
 // This rank's block of one view: the trailer (header + shard indices) and the per-shard lists padded to
 // spr shards.
 int32_t fill_block(osk_view* v, const void* d_queries, int nq, int k, const uint64_t* const* d_accept, int spr,
-                   const uint64_t (&hw)[kXHdrWords], hipStream_t st) {
-    const Block B = block_of(nq, k, spr);
-    OSK_HIP(v->ws_xkeys.reserve(sizeof(uint64_t) * B.words));
+                   const uint64_t (&hw)[kXHdrWords], hipStream_t st, const Block* cap = nullptr) {
+    // (cap: the device entry's fixed block — the call's lists at its start, the header at cap->keys)
+    const Block B = cap ? *cap : block_of(nq, k, spr);
+    OSK_HIP(v->ws_xkeys.reserve(sizeof(uint64_t) * std::max(B.words, (size_t)nq * spr * k)));
     const int64_t qbytes = (int64_t)nq * v->dim * (v->enc == ENC_FLOAT32 ? 4 : 1);
     OSK_HIP(launch_xhdr_fill(v->ws_xkeys.as<uint64_t>() + B.keys, hw, d_queries, qbytes,
                              v->d_shard_index.as<int32_t>(), v->n_shards, spr, st));
     return search_padded(v, d_queries, nq, k, d_accept, spr, st);
+}
+
+// The device entry's fixed block at world > 1: the limits' keys region, the header, the limits' shard slots.
+Block fixed_block_of(const osk_comm* c) {
+    const size_t keys = (size_t)c->dev_max_nq * c->dev_max_spr * c->dev_max_k;
+    return {keys, keys + kXHdrWords + (size_t)(c->dev_max_spr + 1) / 2};
 }
 
 // The reduce's view of a gathered (or, world 1, local) image of blocks.
@@ -712,11 +721,26 @@ int32_t osk_shards_search_merge_device(osk_comm* comm, osk_view* view, const voi
     std::lock_guard<std::mutex> lv(view->mu);
     rc = order_after_last(view, st);
     if (rc) return rc;
-    const Block B = block_of(n_queries, k, shards_per_rank);
+    // world > 1: the communicator's fixed block (the RCCL count is the same on every rank whatever the call
+    // passes; a call that differs is caught by the header check).  A call beyond the limits sends a refusal
+    // header (magic kXRefused) with empty lists, so every rank's reduce reports count −1 and no rank waits
+    // alone in the all-gather; this rank returns OSK_ERR_INVALID after issuing it.
+    const bool fixed = comm->world > 1;
+    const bool over = fixed && (n_queries > comm->dev_max_nq || k > comm->dev_max_k ||
+                                shards_per_rank > comm->dev_max_spr);
+    const Block B = fixed ? fixed_block_of(comm) : block_of(n_queries, k, shards_per_rank);
     uint64_t hw[kXHdrWords];
     header_words(hw, ++comm->seq, n_queries, k, from, size, shards_per_rank, view->dim, view->enc, comm->world);
-    rc = fill_block(view, d_queries, n_queries, k, d_accept, shards_per_rank, hw, st);
-    if (rc) return rc;
+    if (over) {
+        hw[0] = kXRefused;
+        OSK_HIP(view->ws_xkeys.reserve(sizeof(uint64_t) * B.words));
+        OSK_HIP(hipMemsetAsync(view->ws_xkeys.p, 0, sizeof(uint64_t) * B.keys, st));
+        OSK_HIP(launch_xhdr_fill(view->ws_xkeys.as<uint64_t>() + B.keys, hw, d_queries, 0, view->d_shard_index.as<int32_t>(),
+                                 view->n_shards, std::min(view->n_shards, comm->dev_max_spr), st));
+    } else {
+        rc = fill_block(view, d_queries, n_queries, k, d_accept, shards_per_rank, hw, st, fixed ? &B : nullptr);
+        if (rc) return rc;
+    }
     osk_view* const vs[1] = {view};
     const uint64_t* image = view->ws_xkeys.as<uint64_t>();
     if (comm->world > 1) {   // world 1: the local block is the whole image
@@ -731,8 +755,34 @@ int32_t osk_shards_search_merge_device(osk_comm* comm, osk_view* view, const voi
     }
     const int32_t* sidx = nullptr;
     const XLayout x = image_layout(comm, image, B, &sidx);
-    OSK_HIP(launch_coord_reduce(image, nullptr, sidx, n_queries, comm->world, shards_per_rank, k, from, size, d_scores,
-                               d_docs, d_shard_out, d_count, d_total_hits, d_max_score, st, x));
+    // (a refusing rank reduces with the limits' shape: its outputs are count −1 like every other rank's)
+    OSK_HIP(launch_coord_reduce(image, nullptr, sidx, over ? std::min(n_queries, comm->dev_max_nq) : n_queries,
+                               comm->world, over ? comm->dev_max_spr : shards_per_rank, over ? std::min(k, comm->dev_max_k) : k,
+                               from, size, d_scores, d_docs, d_shard_out, d_count, d_total_hits, d_max_score, st, x));
+    if (over) {
+        set_error("osk_shards_search_merge_device: the call (n_queries " + std::to_string(n_queries) + ", k " +
+                  std::to_string(k) + ", shards_per_rank " + std::to_string(shards_per_rank) +
+                  ") exceeds the communicator's device limits (" + std::to_string(comm->dev_max_nq) + ", " +
+                  std::to_string(comm->dev_max_k) + ", " + std::to_string(comm->dev_max_spr) +
+                  "): refused on every rank (count -1), communicator poisoned; see osk_comm_set_device_limits");
+        return OSK_ERR_INVALID;
+    }
+    return OSK_OK;
+    OSK_GUARD_END
+}
+
+int32_t osk_comm_set_device_limits(osk_comm* comm, int32_t max_queries, int32_t max_k, int32_t max_shards_per_rank) {
+    OSK_GUARD_BEGIN
+    clear_error();
+    OSK_REQUIRE(comm != nullptr, "null communicator");
+    OSK_REQUIRE(max_queries >= 1 && max_k >= 1 && max_k <= OSK_MAX_K && max_shards_per_rank >= 1,
+                "limits must be >= 1 (k <= OSK_MAX_K)");
+    OSK_REQUIRE((int64_t)max_queries * max_k * max_shards_per_rank <= ((int64_t)1 << 27),
+                "device limits: the exchange block would exceed 1 GiB");
+    std::lock_guard<std::mutex> lc(comm->mu);
+    comm->dev_max_nq = max_queries;
+    comm->dev_max_k = max_k;
+    comm->dev_max_spr = max_shards_per_rank;
     return OSK_OK;
     OSK_GUARD_END
 }

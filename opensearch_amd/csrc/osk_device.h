@@ -181,6 +181,10 @@ __device__ __forceinline__ int xchg_header_check(const XLayout& x, int n_ranks, 
         const int r = 1 + e / kXHdrWords, w = e % kXHdrWords;
         if (x.hdr[(size_t)r * rank_words + w] != x.hdr[w]) bad_pair = min(bad_pair, e);
     }
+    // a refusing rank (every rank may refuse alike: the headers then agree) — rank 0's refusal counts as a
+    // mismatch at rank 1 (its header word 0), another rank's at its own
+    for (int r = lane; r < n_ranks; r += 64)
+        if (x.hdr[(size_t)r * rank_words] != kXMagic) bad_pair = min(bad_pair, max(r - 1, 0) * kXHdrWords);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) bad_pair = min(bad_pair, __shfl_xor(bad_pair, o));
     if (bad_pair == 0x7FFFFFFF) return 0;

@@ -179,7 +179,7 @@ struct Sq8Params {
     uint32_t* cand6;                 // sq6_scan → sq6_rebound: per list, the rows that passed the 6-bit test
     int32_t* cnt6;                   // [q][n_lists] their count (> cap6: overflowed)
     int cap6;
-    const float4* const* auxt;       // sq8_wide: per segment, the 16-row groups' bound terms (launch_sq8_aux_tile)
+    const float4* const* auxt;       // sq8_wide: per segment, the 16-row groups' bound terms (launch_sq8w_build)
     int wide_grid;                   // sq8_wide: persistent workgroups (the device's CUs)
     int quarter_begin, quarter_end;  // sq8_wide: the launch's quarters in tile order (end 0: all)
     const uint32_t* floors;          // sq8_wide: [q_count][n_shards] floor score (sortable bits; 0 = none)
@@ -297,6 +297,8 @@ hipError_t launch_select_one(const SelParams& p, int cfg, hipStream_t s, hipEven
 // header differs (another call sequence number, batch, k, from/size, shards per rank or query
 // fingerprint) makes every query's count −1 and records the mismatch in `err` (host memory).
 constexpr int kXHdrWords = 8;
+constexpr uint64_t kXMagic = 0x4F534B5800000001ull;     // header word 0 of a block: "OSKX", format 1
+constexpr uint64_t kXRefused = 0x4F534B58FFFFFFFFull;   // ...of a rank that refused its call (device limits)
 struct XHdrWords {
     uint64_t w[kXHdrWords];
 };
@@ -341,23 +343,27 @@ hipError_t launch_sq8_tile(const void* q8, int64_t n_rows, int units8, int ks, v
 hipError_t launch_sq8_mfma(const Sq8Params& p, hipStream_t s, hipEvent_t ev_start = nullptr,
                            hipEvent_t ev_stop = nullptr);
 // int8 MFMA prefilter for large batches (osk_sq8w.hip): kWideQ queries per launch, 32 per wave, rows
-// ≤ 256 int8 dims, unfiltered.  Persistent: one workgroup of 8 waves per CU streams its share of the
+// ≤ 768 int8 dims, unfiltered.  Persistent: one workgroup of 8 waves per CU streams its share of the
 // (tile, quarter) row ranges — the settle's list of a scan wave with scan_R = kMfmaScanR — through an
 // LDS-DMA ring once; every wave scores its 32 queries against every staged row (lists per (quarter, query)
-// in LDS).  pilot = 1: each quarter's first 64 rows only, and per query the best lower-bound key of them to
-// pilot_keys [q][4·n_tiles].
+// in LDS).  It reads its own copy of the rows (launch_sq8w_build).  pilot = 1: each quarter's first step only,
+// and per query the best lower-bound key of it to pilot_keys [q][4·n_tiles].
 constexpr int kWideQB = 2;                      // 16-query MFMA blocks per wave
 constexpr int kWideWaves = 8;                   // two per SIMD
 constexpr int kWideQ = kWideWaves * 16 * kWideQB;   // queries per launch
 constexpr int kAuxGroupF4 = 22;                 // float4 per 16-row group of the tiled bound terms
 int sq8_wide_supported(int units8);
+int sq8_wide_ks(int units8);                    // its 64-dim slabs per row: 2, 4, 8 or 12
 hipError_t launch_sq8_wide(const Sq8Params& p, hipStream_t s, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
-// The wide kernel's bound terms, tiled per 16-row group of a segment (kAuxGroupF4 float4 = 352 B): s_x[16],
-// (s_x|q_x|)[16], |δ_x|[16], |x|²[16] (struct of arrays: a lane reads its 4 rows' terms in one ds_read_b128),
-// {max s|q|, max |δ|, max |x|², min |x|²} and {max s_x, min s_x, 0, 0} of the group's rows, then (COSINE) the
-// rows' device-order |x|² (xnorm; zeros without).  Rows past the last: zero terms, not in the extrema.  The
-// kernel stages the first 18 float4 (COSINE all 22) with the rows.
-hipError_t launch_sq8_aux_tile(const float4* aux, const float* xnorm, int64_t n_rows, float4* out, hipStream_t s);
+// The wide kernel's copy of a segment's fp32 rows (units float4 per row): int8 codes with ONE scale per
+// 16-row group (s_g = the group's max |x| / 127), in the MFMA-tiled layout (16-row blocks × sq8_wide_ks slabs of
+// 1 KiB, chunk-major), and per group kAuxGroupF4 float4 of bound terms (352 B): s_g[16], (s_g|q_x|)[16], |δ_x|[16],
+// |x|²[16] (struct of arrays: a lane reads its 4 rows' terms in one ds_read_b128), {max s|q|, max |δ|, max |x|²,
+// min |x|²}, {s_g, f_cos, zero-row flag, 0} (the quick test's per-group factor) and (COSINE) the rows' device-order
+// |x|² (xnorm; zeros without).  Rows past the last: zero codes and terms, not in the extrema.  The kernel stages
+// the first 18 float4 (COSINE all 22) with the rows.
+hipError_t launch_sq8w_build(const float4* rows, int64_t n_rows, int units, int units8, const float* xnorm, int cosine,
+                             void* codes, float4* auxt, hipStream_t s);
 // Per (tile, quarter) of a view: {max s|q|, max |δ|, max |x|², min |x|²} over its rows (the wide kernel's
 // quick-test terms, from the tiled bound terms' group maxima), out [4·n_tiles]
 hipError_t launch_wide_quarter_max(const TileDev* tiles, int n_tiles, const float4* const* auxt, float4* out,

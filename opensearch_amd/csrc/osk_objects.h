@@ -136,7 +136,8 @@ struct osk_seg {
     void* d_q8 = nullptr;
     float4* d_q8aux = nullptr;
     void* d_q8t = nullptr;    // the int8 rows in sq8_mfma's tiled layout (osk_seg_warm / first batched prefilter)
-    float4* d_q8auxt = nullptr;   // per 16-row group: the bound terms tiled for sq8_wide (launch_sq8_aux_tile), with d_q8t
+    void* d_q8w = nullptr;        // sq8_wide's copy: codes with one scale per 16-row group, tiled (launch_sq8w_build)
+    float4* d_q8auxt = nullptr;   // ...and its bound terms per 16-row group (built with d_q8t)
     void* d_q6 = nullptr;     // the 6-bit tier (dims with sq6_supported, tune sq6 on at staging): tiled codes,
     float4* d_q6aux = nullptr;   // built with the int8 copy; freed when the segment's calibration turns it off
     // The 6-bit tier's calibration, per segment: every view over the segment (a searcher's view, its
@@ -186,6 +187,7 @@ struct osk_view {
     float sq8_gam = 0.f, sq8_g2 = 0.f, sq8_cos_slack = 0.f;
     osk::DevBuf d_sq8_rows, d_sq8_aux, d_counters;   // counters: SettleParams::counters
     osk::DevBuf d_sq8_rows_t;                         // per segment: tiled int8 copy (sq8_mfma)
+    osk::DevBuf d_sq8_rows_w;                         // per segment: the wide kernel's group-scaled copy
     osk::DevBuf d_sq8_auxt, d_shard_quarter_begin;    // per segment: its tiled bound terms (sq8_wide); 4·shard_tile_begin
     osk::DevBuf d_quarter_bm;                         // per (wide tile, quarter): its rows' bound-term maxima
     // sq8_wide's own tiles (ensure_sq8t: quarters of ≈ R / (2·CUs) rows), their shard ranges and dispatch order

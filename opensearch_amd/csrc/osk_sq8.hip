@@ -1704,13 +1704,14 @@ static const SettleFn kSettle[9][2] = {OSK_SETTLE_ROW(4, 2),  OSK_SETTLE_ROW(8, 
                                        OSK_SETTLE_ROW(16, 4), OSK_SETTLE_ROW(16, 8), OSK_SETTLE_ROW(16, 12),
                                        OSK_SETTLE_ROW(32, 8), OSK_SETTLE_ROW(64, 8), OSK_SETTLE_ROW(64, 16)};
 
-// (the wide kernel takes rows of ≤ 256 dims, sq8_wide_supported: settle configs 0–3 only)
-static const SettleFn kSettleWide[4][2] = {
-    {sq8_settle_wide<4, 2, false>, sq8_settle_wide<4, 2, true>},    {sq8_settle_wide<8, 2, false>, sq8_settle_wide<8, 2, true>},
-    {sq8_settle_wide<8, 4, false>, sq8_settle_wide<8, 4, true>},    {sq8_settle_wide<16, 4, false>, sq8_settle_wide<16, 4, true>}};
+// (the wide kernel takes rows of ≤ 768 dims, sq8_wide_supported: settle configs 0–5)
+#define OSK_SETTLE_WIDE_ROW(L, V) {sq8_settle_wide<L, V, false>, sq8_settle_wide<L, V, true>}
+static const SettleFn kSettleWide[6][2] = {OSK_SETTLE_WIDE_ROW(4, 2),  OSK_SETTLE_WIDE_ROW(8, 2),
+                                           OSK_SETTLE_WIDE_ROW(8, 4),  OSK_SETTLE_WIDE_ROW(16, 4),
+                                           OSK_SETTLE_WIDE_ROW(16, 8), OSK_SETTLE_WIDE_ROW(16, 12)};
 
 hipError_t launch_sq8_settle_wide(int cfg, int nq, const SettleParams& p, hipStream_t s) {
-    if (p.accept || p.gtiles || !p.shard_tile_begin || p.k < 1 || p.k > 64 || cfg < 0 || cfg > 3) return hipErrorInvalidValue;
+    if (p.accept || p.gtiles || !p.shard_tile_begin || p.k < 1 || p.k > 64 || cfg < 0 || cfg > 5) return hipErrorInvalidValue;
     hipLaunchKernelGGL(kSettleWide[cfg][p.sim == SIM_EUCLIDEAN ? 1 : 0], dim3(p.n_shards, nq), dim3(kWideSettleThreads), 0,
                        s, p);
     return hipGetLastError();

@@ -3,28 +3,32 @@
 // sq8_mfma (osk_sq8.hip) takes 32 queries per launch, so a batch of B queries streams the int8 corpus
 // B / 32 times: at 100M × 96 and B = 1024 that is 32 passes over 14 GB, 91 ms per batch.  A
 // batched search is compute-light per byte — 96 int8 MACs per (row, query) — so the corpus is read once per
-// 256 queries here (C4 b1024: 38.7 ms):
+// 256 queries here:
 //
+//   * its own copy of each segment (launch_sq8w_build): int8 codes with ONE scale per 16-row group (the
+//     group's max |x| / 127), in the MFMA-tiled layout (16-row blocks, 1 KiB slabs per 64 dims), and per
+//     group the rows' bound terms with that scale plus the group's quick-test factor; KS = 2, 4, 8 or 12
+//     slabs (≤ 128, 256, 512, 768 dims);
 //   * persistent: one workgroup of 8 waves per CU takes every G-th (tile, quarter) of the tile order (tiles
-//     interleaved over shards) as one continuous stream of 128-row steps through a 4-deep LDS-DMA ring
-//     (global_load_lds_dwordx4); a quarter is exactly the row range of one scan-wave list of the settle
-//     (list = tile·4 + quarter), so the settle and the per-shard merge are sq8_mfma's;
-//   * a step is 8 groups of 16 rows: waves 0–3 load the groups' int8 slabs (chunk-major tiled copy: the
-//     lane-linear image is the MFMA A operand), waves 4–7 their bound terms (launch_sq8_aux_tile: struct of
-//     arrays, a lane's 4 rows in one ds_read_b128); one barrier per step;
-//   * each wave owns 32 of the launch's 256 queries: B fragments in VGPRs for the whole launch, 2 query
-//     blocks × KS v_mfma_i32_16x16x64_i8 per group, exact int32 dots;
-//   * the quick test per (row, query) is one fma and a compare (packed pairs): the bound's error terms are
-//     relaxed to the quarter's row maxima (launch_wide_quarter_max), so what stays per pair is I·s_x against a
-//     per-(quarter, query) threshold (EUCLIDEAN: a per-row affine function of |x|²) — provably no stricter
-//     than sq8_bounds' upper side (derivation at quick_consts).  A passing pair takes the precise bound in
-//     its own lane and, above the floor, is appended to its (quarter, query) list by an LDS atomic; lists
-//     that would fill go through sq8_mfma's ordered insertion (sorted once, best kKQ kept);
+//     interleaved over shards) as one continuous stream of steps (GPS groups of 16 rows) through an NS-deep
+//     LDS-DMA ring (global_load_lds_dwordx4); a quarter is exactly one list of the settle
+//     (sq8_settle_wide); one barrier per step;
+//   * waves 0–3 load a step's int8 slabs (the tiled image is lane-linear: it IS the MFMA A operand), waves 4–7
+//     its groups' bound terms; each wave owns 32 of the launch's 256 queries: B fragments in VGPRs for the
+//     whole launch, 2 query blocks × KS v_mfma_i32_16x16x64_i8 per group, exact int32 dots;
+//   * the quick test per group: every row of a group shares the scale s_g, so a lane's 4 rows pass the
+//     per-row test I·s_g ≥ c iff their MAXIMUM dot does — one integer max, one convert and one fma per
+//     (group, query block) and lane, then ONE wave vote per step (COSINE: the factor s_g / √(min |x|²)
+//     bounds every row's s_g / √|x|²).  Only a step with a passing pair takes the slow path: per-row tests,
+//     the precise bound in each passing pair's own lane and, above the floor, an append to its (quarter,
+//     query) list by an LDS atomic; lists that would fill go through sq8_mfma's ordered insertion.  The
+//     per-row test is relaxed to the quarter's row maxima (launch_wide_quarter_max) and is provably no
+//     stricter than sq8_bounds' upper side (derivation at quick_consts);
 //   * floors: pilot = 1 bounds each quarter's first step of rows (the best lower-bound key per query; their k-th
 //     per (query, shard) floors the main pass); the main pass runs in two launches — 1/phase of the quarters
 //     first, then the rest under floors raised to the k-th best list maximum of the first (launch_wide_floor;
 //     the sq8_mfma pilot argument: k distinct rows score ≥ T, a row with ub < T cannot enter or tie into the
-//     top k).  C4 b256: 3.7M → 0.97M insertions per search.
+//     top k).
 // Results are bit-identical to sq8_mfma's, the fp32 streaming scan's and the oracle's (tests/test_gpu_wide.py).
 #include <hip/hip_ext.h>
 
@@ -34,52 +38,107 @@
 
 namespace osk {
 
-int sq8_wide_supported(int u8) { return u8 >= 1 && u8 <= 16 ? 1 : 0; }   // KS = 2 (≤ 128 dims) or 4 (≤ 256)
+// KS (64-dim slabs) of the wide kernel for a row of u8 16-byte int8 units: 2, 4, 8 or 12 (≤ 768 dims)
+int sq8_wide_ks(int u8) { return u8 <= 8 ? 2 : u8 <= 16 ? 4 : u8 <= 32 ? 8 : 12; }
+int sq8_wide_supported(int u8) { return u8 >= 1 && u8 <= 48 ? 1 : 0; }
 
-// The wide kernel's bound terms per 16-row group (osk_internal.h, launch_sq8_aux_tile): one thread per float4.
-__global__ __launch_bounds__(kBlock) void sq8_aux_tile(const float4* __restrict__ aux, const float* __restrict__ xnorm,
-                                                       int64_t n_rows, float4* __restrict__ out) {
-    const int64_t ng = (n_rows + 15) / 16, total = ng * kAuxGroupF4;
-    for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < total; t += (int64_t)gridDim.x * kBlock) {
-        const int64_t g = t / kAuxGroupF4, r0 = g * 16;
-        const int slot = (int)(t - g * kAuxGroupF4);
-        float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (slot < 16 || slot >= 18) {   // component slot / 4 of rows 4·(slot % 4) … + 3 (slots 18–21: xnorm)
-            const int c = slot >> 2, rb = (slot & 3) * 4;   // (slot 18 → rows 8…: re-based below)
-            const int rbase = slot >= 18 ? (slot - 18) * 4 : rb;
-            float v[4];
-            for (int i = 0; i < 4; ++i) {
-                const int64_t r = r0 + rbase + i;
-                if (slot >= 18) {
-                    v[i] = (xnorm && r < n_rows) ? xnorm[r] : 0.0f;
-                } else {
-                    const float4 a = r < n_rows ? aux[r] : make_float4(0.f, 0.f, 0.f, 0.f);
-                    v[i] = c == 0 ? a.x : c == 1 ? a.y : c == 2 ? a.z : a.w;
+// The wide kernel's copy of a segment (launch_sq8w_build), one wave per 16-row group: the group's scale
+// s_g = max |x| over its rows / 127 (sq8_quantize's per-row formula over the group), codes
+// q = clamp(rint(x / s_g), ±127) written in the MFMA-tiled layout (lane l of slab j: row l & 15, 16-B unit
+// 4j + (l >> 4) — the lane-linear A operand), and the group's bound terms in the tiled struct-of-arrays layout
+// of kAuxGroupF4 float4 (osk_internal.h): per row {s_g, s_g·|q| ↑, |x − s_g·q| ↑, |x|²} (sq8_quantize's terms,
+// computed in double, ↑ = rounded up), {max s|q|, max |δ|, max |x|², min |x|²}, {s_g, f_cos, zero-row flag, 0}
+// and (COSINE) the rows' device-order |x|².  f_cos ≥ s_g / √|x|² of every row (rounded up, + 2^-20): the
+// COSINE quick test's per-group factor; a group with a zero row (COSINE) sets the flag instead (its pairs
+// always take the per-row test).  Rows past the last: zero codes and terms, not in the extrema.
+__global__ __launch_bounds__(kBlock) void sq8w_build(const float4* __restrict__ X, int64_t n_rows, int units, int ks,
+                                                     const float* __restrict__ xnorm, int cosine,
+                                                     int4* __restrict__ codes, float4* __restrict__ auxt) {
+    const int lane = threadIdx.x & 63, r = lane & 15, c = lane >> 4;
+    const int64_t ng = (n_rows + 15) / 16;
+    const int64_t wave_global = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int64_t n_waves = ((int64_t)gridDim.x * kBlock) >> 6;
+    for (int64_t g = wave_global; g < ng; g += n_waves) {
+        const int64_t row = g * 16 + r;
+        const bool valid = row < n_rows;
+        const float4* xr = X + (valid ? row : 0) * (int64_t)units;
+        float m = 0.0f;
+        for (int j = 0; j < ks; ++j)
+            for (int e = 0; e < 4; ++e) {
+                const int f = (4 * j + c) * 4 + e;   // fp32 float4 unit
+                if (valid && f < units) {
+                    const float4 x = xr[f];
+                    m = fmaxf(m, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
                 }
             }
-            o = make_float4(v[0], v[1], v[2], v[3]);
-        } else {
-            float y = 0.0f, z = 0.0f, w = 0.0f, wmin = __builtin_inff(), amax = 0.0f, amin = __builtin_inff();
-            for (int i = 0; i < 16 && r0 + i < n_rows; ++i) {
-                const float4 a = aux[r0 + i];
-                y = fmaxf(y, a.y);
-                z = fmaxf(z, a.z);
-                w = fmaxf(w, a.w);
-                wmin = fminf(wmin, a.w);
-                amax = fmaxf(amax, a.x);
-                amin = fminf(amin, a.x);
+        for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+        const float sg = m / 127.0f;
+        long long sq = 0;
+        double se = 0.0, sx = 0.0;
+        for (int j = 0; j < ks; ++j) {
+            uint32_t w4[4];
+            for (int e = 0; e < 4; ++e) {
+                const int f = (4 * j + c) * 4 + e;
+                uint32_t packed = 0u;
+                if (valid && f < units) {
+                    const float4 x = xr[f];
+                    const float xs[4] = {x.x, x.y, x.z, x.w};
+                    for (int t = 0; t < 4; ++t) {
+                        int qi = 0;
+                        if (sg > 0.0f) qi = (int)fminf(fmaxf(rintf(xs[t] / sg), -127.0f), 127.0f);
+                        packed |= ((uint32_t)qi & 0xFFu) << (8 * t);
+                        sq += (long long)(qi * qi);
+                        const double rr = (double)xs[t] - (double)sg * (double)qi;   // exact in double
+                        se += rr * rr;
+                        sx += (double)xs[t] * (double)xs[t];
+                    }
+                }
+                w4[e] = packed;
             }
-            o = slot == 16 ? make_float4(y, z, w, wmin) : make_float4(amax, amin, 0.0f, 0.0f);
+            codes[(g * ks + j) * 64 + lane] = make_int4((int)w4[0], (int)w4[1], (int)w4[2], (int)w4[3]);
         }
-        out[t] = o;
+        for (int o = 16; o <= 32; o <<= 1) {   // the row's 4 lanes (c = 0..3)
+            sq += __shfl_xor(sq, o);
+            se += __shfl_xor(se, o);
+            sx += __shfl_xor(sx, o);
+        }
+        const float A = valid ? f32_round_up((double)sg * sqrt((double)sq) * (1.0 + 1e-12)) : 0.0f;
+        const float B = valid ? f32_round_up(sqrt(se) * (1.0 + 1e-12)) : 0.0f;
+        const float W = valid ? (float)sx : 0.0f;
+        float mA = A, mB = B, mW = W, nW = valid ? W : __builtin_inff();
+        for (int o = 1; o <= 8; o <<= 1) {
+            mA = fmaxf(mA, __shfl_xor(mA, o));
+            mB = fmaxf(mB, __shfl_xor(mB, o));
+            mW = fmaxf(mW, __shfl_xor(mW, o));
+            nW = fminf(nW, __shfl_xor(nW, o));
+        }
+        float* af = reinterpret_cast<float*>(auxt + g * kAuxGroupF4);
+        if (c == 0) {
+            af[r] = valid ? sg : 0.0f;
+            af[16 + r] = A;
+            af[32 + r] = B;
+            af[48 + r] = W;
+            af[72 + r] = (cosine && valid && xnorm) ? xnorm[row] : 0.0f;
+        }
+        if (lane == 0) {
+            float fcos = 0.0f, zflag = 0.0f;
+            if (cosine) {
+                if (nW > 0.0f) fcos = f32_round_up((double)sg / sqrt((double)nW) * (1.0 + 0x1p-20));
+                else zflag = 1.0f;
+            }
+            auxt[g * kAuxGroupF4 + 16] = make_float4(mA, mB, mW, nW);
+            auxt[g * kAuxGroupF4 + 17] = make_float4(sg, fcos, zflag, 0.0f);
+        }
     }
 }
 
-hipError_t launch_sq8_aux_tile(const float4* aux, const float* xnorm, int64_t n_rows, float4* out, hipStream_t s) {
-    if (n_rows <= 0) return hipMemsetAsync(out, 0, (size_t)kAuxGroupF4 * sizeof(float4), s);
-    const int64_t total = (n_rows + 15) / 16 * kAuxGroupF4;
-    const int64_t blocks = std::min<int64_t>(8192, (total + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(sq8_aux_tile, dim3((unsigned)blocks), dim3(kBlock), 0, s, aux, xnorm, n_rows, out);
+hipError_t launch_sq8w_build(const float4* rows, int64_t n_rows, int units, int u8, const float* xnorm, int cosine,
+                             void* codes, float4* auxt, hipStream_t s) {
+    if (n_rows <= 0) return hipMemsetAsync(auxt, 0, (size_t)kAuxGroupF4 * sizeof(float4), s);
+    const int64_t ng = (n_rows + 15) / 16;
+    const int64_t blocks = std::min<int64_t>(8192, (ng + 3) / 4);
+    hipLaunchKernelGGL(sq8w_build, dim3((unsigned)blocks), dim3(kBlock), 0, s, rows, n_rows, units, sq8_wide_ks(u8),
+                       xnorm, cosine, static_cast<int4*>(codes), auxt);
     return hipGetLastError();
 }
 
@@ -228,8 +287,8 @@ __device__ __forceinline__ void quick_consts(float tq, float sb, float inv, floa
 // One quarter of a workgroup's share (persistent kernel), described once in LDS so that no global load of
 // tile or segment metadata sits between the ring's LDS-DMAs (a compiler-inserted vmcnt(0) would drain it).
 struct WideQuarter {
-    const int4* xt;       // the tiled int8 rows from the quarter's first 16-row group
-    const float4* at;     // the tiled bound terms from its first group (kAuxGroupF4 float4 per group)
+    const int4* xt;       // the wide copy's codes from the quarter's first 16-row group
+    const float4* at;     // the wide copy's bound terms from its first group (kAuxGroupF4 float4 per group)
     uint32_t vrow0;       // view row of its first row
     int32_t nrows;        // (the pilot: its first step's rows at most)
     int32_t list;         // tile·4 + quarter: the settle's list, the pilot's slot
@@ -241,36 +300,46 @@ struct WideQuarter {
 constexpr int kWideMaxFloorShards = 16;   // per-(shard, query) floors held in LDS up to this many shards
 constexpr int kWideThreads = kWideWaves * 64;
 constexpr int kWideSorted = 1 << 20;      // s_cnt of a list the ordered insertion has sorted
+constexpr int kWidePilotRows = 128;       // the pilot bounds each quarter's first 128 rows (1–4 steps)
+
+// The ring's geometry per KS: GPS 16-row groups per step (one barrier per step), NS steps in the ring, the
+// int8 slab DMAs per loader wave per step (waves 0–3: slab units w, w + 4, … of the step's GPS·KS) and the
+// bound-term DMAs per aux wave (waves 4 … 4 + min(GPS, 4) − 1: groups w − 4, w, …).  LDS: KS = 2 → 4 steps of
+// 8 groups (75 KB), 4 → 4 × 4 (71 KB), 8 → 4 × 2 (68 KB), 12 → 3 × 2 (76 KB), beside the lists (48 KB).
+template <int KS>
+struct WideGeom {
+    static constexpr int GPS = KS <= 4 ? 16 / KS : 2;
+    static constexpr int NS = KS <= 8 ? 4 : 3;
+    static constexpr int LPW = GPS * KS / 4;
+    static constexpr int APW = GPS >= 4 ? GPS / 4 : 1;
+};
 
 // Persistent: gridDim.x workgroups (one per CU), workgroup w takes quarters w, w + G, w + 2G, … of the
-// tile order (tiles interleaved over shards), as ONE continuous stream of 64-row steps through an NS-deep
-// LDS-DMA ring, so the ring never drains at a quarter boundary and the queries' B fragments, constants and
-// floors are set up once per launch.  8 waves, two per SIMD (one's MFMAs overlap the other's quick tests
-// and LDS latency): waves 0–3 load group w's KS int8 slabs of a step, waves 4–7 group w − 4's bound terms;
-// every wave scores its 32 queries against all 4 groups.  Each wave flushes its queries' lists when its
-// quarter ends.
-template <int KS, int HT, int SIM, int NS>
+// tile order (tiles interleaved over shards), as ONE continuous stream of steps through the NS-deep LDS-DMA
+// ring, so the ring never drains at a quarter boundary and the queries' B fragments, constants and floors
+// are set up once per launch.  8 waves, two per SIMD; every wave scores its 32 queries against every group
+// of a step.  Each wave flushes its queries' lists when its quarter ends.
+template <int KS, int SIM>
 __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
     typedef int i32x4 __attribute__((ext_vector_type(4)));
     typedef float f32x2 __attribute__((ext_vector_type(2)));
+    using Geo = WideGeom<KS>;
+    constexpr int GPS = Geo::GPS, NS = Geo::NS, LPW = Geo::LPW, APW = Geo::APW;
     constexpr int QB = kWideQB;
     constexpr int AUXF4 = SIM == SIM_COSINE ? kAuxGroupF4 : 18;   // staged float4 of a group's bound terms
-    constexpr int AUXB = AUXF4 * 16;          // a[16] y[16] z[16] w[16] {maxima} {a range} (COSINE: xnorm[16])
+    constexpr int AUXB = AUXF4 * 16;          // a[16] y[16] z[16] w[16] {maxima} {s_g, f_cos, zero} (COSINE: xnorm[16])
     constexpr int GB = KS * 1024 + AUXB;      // one 16-row group in a slot
-    constexpr int GPS = KS == 2 ? 8 : 4;      // 16-row groups per step (one barrier per step)
-    constexpr int PP = 0;                     // 1: waves 4–7 run a step's quick tests one step late (ping-pong;
-                                              // measured no faster), the ring then holds one more step
     constexpr int SLOT = GPS * GB;            // one step
     constexpr int sim = SIM;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int col = lane & 15, grp = lane >> 4;
-    const int gm = wave & 3;            // the groups of a step this wave loads: gm, gm + 4, …
-    const bool dma_rows = wave < 4;     // its int8 slabs (waves 0–3) or its bound terms (waves 4–7)
+    const bool dma_rows = wave < 4;                      // its int8 slabs (waves 0–3)…
+    const bool dma_aux = !dma_rows && wave - 4 < GPS;    // …or bound terms (waves 4 … 4 + min(GPS, 4) − 1)
     const int u8 = p.units8, S = p.n_shards;
     const bool pilot = p.pilot != 0;
 #ifdef OSK_TESTING
-    // A/B timing only (results wrong): 1 skip the quick tests and lists, 2 skip the MFMAs, 8 no barrier between steps, 16 no list / pilot-key stores, 32 quick tests without
-    // their insertions, 64 the ring alone (no step processing)
+    // A/B timing only (results wrong): 1 skip the quick tests and lists, 2 skip the MFMAs, 8 no barrier between
+    // steps, 16 no list / pilot-key stores, 32 quick tests without their insertions, 64 the ring alone
     const int ablate = p.ablate;
 #else
     constexpr int ablate = 0;
@@ -311,7 +380,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
         d.xt = p.rows8t[tile.seg] + (rb >> 4) * (KS * 64);
         d.at = p.auxt[tile.seg] + (rb >> 4) * kAuxGroupF4;
         d.vrow0 = (uint32_t)(p.seg_vrow[tile.seg] + rb);
-        d.nrows = (int32_t)(pilot ? min<int64_t>(16 * GPS, re - rb) : re - rb);   // the pilot: one step
+        d.nrows = (int32_t)(pilot ? min<int64_t>(kWidePilotRows, re - rb) : re - rb);   // the pilot: its first rows
         d.list = tix * 4 + quarter;
         d.shard = tile.shard;
         d.seg = tile.seg;
@@ -321,13 +390,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
 
     // this lane's queries: wq0 + qb·16 + col
     const int wq0 = wave * 16 * QB;
-    // the dims' K-steps: nf full 64-dim slabs, then (ht) a 32-dim tail, the first two chunks of slab nf (a
-    // slab with ≤ 2 of its 4 chunks in use; v_mfma_i32_16x16x32_i8: half the MFMA cycles, LDS reads and
-    // HBM bytes of that slab)
-    constexpr bool ht = HT != 0;
-    constexpr int nf = KS - HT;   // (dims short of the last slab compute zeros there: exact)
     i32x4 bfr[KS][QB];
-    long bfh[QB];   // the tail's B fragment: 8 B (chunk (grp >> 1) of slab nf, half grp & 1)
     float sb[QB], inv[QB], QY[QB], QZ[QB], Q0[QB], zq[QB], tq[QB], qnd[QB];   // qnd: |q|² in device lane order (COSINE)
     uint64_t tkey[QB], qvm[QB];
     const float QW = __double2float_ru((double)p.gam * (1.0 + 0x1p-18));
@@ -341,12 +404,6 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
             const int f = s * 4 + grp;
             const int4 v = (qv && f < u8) ? p.q8[(int64_t)qi * u8 + f] : make_int4(0, 0, 0, 0);
             bfr[s][qb] = i32x4{v.x, v.y, v.z, v.w};
-        }
-        {
-            const int f = nf * 4 + (grp >> 1);
-            const int4 v = (ht && qv && f < u8) ? p.q8[(int64_t)qi * u8 + f] : make_int4(0, 0, 0, 0);
-            bfh[qb] = (grp & 1) ? (long)(((uint64_t)(uint32_t)v.w << 32) | (uint32_t)v.z)
-                                : (long)(((uint64_t)(uint32_t)v.y << 32) | (uint32_t)v.x);
         }
         const float4 qc = qv ? p.qc[qi] : make_float4(0.f, 0.f, 0.f, 0.f);
         sb[qb] = qc.x;
@@ -376,56 +433,61 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
     for (int qb = 0; qb < QB; ++qb) {
 #pragma unroll
         for (int s = 0; s < KS; ++s) asm volatile("" ::"v"(bfr[s][qb]));
-        asm volatile("" ::"v"(bfh[qb]));
         asm volatile("" ::"v"(qnd[qb]), "v"(inv[qb]));
     }
 
-    // the workgroup's steps: its quarters' 64-row steps back to back (empty quarters take none)
-    auto steps_of = [&](int q) { return (s_quart[q].nrows + 16 * GPS - 1) / (16 * GPS); };
+    // the workgroup's steps: its quarters' steps back to back (empty quarters take none)
+    // (LDS values the whole wave reads alike: readfirstlane keeps the loop control in SGPRs)
+    auto steps_of = [&](int q) {
+        return __builtin_amdgcn_readfirstlane((s_quart[q].nrows + 16 * GPS - 1) / (16 * GPS));
+    };
     int total = 0;
     for (int q = 0; q < n_mine; ++q) total += steps_of(q);
+    total = __builtin_amdgcn_readfirstlane(total);
     const uint32_t ring_lds =
         __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem);
-    // a lane's tail fragment in its slab image (chunk-major: row lane & 15, 8 B at dims 8·(lane >> 4))
-    const uint32_t tail_off = (uint32_t)((lane >> 5) * 256 + (lane & 15) * 16 + ((lane >> 4) & 1) * 8);
     // a group's dots: acc[qb] = the int8 dots of its 16 rows (4·grp + r) with query block qb (column col)
     auto group_dots = [&](const char* gb, i32x4 (&ac)[QB]) {
 #pragma unroll
         for (int qb = 0; qb < QB; ++qb) ac[qb] = i32x4{0, 0, 0, 0};
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
-            if (s < nf) {
-                const i32x4 a = *reinterpret_cast<const i32x4*>(gb + s * 1024 + lane * 16);
+            const i32x4 a = *reinterpret_cast<const i32x4*>(gb + s * 1024 + lane * 16);
 #pragma unroll
-                for (int qb = 0; qb < QB; ++qb)
-                    ac[qb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bfr[s][qb], ac[qb], 0, 0, 0);
-            }
-        }
-        if (ht) {   // (own accumulators, added after: no K=64 → K=32 MFMA accumulator chain)
-            const long ah = *reinterpret_cast<const long*>(gb + nf * 1024 + tail_off);
-#pragma unroll
-            for (int qb = 0; qb < QB; ++qb)
-                ac[qb] += __builtin_amdgcn_mfma_i32_16x16x32_i8(ah, bfh[qb], i32x4{0, 0, 0, 0}, 0, 0, 0);
+            for (int qb = 0; qb < QB; ++qb) ac[qb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bfr[s][qb], ac[qb], 0, 0, 0);
         }
     };
     int iq = 0, ist = 0;   // the next step to issue: quarter iq of mine, its step ist
     while (iq < n_mine && steps_of(iq) == 0) ++iq;
     // this wave's part of the step → slot; groups past the quarter load its first group (valid, skipped)
+    auto rfl_ptr = [](const void* ptr) {
+        const uint64_t v = (uint64_t)ptr;
+        return (const char*)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+                             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v));
+    };
     auto issue = [&](int slot) {
+        // the quarter's descriptor in SGPRs first (each DMA's asm clobbers memory: re-reading it from LDS
+        // between DMAs would put an LDS wait before each)
         const WideQuarter& d = s_quart[iq];
+        const int nrows = __builtin_amdgcn_readfirstlane(d.nrows);
+        const int4* xt = reinterpret_cast<const int4*>(rfl_ptr(d.xt));
+        const float4* at = reinterpret_cast<const float4*>(rfl_ptr(d.at));
+        const uint32_t base = ring_lds + (uint32_t)(slot * SLOT);
+        if (dma_rows) {
 #pragma unroll
-        for (int h = 0; h < GPS / 4; ++h) {
-            const int gi = GPS * ist + gm + 4 * h;
-            const int gv = 16 * gi < d.nrows ? gi : 0;
-            const uint32_t dst = ring_lds + (uint32_t)(slot * SLOT + (gm + 4 * h) * GB);
-            if (dma_rows) {
-                const int4* src = d.xt + gv * (KS * 64);
+            for (int j = 0; j < LPW; ++j) {
+                const int u = wave + 4 * j, g = u / KS, s = u - g * KS;   // (wave-uniform)
+                const int gi = GPS * ist + g;
+                const int gv = 16 * gi < nrows ? gi : 0;
+                glds16(xt + gv * (KS * 64) + s * 64 + lane, base + (uint32_t)(g * GB + s * 1024));
+            }
+        } else if (dma_aux && lane < AUXF4) {
 #pragma unroll
-                for (int s = 0; s < KS; ++s)
-                    if (s < nf) glds16(src + s * 64 + lane, dst + s * 1024);   // (the slab image is lane-linear)
-                if (ht && lane < 32) glds16(src + nf * 64 + lane, dst + nf * 1024);
-            } else if (lane < AUXF4) {
-                glds16(d.at + gv * kAuxGroupF4 + lane, dst + KS * 1024);
+            for (int h = 0; h < APW; ++h) {
+                const int g = wave - 4 + 4 * h;
+                const int gi = GPS * ist + g;
+                const int gv = 16 * gi < nrows ? gi : 0;
+                glds16(at + gv * kAuxGroupF4 + lane, base + (uint32_t)(g * GB + KS * 1024));
             }
         }
         if (++ist == steps_of(iq)) {
@@ -445,7 +507,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
         ax[2] = make_float4(A.z, Y.z, Z.z, W.z);
         ax[3] = make_float4(A.w, Y.w, Z.w, W.w);
     };
-    // the quick test of the lane's 4 rows against one query: t_r = fma(I, a_r, −ca) (EUCLIDEAN
+    // the per-row quick test of the lane's 4 rows against one query: t_r = fma(I, a_r, −ca) (EUCLIDEAN
     // fma(I, a_r, −fma(w_r, ca, cb))), as packed pairs; pass = !(t_r < 0).  Rows past the quarter may pass
     // here (the insertion drops them).
     auto quick_t = [&](const i32x4& I, const float (&ar)[4], const float (&wr)[4], float c, float c2, f32x2& t01,
@@ -463,10 +525,10 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
         }
     };
 #ifdef OSK_TESTING
-    uint32_t n_events = 0, n_pairs = 0;   // insertion events (wave-uniform) and quick-test passes (per lane)
+    uint32_t n_events = 0, n_pairs = 0, n_slow = 0;   // insertion events, quick-test passes, slow-path steps
     uint64_t cyc_wait = 0, cyc_loop = 0;   // wave 0's clocks: the step loop's waits, the whole loop
 #endif
-    float ca[QB], cb[QB];   // the held step's quick-test constants
+    float ca[QB], cb[QB];   // the current quarter's quick-test constants
     // a quarter ends: its lists (this wave's queries, 4 per pass of 16 lanes) → the settle's arrays, zeroed
     auto flush = [&](const WideQuarter& d) {
         const int q_end = min(wq0 + 16 * QB, p.q_count);
@@ -510,58 +572,73 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
         }
     }
     if (total > 0) {
-        // Two waves per SIMD in ping-pong: waves 0–3 read and multiply step i, then run its quick tests;
-        // waves 4–7 first run step i − 1's quick tests (held in registers), then read and multiply step i.
-        // So one wave's MFMAs and LDS reads overlap the other's quick tests and insertions, and the ring keeps
-        // one more slot (step i − 1) readable: the DMA at step i targets step i − 2's slot.
-        const bool late = PP && wave >= 4;
-        for (int st = 0; st < NS - 1 - PP && st < total; ++st) issue(st);
-        int s_issue = (NS - 1 - PP) % NS, s_read = 0;
-        int pq = -1, pst = 0;   // the quarter of mine and its step that the next read starts from / reaches
-        // the held step (read and multiplied, quick tests pending)
-        bool held = false;
+        for (int st = 0; st < NS - 1 && st < total; ++st) issue(st);
+        int s_issue = (NS - 1) % NS, s_read = 0;
+        int pq = -1, pst = 0;   // the quarter of mine and its step the current step belongs to
         const char* hslot = smem;
         int hst = 0, hgroups = 0, hq = 0;
         i32x4 acc[GPS][QB];
+        uint64_t pbest[QB];   // the pilot: the current quarter's best lower-bound key per query so far
         float4 bm = make_float4(0.f, 0.f, 0.f, 0.f);
-        // the held step's quick tests and insertions
+        // the step's quick tests and insertions
         auto quick_phase = [&]() __attribute__((always_inline)) {
             const WideQuarter& hd = s_quart[hq];
-            float4 A4[GPS], W4[GPS];   // the groups' a_r, w_r of the lane's rows (re-read from the slot)
+            // (1) the fast test: per group, the lane's largest dot over its 4 rows against a factor common to
+            // the group's rows, ONE vote per step.  DOT / MIP: every row's factor is s_g, and fma(I, s_g, −c) is
+            // monotone in I, so t = fma(max I, s_g, −c) < 0 iff every row fails the per-row test.  COSINE: the
+            // per-row factor a_r·rsq(w_r) ≤ f_cos (2^-20 above s_g / √(min w), far beyond v_rsq's error), so with
+            // c > 0 (a row can pass only with I > 0) t = fma(max I, f_cos, −c) < 0 implies every row fails; with
+            // c ≤ 0 every pair takes the slow path, and so does a group with a zero row.  EUCLIDEAN: the per-row
+            // test itself (its threshold is affine in each row's |x|²), reduced to one vote per step.
+            float tf[GPS][QB];
+            bool zg[GPS];
 #pragma unroll
             for (int g = 0; g < GPS; ++g) {
-                A4[g] = *reinterpret_cast<const float4*>(hslot + g * GB + KS * 1024 + grp * 16);
-                W4[g] = (SIM == SIM_EUCLIDEAN || SIM == SIM_COSINE)
-                            ? *reinterpret_cast<const float4*>(hslot + g * GB + KS * 1024 + 192 + grp * 16)
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-            // the rows' quick-test factors: a_r (COSINE a_r/√w_r; a zero row's pairs pass), w_r (EUCLIDEAN)
-            float ar[GPS][4], wr[GPS][4];
-            bool zr[GPS];
+                const char* ga = hslot + g * GB + KS * 1024;
+                zg[g] = false;
+                if constexpr (SIM == SIM_EUCLIDEAN) {
+                    const float4 A4 = *reinterpret_cast<const float4*>(ga + grp * 16);
+                    const float4 W4 = *reinterpret_cast<const float4*>(ga + 192 + grp * 16);
+                    const float ar[4] = {A4.x, A4.y, A4.z, A4.w}, wr[4] = {W4.x, W4.y, W4.z, W4.w};
 #pragma unroll
-            for (int g = 0; g < GPS; ++g) {
-                ar[g][0] = A4[g].x; ar[g][1] = A4[g].y; ar[g][2] = A4[g].z; ar[g][3] = A4[g].w;
-                wr[g][0] = W4[g].x; wr[g][1] = W4[g].y; wr[g][2] = W4[g].z; wr[g][3] = W4[g].w;
-                zr[g] = false;
-                if constexpr (SIM == SIM_COSINE) {
+                    for (int qb = 0; qb < QB; ++qb) {
+                        f32x2 t01, t23;
+                        quick_t(acc[g][qb], ar, wr, ca[qb], cb[qb], t01, t23);
+                        tf[g][qb] = fmaxf(fmaxf(t01.x, t01.y), fmaxf(t23.x, t23.y));
+                    }
+                } else {
+                    const float4 gf = *reinterpret_cast<const float4*>(ga + 17 * 16);   // {s_g, f_cos, zero row, 0}
+                    const float f = SIM == SIM_COSINE ? gf.y : gf.x;
+                    if constexpr (SIM == SIM_COSINE) zg[g] = gf.z != 0.0f;   // (wave-uniform: one LDS word)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        zr[g] |= !(wr[g][r] > 0.0f);
-                        ar[g][r] = ar[g][r] * __builtin_amdgcn_rsqf(wr[g][r]);   // (0 · ∞ = NaN: passes)
+                    for (int qb = 0; qb < QB; ++qb) {
+                        const i32x4& I = acc[g][qb];
+                        const int M = max(max(I[0], I[1]), max(I[2], I[3]));
+                        const float c = (SIM == SIM_COSINE && !(ca[qb] > 0.0f)) ? -__builtin_inff() : ca[qb];
+                        tf[g][qb] = fmaf((float)M, f, -c);
                     }
                 }
             }
-            uint32_t qmg[GPS];   // per group: the wave's queries with a passing pair (wave-uniform)
+            float run = -__builtin_inff();
+            bool zany = false;
+#pragma unroll
+            for (int g = 0; g < GPS; ++g) {
+                zany = zany || zg[g];
+#pragma unroll
+                for (int qb = 0; qb < QB; ++qb) run = fmaxf(run, tf[g][qb]);
+            }
+            if (!__ballot(!(run < 0.0f)) && !zany) return;
+#ifdef OSK_TESTING
+            ++n_slow;
+#endif
+            // (2) the slow path: per group the wave's queries with a group that may pass (wave-uniform)
+            uint32_t qmg[GPS];
 #pragma unroll
             for (int g = 0; g < GPS; ++g) {
                 uint32_t qm = 0u;
 #pragma unroll
                 for (int qb = 0; qb < QB; ++qb) {
-                    f32x2 t01, t23;
-                    quick_t(acc[g][qb], ar[g], wr[g], ca[qb], cb[qb], t01, t23);
-                    const float mx = fmaxf(fmaxf(t01.x, t01.y), fmaxf(t23.x, t23.y));   // (NaN terms dropped)
-                    const bool any = !(mx < 0.0f) || zr[g];
-                    const uint64_t bl = __ballot(any) & qvm[qb];
+                    const uint64_t bl = __ballot(!(tf[g][qb] < 0.0f) || zg[g]) & qvm[qb];
                     qm |= (uint32_t)((bl | (bl >> 16) | (bl >> 32) | (bl >> 48)) & 0xFFFFull) << (16 * qb);
                 }
                 qmg[g] = g < hgroups ? qm : 0u;
@@ -570,28 +647,20 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
 #pragma unroll
             for (int g = 0; g < GPS; ++g) qany |= qmg[g];
             if (!qany || (ablate & 32)) return;
-#pragma unroll 1
-            for (int g = 0; g < hgroups; ++g) {
-                uint32_t qmgg = 0u;   // (g is wave-uniform: selects, no indexed register access)
-#pragma unroll
-                for (int gg = 0; gg < GPS; ++gg) qmgg = gg == g ? qmg[gg] : qmgg;
-                if (!qmgg) continue;
+            // group g's insertions, its dots in ac
+            auto event_group = [&](int g, const i32x4 (&ac)[QB], uint32_t qmgg) __attribute__((always_inline)) {
 #ifdef OSK_TESTING
                 n_events += __popc(qmgg);
 #endif
-                // group g's dots and row factors again, from its slot (no register array indexed by the
-                // runtime g: that would put the step's accumulators in scratch memory)
                 const char* gb = hslot + g * GB;
                 const char* ga = gb + KS * 1024;
-                i32x4 ac[QB];
-                group_dots(gb, ac);
                 const float4 Ag = *reinterpret_cast<const float4*>(ga + grp * 16);
                 const float4 Wg = *reinterpret_cast<const float4*>(ga + 192 + grp * 16);
                 float arg[4] = {Ag.x, Ag.y, Ag.z, Ag.w};
                 const float wrg[4] = {Wg.x, Wg.y, Wg.z, Wg.w};
                 if constexpr (SIM == SIM_COSINE) {
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) arg[r] = arg[r] * __builtin_amdgcn_rsqf(wrg[r]);
+                    for (int r = 0; r < 4; ++r) arg[r] = arg[r] * __builtin_amdgcn_rsqf(wrg[r]);   // (0 · ∞ = NaN: passes)
                 }
                 const int r0 = 16 * (GPS * hst + g);   // rows of the quarter
                 const int nr = min(16, hd.nrows - r0);
@@ -683,42 +752,51 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                         }
                     }
                 }
+            };
+            if constexpr (GPS <= 2) {   // the step's accumulators are still here (static indices: unrolled)
+#pragma unroll
+                for (int g = 0; g < GPS; ++g)
+                    if (g < hgroups && qmg[g]) event_group(g, acc[g], qmg[g]);
+            } else {
+#pragma unroll 1
+                for (int g = 0; g < hgroups; ++g) {
+                    uint32_t qmgg = 0u;   // (g is wave-uniform: selects, no indexed register access)
+#pragma unroll
+                    for (int gg = 0; gg < GPS; ++gg) qmgg = gg == g ? qmg[gg] : qmgg;
+                    if (!qmgg) continue;
+                    // group g's dots again, from its slot (no register array indexed by the runtime g: that
+                    // would put the step's accumulators in scratch memory)
+                    i32x4 ac[QB];
+                    group_dots(hslot + g * GB, ac);
+                    event_group(g, ac, qmgg);
+                }
             }
         };
 #ifdef OSK_TESTING
         const uint64_t c_loop0 = clock64();
 #endif
-        // (one iteration past the last step: the late waves' quick tests of it; one call site of each phase)
-        for (int i = 0; i <= total; ++i) {
-            if (i < total) {
+        for (int i = 0; i < total; ++i) {
 #ifdef OSK_TESTING
-                const uint64_t c0 = clock64();
+            const uint64_t c0 = clock64();
 #endif
-                // this wave's DMAs of step i have landed (steps i+1 … i+NS−3 may still be in flight); every
-                // wave's have once all pass the barrier, which also retires every wave's reads of step i − 2's slot
-                if (i + NS - 1 - PP <= total) {   // (this wave's LDS-DMA instructions per step: GPS/4 · …)
-                    if (dma_rows) vm_wait<(NS - 2 - PP) * (GPS / 4) * (nf + HT)>();
-                    else vm_wait<(NS - 2 - PP) * (GPS / 4)>();
-                } else {
-                    vm_wait<0>();
-                }
-                if (!(ablate & 8)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            // this wave's DMAs of step i have landed (steps i+1 … i+NS−2 may still be in flight); every wave's
+            // have once all pass the barrier, which also retires every wave's reads of step i − 1's slot
+            if (i + NS - 1 <= total) {
+                if (dma_rows) vm_wait<(NS - 2) * LPW>();
+                else if (dma_aux) vm_wait<(NS - 2) * APW>();
+                else vm_wait<0>();
+            } else {
+                vm_wait<0>();
+            }
+            if (!(ablate & 8)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #ifdef OSK_TESTING
-                cyc_wait += clock64() - c0;
+            cyc_wait += clock64() - c0;
 #endif
-                if (i + NS - 1 - PP < total) {
-                    issue(s_issue);
-                    s_issue = s_issue + 1 == NS ? 0 : s_issue + 1;
-                }
+            if (i + NS - 1 < total) {
+                issue(s_issue);
+                s_issue = s_issue + 1 == NS ? 0 : s_issue + 1;
             }
             if (ablate & 64) continue;   // (A/B: the ring alone)
-#pragma unroll 1
-            for (int ph = 0; ph < 2; ++ph) {
-            if (held && (late ? ph == 0 : ph == 1)) {
-                quick_phase();
-                held = false;
-            }
-            if (ph == 1 || i == total) continue;
             if (pq < 0 || ++pst == steps_of(pq)) {   // a new quarter: flush the last one, take its floors
                 if (pq >= 0 && !pilot) flush(s_quart[pq]);
                 do ++pq; while (steps_of(pq) == 0);
@@ -743,20 +821,20 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
             s_read = s_read + 1 == NS ? 0 : s_read + 1;
             hq = pq;
             hst = pst;
-            hgroups = min(GPS, ((s_quart[pq].nrows + 15) >> 4) - GPS * pst);   // (< GPS: the quarter's last step)
-            if (pilot) {
+            hgroups = __builtin_amdgcn_readfirstlane(min(GPS, ((s_quart[pq].nrows + 15) >> 4) - GPS * pst));   // (< GPS: the quarter's last step)
+            if (pilot) {   // the quarter's first rows: per query the best lower-bound key → pilot_keys
                 const WideQuarter& hd = s_quart[hq];
-            {   // the quarter's first 64 rows: per query the best lower-bound key → pilot_keys
-                uint64_t pbest[QB];
+                if (pst == 0) {
 #pragma unroll
-                for (int qb = 0; qb < QB; ++qb) pbest[qb] = 0ull;
+                    for (int qb = 0; qb < QB; ++qb) pbest[qb] = 0ull;
+                }
 #pragma unroll 1
                 for (int g = 0; g < hgroups; ++g) {
                     const char* gb = hslot + g * GB;
                     const char* ga = gb + KS * 1024;
-                    const int r0 = 16 * g, nr = min(16, hd.nrows - r0);
-                    i32x4 acc[QB];
-                    group_dots(gb, acc);
+                    const int r0 = 16 * (GPS * hst + g), nr = min(16, hd.nrows - r0);
+                    i32x4 pacc[QB];
+                    group_dots(gb, pacc);
                     float4 ax[4];
                     row_terms(ga, ax);
 #pragma unroll
@@ -770,7 +848,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                             float xnd = 0.0f;
                             if constexpr (SIM == SIM_COSINE) xnd = *reinterpret_cast<const float*>(ga + 288 + rr * 4);
                             float lo, hi;
-                            sq8_bounds(sim, (float)acc[qb][r], ax[r], qc, p.gam, p.g2, lo, hi);
+                            sq8_bounds(sim, (float)pacc[qb][r], ax[r], qc, p.gam, p.g2, lo, hi);
                             const float lb = SIM == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qnd[qb], xnd);
                             const uint64_t key = rr < nr ? make_key(lb, hd.vrow0 + (uint32_t)(r0 + rr)) : 0ull;
                             best = key > best ? key : best;
@@ -784,6 +862,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                         pbest[qb] = best > pbest[qb] ? best : pbest[qb];
                     }
                 }
+                if (pst + 1 < steps_of(pq)) continue;   // (the quarter's last pilot step writes its keys)
 #pragma unroll
                 for (int qb = 0; qb < QB; ++qb) {
                     const int qi = wq0 + qb * 16 + col;
@@ -792,24 +871,10 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                     // the two-pass main pass reads the second pass's list maxima as empty until it writes them
                     if (grp == 0 && qi < p.q_count) p.list_lbmax[(size_t)(p.q0 + qi) * p.n_lists + hd.list] = 0u;
                 }
-            }
                 continue;
             }
-            {   // read and multiply step i
-                const char* slot = hslot;
-            // Every LDS read of the step first (the 4 groups' A fragments and maxima), then the step's 4·KS·QB
-            // MFMAs as straight-line code: one exposed LDS latency per step.  Groups past the quarter's end (its
-            // last step) hold valid rows of its first group; their passes are masked.
-            i32x4 a[GPS][KS];
-            long ah[GPS];
-#pragma unroll
-            for (int g = 0; g < GPS; ++g) {
-                const char* gb = slot + g * GB;
-#pragma unroll
-                for (int s = 0; s < KS; ++s)
-                    a[g][s] = s < nf ? *reinterpret_cast<const i32x4*>(gb + s * 1024 + lane * 16) : i32x4{0, 0, 0, 0};
-                ah[g] = ht ? *reinterpret_cast<const long*>(gb + nf * 1024 + tail_off) : 0l;
-            }
+            // read and multiply the step: every LDS read of a group's A fragments, then its KS·QB MFMAs as
+            // straight-line code (≤ 256 dims: every group's reads first, one exposed LDS latency per step)
 #pragma unroll
             for (int g = 0; g < GPS; ++g)
 #pragma unroll
@@ -818,30 +883,30 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
 #pragma unroll
                 for (int g = 0; g < GPS; ++g)
 #pragma unroll
-                    for (int s = 0; s < KS; ++s) acc[g][0] ^= a[g][s];
-            } else {
+                    for (int s = 0; s < KS; ++s)
+                        acc[g][0] ^= *reinterpret_cast<const i32x4*>(hslot + g * GB + s * 1024 + lane * 16);
+            } else if constexpr (KS <= 4) {
+                i32x4 a[GPS][KS];
 #pragma unroll
-                for (int g = 0; g < GPS; ++g) {
+                for (int g = 0; g < GPS; ++g)
+#pragma unroll
+                    for (int s = 0; s < KS; ++s) a[g][s] = *reinterpret_cast<const i32x4*>(hslot + g * GB + s * 1024 + lane * 16);
+#pragma unroll
+                for (int g = 0; g < GPS; ++g)
 #pragma unroll
                     for (int s = 0; s < KS; ++s)
-                        if (s < nf)
-#pragma unroll
-                            for (int qb = 0; qb < QB; ++qb)
-                                acc[g][qb] =
-                                    __builtin_amdgcn_mfma_i32_16x16x64_i8(a[g][s], bfr[s][qb], acc[g][qb], 0, 0, 0);
-                    if (ht)   // (own accumulators, added after: no K=64 → K=32 MFMA accumulator chain)
 #pragma unroll
                         for (int qb = 0; qb < QB; ++qb)
-                            acc[g][qb] += __builtin_amdgcn_mfma_i32_16x16x32_i8(ah[g], bfh[qb], i32x4{0, 0, 0, 0}, 0, 0, 0);
-                }
+                            acc[g][qb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[g][s], bfr[s][qb], acc[g][qb], 0, 0, 0);
+            } else {
+#pragma unroll
+                for (int g = 0; g < GPS; ++g) group_dots(hslot + g * GB, acc[g]);
             }
             if (ablate & 1) {
-                if (acc[0][0][0] + acc[3][QB - 1][3] == 0x7FFFFFFF && bm.x == 1.0f) s_lp[tid] = 1u;
-                held = false;
+                if (acc[0][0][0] + acc[GPS - 1][QB - 1][3] == 0x7FFFFFFF && bm.x == 1.0f) s_lp[tid] = 1u;
+                continue;
             }
-            }
-            held = !(ablate & 1);
-            }
+            quick_phase();
         }
         vm_wait<0>();
 #ifdef OSK_TESTING
@@ -856,6 +921,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
         if (lane == 0) {
             atomicAdd(&p.counters[4], (unsigned long long)n_events);
             atomicAdd(&p.counters[5], (unsigned long long)n_pairs);
+            atomicAdd(&p.counters[7], (unsigned long long)n_slow);
             if (wave == 0) {
                 atomicAdd(&p.counters[6], (unsigned long long)cyc_wait);
                 atomicAdd(&p.counters[8], (unsigned long long)cyc_loop);
@@ -866,19 +932,19 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
 }
 
 using WideFn = void (*)(Sq8Params);
-// ring depth per KS: the deepest ring that leaves room for the lists, the floors of ≤ 16 shards and the
-// quarter descriptors in 160 KiB (one workgroup per CU): KS = 2 → 8 steps (75 KB), KS = 4 → 4 (70 KB)
-#define OSK_WIDE_SIMS(KS, HT, NS) \
-    {sq8_wide<KS, HT, 0, NS>, sq8_wide<KS, HT, 1, NS>, sq8_wide<KS, HT, 2, NS>, sq8_wide<KS, HT, 3, NS>}
-// [KS = 4][HT]: HT = 1 when the last slab holds ≤ 2 chunks of dims (u8 ≤ 6 / ≤ 14; fewer dims: zero slabs)
-static const WideFn kWide[2][2][4] = {{OSK_WIDE_SIMS(2, 0, 4), OSK_WIDE_SIMS(2, 1, 4)},
-                                      {OSK_WIDE_SIMS(4, 0, 4), OSK_WIDE_SIMS(4, 1, 4)}};
-static constexpr int kWideNS[2] = {4, 4};
+#define OSK_WIDE_SIMS(KS) {sq8_wide<KS, 0>, sq8_wide<KS, 1>, sq8_wide<KS, 2>, sq8_wide<KS, 3>}
+static const WideFn kWide[4][4] = {OSK_WIDE_SIMS(2), OSK_WIDE_SIMS(4), OSK_WIDE_SIMS(8), OSK_WIDE_SIMS(12)};
 static constexpr size_t kLdsCap = 160 * 1024;
 
+template <int KS>
+static size_t wide_ring_bytes(int sim) {
+    using Geo = WideGeom<KS>;
+    return (size_t)Geo::NS * Geo::GPS * (KS * 1024 + (sim == SIM_COSINE ? kAuxGroupF4 : 18) * 16);
+}
 static size_t sq8_wide_lds(int ks, int sim, int n_shards, int n_mine) {
-    const size_t slot = (size_t)(ks == 2 ? 8 : 4) * (ks * 1024 + (sim == SIM_COSINE ? kAuxGroupF4 : 18) * 16);
-    return (size_t)kWideNS[ks == 4] * slot + (size_t)kWideQ * kKQ * 12 + (size_t)kWideQ * 16 + (size_t)kWideQ * 4 +
+    const size_t ring = ks == 2 ? wide_ring_bytes<2>(sim) : ks == 4 ? wide_ring_bytes<4>(sim)
+                      : ks == 8 ? wide_ring_bytes<8>(sim) : wide_ring_bytes<12>(sim);
+    return ring + (size_t)kWideQ * kKQ * 12 + (size_t)kWideQ * 16 + (size_t)kWideQ * 4 +
            (n_shards <= kWideMaxFloorShards ? (size_t)n_shards * kWideQ * 4 : 0) + (size_t)n_mine * sizeof(WideQuarter);
 }
 
@@ -887,9 +953,8 @@ hipError_t launch_sq8_wide(const Sq8Params& p, hipStream_t s, hipEvent_t ev_star
         p.sim < 0 || p.sim > 3 || !p.rows8t || !p.auxt || p.n_lists != 4 * p.n_tiles || p.k < 1 || p.k > kKQ ||
         p.n_shards < 1 || p.wide_grid < 1 || (p.pilot && !p.pilot_keys) || (!p.pilot && !p.quarter_bm))
         return hipErrorInvalidValue;
-    const int ks = p.units8 <= 8 ? 2 : 4;
-    const int ht = 0;   // (the K = 32 tail variant measured slower: C4 b256 13.3 vs 12.7 ms; kept for study)
-    const auto fn = kWide[ks == 4][ht][p.sim];
+    const int ks = sq8_wide_ks(p.units8);
+    const auto fn = kWide[ks == 2 ? 0 : ks == 4 ? 1 : ks == 8 ? 2 : 3][p.sim];
     const int nq4 = (p.quarter_end > 0 ? p.quarter_end : 4 * p.n_tiles) - p.quarter_begin;
     if (p.quarter_begin < 0 || nq4 < 1 || p.quarter_begin + nq4 > 4 * p.n_tiles || (p.quarter_begin && p.pilot))
         return hipErrorInvalidValue;

@@ -89,6 +89,12 @@ class DeviceComm:
         rc = lib().osk_comm_status(self._h, info)
         return rc, list(info)
 
+    def set_device_limits(self, max_queries: int, max_k: int, max_shards_per_rank: int) -> None:
+        """The device entry's exchange limits (osk_comm_set_device_limits): at world > 1 every
+        osk_shards_search_merge_device call all-gathers a block of this fixed size, so ranks whose calls
+        differ get count −1 instead of an all-gather of mismatched counts.  Same values on every rank."""
+        check(lib().osk_comm_set_device_limits(self._h, max_queries, max_k, max_shards_per_rank))
+
     @classmethod
     def from_process_group(cls, device: int, group=None) -> "DeviceComm":
         """Rank 0 makes the id; torch.distributed (any backend) hands it to the other ranks."""

@@ -80,6 +80,10 @@ def _worker(rank, world, name, mode, out_q):
 
             view = make_view()
             comm = D.DeviceComm.init_loopback(0, rank, world, name)
+            if mode == "over":
+                comm.set_device_limits(1, 10, spr)
+            else:   # (every rank alike: the device entry's fixed exchange block)
+                comm.set_device_limits(165, 100, spr)
             stream = torch.cuda.Stream()
 
             def device_call(nq, k, from_, size, qs):
@@ -120,6 +124,30 @@ def _worker(rank, world, name, mode, out_q):
                 stream.synchronize()
                 rc, info = comm.status()
                 results = [res[3].cpu().numpy().copy(), rc]
+            elif mode == "devnq":
+                # device entry, another batch size on rank 1: the block gather has the communicator's fixed
+                # size on both ranks (no RCCL count mismatch), the header check reports count −1 on both
+                nq = 1 if rank == 0 else 2
+                first = device_call(nq, 10, 0, 10, 5)
+                rc, info = comm.status()
+                results = [first[3].tolist(), rc, info]
+            elif mode == "devk":
+                # device entry, another k on rank 1 (same batch): also only a header difference
+                first = device_call(1, 10 if rank == 0 else 12, 0, 10, 5)
+                rc, info = comm.status()
+                results = [first[3].tolist(), rc, info]
+            elif mode == "over":
+                # rank 1 passes a batch beyond the limits (1 query): it still issues the collective (with a
+                # refusal header) and returns OSK_ERR_INVALID; rank 0's call reports count −1
+                nq = 1 if rank == 0 else 2
+                try:
+                    first = device_call(nq, 10, 0, 10, 5)
+                    results = ["ok", first[3].tolist()]
+                except _lib.OskError as e:
+                    stream.synchronize()
+                    results = [e.code, str(e)]
+                rc, info = comm.status()
+                results += [rc, info[0]]
             elif mode == "misnq":
                 # host entry, another batch size on rank 1: caught by the fixed-size call agreement before
                 # the (differently sized) block gather
@@ -234,6 +262,26 @@ def test_batches_differing_only_in_the_last_query_are_caught():
     for r in range(2):
         counts, rc = out[r]
         assert (counts == -1).all() and rc == -1, (r, counts[:4], rc)
+
+
+@pytest.mark.parametrize("mode", ["devnq", "devk"])
+def test_device_entry_mismatched_batch_or_k_gives_count_minus_one_no_hang(mode):
+    """The device entry never waits on the host, so it cannot agree on the gather's size first: its block has
+    the communicator's fixed size (osk_comm_set_device_limits) and a rank with another batch or k is a header
+    difference — count −1 and a poisoned communicator on both ranks, not two all-gathers of different counts."""
+    out = _run(2, mode)
+    for r in range(2):
+        counts, rc, info = out[r]
+        assert all(c == -1 for c in counts), (r, counts)
+        assert rc == -1 and info[0] == 1, (r, rc, info)
+
+
+def test_device_entry_call_beyond_the_limits_is_refused_on_every_rank():
+    out = _run(2, "over")
+    assert out[0][0] == "ok" and out[0][1] == [-1], out[0]
+    assert out[0][2] == -1 and out[0][3] == 1
+    assert out[1][0] == -1 and "device limits" in out[1][1], out[1]
+    assert out[1][2] == -1 and out[1][3] == 1
 
 
 def test_mismatched_batch_size_fails_the_host_entry_before_the_gather():

@@ -7,10 +7,10 @@ that size is checked against the oracle — docs, shard indices and score bits o
 * C3-shaped 6.5M × 768 COSINE, 8 shards: batch 1 on the 6-bit tier (sq6_pilot + sq6_scan + the int8
   re-bound, DESIGN.md §3f — the headline kernel), both on a calibration probe and in the steady state
   after the segments' calibration has kept the tier, batch 32 on
-  the int8 MFMA prefilter (sq8_mfma, register path at 768 dims), batch 256 on the bf16×3 MFMA
-  candidate path, batches 128 / 160 / 192 on whichever path the library's cost model picks (the
-  test restates the model and asserts the choice), and a 10 %-filtered single query (compacted
-  gather scan);
+  the int8 MFMA prefilter (sq8_mfma, register path at 768 dims), batches 128 / 160 / 192 / 256 on
+  whichever path the library's cost model picks (the wide int8 prefilter at KS = 12; the test restates
+  the model and asserts the choice), b256 also forced onto the bf16×3 MFMA candidate path, and a
+  10 %-filtered single query (compacted gather scan);
 * C4-shaped 6.5M × 96, DOT_PRODUCT and MAXIMUM_INNER_PRODUCT: batches 32 and 1024 on the LDS-DMA
   ring instance of sq8_mfma;
 * C2 1M × 128 EUCLIDEAN (SIFT-like), one shard, batch 256 on bf16×3;
@@ -80,9 +80,13 @@ def _sample(n, m, seed):
 
 
 # ---- the library's path cost model, restated (osk_api.hip view_search_device) -------
-def _wide_us(rows, dim, nq):
+def _wide_ks(dim):
     u8 = (dim + 15) // 16
-    return ((nq + 255) // 256) * (rows * (2.0 if u8 <= 8 else 4.0) * 0.0454e-3 + 300.0)
+    return 2 if u8 <= 8 else 4 if u8 <= 16 else 8 if u8 <= 32 else 12
+
+
+def _wide_us(rows, dim, nq):
+    return ((nq + 255) // 256) * (rows * _wide_ks(dim) * 0.0454e-3 + 300.0)
 
 
 def _narrow_us(rows, dim, nq):
@@ -90,8 +94,8 @@ def _narrow_us(rows, dim, nq):
 
 
 def _takes_wide(rows, dim, nq):
-    """osk_api.hip sq8_wide_pick: unfiltered batches of >= 64 queries of <= 256 dims, when cheaper."""
-    return dim <= 256 and nq >= 64 and _wide_us(rows, dim, nq) <= _narrow_us(rows, dim, nq)
+    """osk_api.hip sq8_wide_pick: unfiltered batches of >= 64 queries of <= 768 dims, when cheaper."""
+    return dim <= 768 and nq >= 64 and _wide_us(rows, dim, nq) <= _narrow_us(rows, dim, nq)
 
 
 def _takes_bf16x3(rows, dim, nq, k=10):
@@ -154,10 +158,21 @@ def test_c3_b32_sq8_mfma(c3):
     _check(out, want["b32"], samp["b32"], 10)
 
 
-def test_c3_b256_bf16x3(c3):
+def test_c3_b256_wide_and_bf16x3(c3):
+    """C3 b256: the cost model's pick is the wide int8 prefilter at 768 dims (KS = 12, one corpus pass per 256
+    queries); bf16×3 forced (the prefilter priced out) equals the oracle too."""
     ds, q, samp, want = c3
-    out, d = _search_counted(ds, q["b256"])
-    assert d["mfma_calls"] == 1 and d["sq8_calls"] == 0
+    counters = ("sq8_calls", "mfma_calls", "sq8_wide_calls")
+    assert _takes_wide(N_SHARDS * C3_RPS, C3_DIM, 256) and not _takes_bf16x3(N_SHARDS * C3_RPS, C3_DIM, 256)
+    out, d = _search_counted(ds, q["b256"], counters=counters)
+    assert d == {"sq8_calls": 1, "mfma_calls": 0, "sq8_wide_calls": 1}, d
+    _check(out, want["b256"], samp["b256"], 10)
+    _lib.tune("sq8_cost_pct", 100000)
+    try:
+        out, d = _search_counted(ds, q["b256"], counters=counters)
+    finally:
+        _lib.tune("sq8_cost_pct", 100)
+    assert d == {"sq8_calls": 0, "mfma_calls": 1, "sq8_wide_calls": 0}, d
     _check(out, want["b256"], samp["b256"], 10)
 
 
@@ -165,10 +180,10 @@ def test_c3_b256_bf16x3(c3):
 def test_c3_path_choice_follows_the_cost_model(c3, b):
     ds, q, samp, want = c3
     rows = N_SHARDS * C3_RPS
-    bf = _takes_bf16x3(rows, C3_DIM, b)
-    assert bf == (b >= 160)   # 768-dim rows switch at about 160 queries
-    out, d = _search_counted(ds, q[f"b{b}"])
-    assert d == ({"sq8_calls": 0, "mfma_calls": 1} if bf else {"sq8_calls": 1, "mfma_calls": 0})
+    wide, bf = _takes_wide(rows, C3_DIM, b), _takes_bf16x3(rows, C3_DIM, b)
+    assert wide and not bf   # 768-dim batches of ≥ 64 take the wide kernel
+    out, d = _search_counted(ds, q[f"b{b}"], counters=("sq8_calls", "mfma_calls", "sq8_wide_calls"))
+    assert d == {"sq8_calls": 1, "mfma_calls": 0, "sq8_wide_calls": 1}, d
     _check(out, want[f"b{b}"], samp[f"b{b}"], 10)
 
 

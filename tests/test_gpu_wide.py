@@ -4,7 +4,7 @@ Large unfiltered batches of float32 rows of ≤ 256 dims read the int8 corpus on
 quick test is relaxed to per-step row maxima and its lists are per (quarter, query), so every result must
 still equal the fp32 streaming scan (tune "sq8" 0), sq8_mfma (tune "sq8_wide_min" 0) and the oracle's
 device-order exactSearch + TopDocs.merge bit for bit: docs, score bits, tie order, shard indices.
-Covered: every similarity, dims 1…256 (KS = 2 and 4), batches that are not multiples of 16, 64 or 256
+Covered: every similarity, dims 1…768 (KS = 2, 4, 8 and 12), batches that are not multiples of 16, 64 or 256
 (partial query blocks, idle waves, several launches), k 1…12, ragged multi-segment multi-shard views with
 partial 16-row groups and 1-row segments, heavy ties, zero and constant rows, a zero query, and the
 pilot floor on data where most rows tie.
@@ -99,7 +99,7 @@ def defaults():
     _lib.tune("sq8_wide_force", 0)
 
 
-@pytest.mark.parametrize("dim", [1, 17, 64, 96, 100, 128, 129, 200, 256])
+@pytest.mark.parametrize("dim", [1, 17, 64, 96, 100, 128, 129, 200, 256, 257, 400, 512, 513, 700, 768])
 @pytest.mark.parametrize("sim", SIMS, ids=lambda s: s.name)
 def test_wide_equals_mfma_scan_and_oracle(dim, sim):
     sizes = [7001, 1, 2999, 16, 4100]

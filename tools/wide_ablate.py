@@ -53,6 +53,7 @@ for ab in [int(x) for x in os.environ.get("ABLATE", "0,1,2,3").split(",")]:
     e0, p0, w0 = counter("sq8_wide_events"), counter("sq8_wide_pairs"), counter("sq8_wide_calls")
     x0 = [counter(c) for c in ("sq8_fallback_queries", "sq8_exact_tiles", "sq8_rescored_rows")]
     cyc0 = [counter("sq8_wide_" + c + "_cycles") for c in ("wait", "loop")]
+    slow0 = counter("sq8_wide_slow_steps")
     check(lib().osk_view_profile(shards.view, 1))
     n = 5
     for _ in range(n):
@@ -69,6 +70,11 @@ for ab in [int(x) for x in os.environ.get("ABLATE", "0,1,2,3").split(",")]:
     print(f"   settle per search: fallback queries {x1[0] / n:.1f}, exactly re-scanned lists {x1[1] / n:.1f}, "
           f"re-scored rows {x1[2] / n:.0f}", flush=True)
     cyc = [counter("sq8_wide_" + c + "_cycles") - c0 for c0, c in zip(cyc0, ("wait", "loop"))]
+    slow = counter("sq8_wide_slow_steps") - slow0
+    rows = NS * RPS
+    wave_steps = launches * (rows / 16.0) * 8 / ({96: 8, 128: 8, 768: 2}.get(DIM, 4))
+    print(f"   wave-steps on the slow path per search: {slow / n:.0f} ({slow / max(1.0, wave_steps):.3f} of "
+          f"≈{wave_steps / n:.0f})", flush=True)
     # wave 0's shader clocks summed over workgroups (pilot + main): per workgroup per search, and the split
     wgs = 256 * 2 * n
     print(f"   clocks per wg-launch (wave 0): loop {cyc[1] / wgs:.0f}, wait+barrier {cyc[0] / wgs:.0f} "
