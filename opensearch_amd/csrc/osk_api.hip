@@ -317,6 +317,9 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         {"sq8_wide_phase", &g_tuning.sq8_wide_phase, 0, 1 << 16, false},
         {"sq8_wide_grid", &g_tuning.sq8_wide_grid, 0, 1 << 16, false},
         {"sq8_wide_quarter_rows", &g_tuning.sq8_wide_quarter_rows, 0, 1 << 20, false},
+        {"sq8_wide_pilot_rows", &g_tuning.sq8_wide_pilot_rows, 0, 1 << 16, false},
+        {"sq8_wide_defer", &g_tuning.sq8_wide_defer, 0, 1, false},
+        {"sq6_rebound_stride", &g_tuning.sq6_rebound_stride, 0, 1, false},
         {"sq8_mfma_ring", &g_tuning.sq8_mfma_ring, -1, 8, false},
         {"i8_stream", &g_tuning.i8_stream, 0, 1, false},
         {"call_timing", &g_tuning.call_timing, 0, 1, false},
@@ -1629,6 +1632,8 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             p.ablate = g_tuning.sq8_mfma_ablate;
             p.counters = v->d_counters.as<unsigned long long>();   // (testing build: event counts)
             p.pilot = 1;
+            p.pilot_rows = g_tuning.sq8_wide_pilot_rows;
+            p.wide_defer = g_tuning.sq8_wide_defer;
             p.pilot_keys = v->ws_pilot.as<uint64_t>();
             p.quarter_begin = 0;
             p.quarter_end = 0;
@@ -1690,6 +1695,13 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             p.counters = v->d_counters.as<unsigned long long>();
             p.ablate = g_tuning.sq8_mfma_ablate;
             p.tile_order = v->d_tile_order.as<int32_t>();
+            if (v->n_cus <= 0 &&
+                (hipDeviceGetAttribute(&v->n_cus, hipDeviceAttributeMultiprocessorCount, v->device) != hipSuccess ||
+                 v->n_cus <= 0))
+                v->n_cus = 256;
+            p.wide_grid = v->n_cus;   // (the persistent re-bound's grid: 4 workgroups per CU)
+            p.n_segs = ns;
+            p.rb_stride = g_tuning.sq6_rebound_stride;
             OSK_HIP(v->ws_cand6.reserve(sizeof(uint32_t) * (size_t)p.n_lists * kSq6Cap));
             OSK_HIP(v->ws_cnt6.reserve(sizeof(int32_t) * (size_t)nq * p.n_lists));
             p.cand6 = v->ws_cand6.as<uint32_t>();
@@ -2166,7 +2178,9 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
     const bool dev = n == "sq8_fallback_queries" || n == "sq8_rescored_rows" || n == "sq8_exact_tiles" ||
                      n == "sq6_rebound_rows" || n == "sq8_wide_events" || n == "sq8_wide_pairs" ||
                      n == "sq8_wide_wait_cycles" || n == "sq8_wide_slow_steps" || n == "sq8_wide_loop_cycles" ||
-                     n == "sq8_wide_quarter_cycles" || n == "sq8_wide_consts_cycles";
+                     n == "sq8_wide_quarter_cycles" || n == "sq8_wide_consts_cycles" ||
+                     n == "sq6_rebound_max_wave_passes" || n == "sq6_rebound_passes" ||
+                     n == "sq6_rebound_max_wave_cycles";
     OSK_REQUIRE(dev || n == "mfma_calls" || n == "mfma_fallback_queries" || n == "sq8_calls" || n == "sq6_calls" ||
                     n == "select_calls" || n == "sq8_wide_calls",
                 "unknown counter: " + n);
@@ -2185,7 +2199,9 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
                              : n == "sq8_exact_tiles" ? c[2] : n == "sq6_rebound_rows" ? c[3]
                              : n == "sq8_wide_events" ? c[4] : n == "sq8_wide_pairs" ? c[5]
                              : n == "sq8_wide_wait_cycles" ? c[6] : n == "sq8_wide_slow_steps" ? c[7]
-                             : n == "sq8_wide_loop_cycles" ? c[8] : n == "sq8_wide_quarter_cycles" ? c[9] : c[10]);
+                             : n == "sq8_wide_loop_cycles" ? c[8] : n == "sq8_wide_quarter_cycles" ? c[9]
+                             : n == "sq8_wide_consts_cycles" ? c[10] : n == "sq6_rebound_max_wave_passes" ? c[11]
+                             : n == "sq6_rebound_passes" ? c[12] : c[13]);
         } else {
             sum += n == "mfma_calls" ? s->mfma_calls : n == "mfma_fallback_queries" ? s->mfma_fallback_queries
                  : n == "sq8_calls" ? s->sq8_calls : n == "sq6_calls" ? s->sq6_calls

@@ -181,7 +181,12 @@ struct Sq8Params {
     int cap6;
     const float4* const* auxt;       // sq8_wide: per segment, the 16-row groups' bound terms (launch_sq8w_build)
     int wide_grid;                   // sq8_wide: persistent workgroups (the device's CUs)
+    int n_segs;                      // sq6_rebound: the view's segments (LDS per-segment counts when ≤ 64)
+    int rb_stride;                   // sq6_rebound: 1 = wave gw takes lists gw, gw + W, … (tune sq6_rebound_stride)
     int quarter_begin, quarter_end;  // sq8_wide: the launch's quarters in tile order (end 0: all)
+    int pilot_rows;                  // sq8_wide pilot: rows bounded per quarter (0 = kWidePilotRows)
+    int wide_defer;                  // sq8_wide: defer insertions to the quarter's end when LDS allows (tune)
+    int wide_qcap;                   // (set by launch_sq8_wide: entries per wave's deferred queue, 0 = immediate)
     const uint32_t* floors;          // sq8_wide: [q_count][n_shards] floor score (sortable bits; 0 = none)
     const float4* quarter_bm;        // sq8_wide: [4·n_tiles] the quarters' row maxima (launch_wide_quarter_max)
 };
@@ -444,6 +449,9 @@ struct Tuning {
     std::atomic<int> sq8_wide_min{64};    // ...and unfiltered batches ≥ this on the wide kernel, kWideQ per launch, when
                                           // its cost model beats sq8_mfma's (0 = never)
     std::atomic<int> sq8_wide_grid{0};    // wide kernel's persistent workgroups (0 = one per CU)
+    std::atomic<int> sq8_wide_pilot_rows{0};   // wide pilot rows per quarter (0 = 128)
+    std::atomic<int> sq6_rebound_stride{1};   // sq6_rebound: strided list assignment (0: contiguous)
+    std::atomic<int> sq8_wide_defer{1};   // wide kernel: defer list insertions to each quarter's end (0: immediate)
     std::atomic<int> sq8_wide_quarter_rows{0};   // rows per wide quarter, read when a view builds its table (0 = auto)
     std::atomic<int> sq8_wide_force{0};   // (tests) the wide kernel for every eligible batch, whatever the model says
     std::atomic<int> sq8_wide_phase{8};   // the wide kernel's first pass covers 1/this of the quarters, whose lists

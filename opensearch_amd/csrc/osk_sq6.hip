@@ -407,102 +407,190 @@ __global__ __launch_bounds__(kBlock, 4) void sq6_scan(Sq8Params p) {   // ≤ 12
 // then not re-scored).
 template <int C>
 __global__ __launch_bounds__(kBlock) void sq6_rebound(Sq8Params p) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform: scalar loop control
+    // Persistent waves (round 5): W waves walk the list table, each with the NEXT list's descriptor loads —
+    // its tile, candidate count and first 8 candidates — issued before the current list's rows are read, so
+    // each list costs one dependent round trip (rows + bound terms) instead of the 4–5 of a one-list-per-wave
+    // launch.  Assignment (p.rb_stride): contiguous (wave gw: lists [gw·per, (gw+1)·per)) or strided (lists
+    // gw, gw + W, …).  The lists scanned first (the first tiles of every shard, under the pilot's floor)
+    // carry the most candidates, and a contiguous split hands them to the same few waves; the strided one
+    // spreads them.  The shards' floors (≤ 64 shards) and the per-segment counts (≤ 64 segments) live in LDS,
+    // so neither changes of shard nor of segment cost a global round trip or a same-address atomic per list.
+    constexpr int kMaxLds = 64;
+    __shared__ uint32_t s_floor[kMaxLds];
+    __shared__ unsigned long long s_vis[kMaxLds], s_reb[kMaxLds];
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int cg = lane >> 4, ct = lane & 15;
-    const int tix = blockIdx.x;
-    const int list = tix * 4 + wave;
-    const TileDev tile = p.tiles[tix];
-    const SegDev seg = p.segs[tile.seg];
-    const int4* __restrict__ X8 = p.rows8[tile.seg];
-    const float4* __restrict__ AX8 = p.aux[tile.seg];
-    const uint32_t vbase = (uint32_t)p.seg_vrow[tile.seg];
+    const int W = gridDim.x * 4, gw = blockIdx.x * 4 + wave;
+    const bool strided = p.rb_stride != 0;
+    const int per = (p.n_lists + W - 1) / W;
+    const int l0 = strided ? gw : min(gw * per, p.n_lists);
+    const int l1 = strided ? p.n_lists : min(l0 + per, p.n_lists);
+    const int dl = strided ? W : 1;
     const int sim = p.sim, u8 = p.units8;
+    const bool floor_lds = p.n_shards <= kMaxLds, seg_lds = p.n_segs <= kMaxLds;
     const float4 qc = p.qc[0];
     const float qnd0 = sim == SIM_COSINE ? p.qn_dev[0] : 0.0f;
     const float sqn0 = sqrtf(qnd0);
-    const uint32_t* fb = p.floor + ((size_t)p.q0 * p.n_shards + tile.shard) * (kFloorBuckets + 1) * kFloorStride;
-    uint64_t fkey = (uint64_t)max(wave_kth_largest(fb[lane * kFloorStride], lane, p.k),
-                                  fb[kFloorBuckets * kFloorStride]) << 32;
-    if (!(key_score(fkey) > 0.0f)) fkey = 0ull;
-    const int nc = p.cnt6[(size_t)p.q0 * p.n_lists + list];
     int4 qv8[C];   // this lane's units of the int8 query
 #pragma unroll
     for (int i = 0; i < C; ++i) qv8[i] = ct + 16 * i < u8 ? p.q8[ct + 16 * i] : make_int4(0, 0, 0, 0);
-    const uint32_t* cbuf = p.cand6 + (size_t)list * p.cap6;
-    uint64_t lk0 = 0ull, thr0 = 0ull;
-    uint32_t lp0 = 0u;
-    float tq0 = sq8_quick(sim, fkey, sqn0, p.cos_slack);
-    if (nc <= p.cap6) {
-        // 8 candidates per pass (two halves of 4 rows × 16 lanes), every load of both halves issued
-        // before any is used: one round trip per 8 candidates
-        for (int c0 = 0; c0 < nc; c0 += 8) {
-            bool v[2];
-            uint32_t r[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                v[h] = c0 + 4 * h + cg < nc;
-                r[h] = v[h] ? cbuf[c0 + 4 * h + cg] : cbuf[0];
-            }
-            int4 xv[2][C];
-            float4 ax[2];
-            float xnd[2] = {0.0f, 0.0f};
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {   // unconditional loads of clamped rows, masked after
-                const int4* xr = X8 + (int64_t)r[h] * u8;
-#pragma unroll
-                for (int i = 0; i < C; ++i) xv[h][i] = ct + 16 * i < u8 ? xr[ct + 16 * i] : make_int4(0, 0, 0, 0);
-                ax[h] = AX8[r[h]];
-                if (sim == SIM_COSINE) xnd[h] = seg.xnorm_f[r[h]];
-            }
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                int a8 = 0;
-#pragma unroll
-                for (int i = 0; i < C; ++i) {
-                    const int4 qv = qv8[i];
-                    a8 = __builtin_amdgcn_sdot4(xv[h][i].x, qv.x, a8, false);
-                    a8 = __builtin_amdgcn_sdot4(xv[h][i].y, qv.y, a8, false);
-                    a8 = __builtin_amdgcn_sdot4(xv[h][i].z, qv.z, a8, false);
-                    a8 = __builtin_amdgcn_sdot4(xv[h][i].w, qv.w, a8, false);
-                }
-                a8 = lane_sum<16>(a8);
-                float lo, hi;
-                sq8_bounds(sim, (float)a8, ax[h], qc, p.gam, p.g2, lo, hi);
-                const float sx = sim == SIM_COSINE ? __builtin_amdgcn_sqrtf(ax[h].w) : 0.0f;
-                const bool pass = v[h] && sq8_pass(sim, lo, hi, tq0, sx);
-                if (__ballot(pass && ct == 0)) {
-                    const float ub = sim == SIM_EUCLIDEAN ? score_f32_l2(lo) : score_f32(sim, hi, qnd0, xnd[h]);
-                    const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qnd0, xnd[h]);
-                    const uint64_t key = pass ? make_key(ub, vbase + r[h]) : 0ull;
-                    wave_offer2(key, float_to_sortable(lb), pass && ct == 0, lk0, lp0, thr0, lane, kKQ);
-                    tq0 = sq8_quick(sim, max(thr0, fkey), sqn0, p.cos_slack);
-                }
-            }
+    const size_t cnt_base = (size_t)p.q0 * p.n_lists;
+    auto shard_floor = [&](int shard) -> uint32_t {   // the k-th best bucket maximum, or the floor cell
+        const uint32_t* fb = p.floor + ((size_t)p.q0 * p.n_shards + shard) * (kFloorBuckets + 1) * kFloorStride;
+        return max(wave_kth_largest(fb[lane * kFloorStride], lane, p.k), fb[kFloorBuckets * kFloorStride]);
+    };
+    if (floor_lds)
+        for (int s = wave; s < p.n_shards; s += 4) {
+            const uint32_t f = shard_floor(s);
+            if (lane == 0) s_floor[s] = f;
         }
-    } else if (lane == kKQ - 1) {
-        lk0 = ~0ull;   // overflowed: above every threshold → the settle re-scans the list's rows exactly
-        lp0 = 0u;
-    }
-    uint32_t m = (lane < kKQ && lk0 && lk0 != ~0ull) ? lp0 : 0u;
+    if (seg_lds)
+        for (int i = threadIdx.x; i < kMaxLds; i += kBlock) s_vis[i] = 0ull, s_reb[i] = 0ull;
+    __syncthreads();
+    // the next list's descriptor, loaded one list ahead
+    auto load_desc = [&](int list, TileDev& td, int& nc, uint32_t (&c8)[2]) {
+        const int l = list < l1 ? list : l0;   // (clamped: a valid address, unused)
+        td = p.tiles[l >> 2];
+        nc = p.cnt6[cnt_base + l];
+        const uint32_t* cb = p.cand6 + (size_t)l * p.cap6;
+        c8[0] = cb[cg];
+        c8[1] = cb[4 + cg];
+    };
+    int cur_shard = -1, cur_seg = -1;
+    uint64_t fkey = 0ull;
+    const int4* X8 = nullptr;
+    const float4* AX8 = nullptr;
+    const float* XN = nullptr;
+    uint32_t vbase = 0;
+    unsigned long long vis = 0, reb = 0, reb_seg = 0;   // (current segment's) visited rows and re-bounds
+#ifdef OSK_TESTING
+    unsigned long long n_pass = 0;
+    const long long t_begin = clock64();
+#endif
+    auto flush_seg = [&]() {   // the current segment's counts: LDS, or (> 64 segments) one global atomic each
+        if (cur_seg < 0 || lane != 0) return;
+        if (seg_lds) {
+            if (vis) atomicAdd(&s_vis[cur_seg], vis);
+            if (reb_seg) atomicAdd(&s_reb[cur_seg], reb_seg);
+        } else {
+            if (p.visited && p.q0 == 0 && vis) atomicAdd(&p.visited[cur_seg], vis);
+            if (p.seg_rebound && reb_seg) atomicAdd(&p.seg_rebound[cur_seg], reb_seg);
+        }
+    };
+    TileDev td_n;
+    int nc_n = 0;
+    uint32_t c8_n[2] = {0u, 0u};
+    if (l0 < l1) load_desc(l0, td_n, nc_n, c8_n);
+    for (int list = l0; list < l1; list += dl) {
+        TileDev tile = td_n;   // (every lane loaded the same descriptor: keep it in SGPRs)
+        tile.seg = __builtin_amdgcn_readfirstlane(tile.seg);
+        tile.shard = __builtin_amdgcn_readfirstlane(tile.shard);
+        const int nc = __builtin_amdgcn_readfirstlane(nc_n);
+        const uint32_t c8[2] = {c8_n[0], c8_n[1]};
+        if (list + dl < l1) load_desc(list + dl, td_n, nc_n, c8_n);
+        if (tile.seg != cur_seg) {   // (wave-uniform) the segment's pointers; flush its counts
+            flush_seg();
+            vis = 0;
+            reb_seg = 0;
+            cur_seg = tile.seg;
+            X8 = p.rows8[tile.seg];
+            AX8 = p.aux[tile.seg];
+            XN = p.segs[tile.seg].xnorm_f;
+            vbase = (uint32_t)p.seg_vrow[tile.seg];
+        }
+        if (tile.shard != cur_shard) {   // the shard's floor
+            cur_shard = tile.shard;
+            fkey = (uint64_t)(floor_lds ? s_floor[tile.shard] : shard_floor(tile.shard)) << 32;
+            if (!(key_score(fkey) > 0.0f)) fkey = 0ull;
+        }
+        if ((list & 3) == 0) vis += (unsigned long long)(tile.row_end - tile.row_begin);   // (each tile once)
+        reb += (unsigned long long)nc;
+        reb_seg += (unsigned long long)nc;
+        uint64_t lk0 = 0ull, thr0 = 0ull;
+        uint32_t lp0 = 0u;
+        float tq0 = sq8_quick(sim, fkey, sqn0, p.cos_slack);
+        const uint32_t* cbuf = p.cand6 + (size_t)list * p.cap6;
+        if (nc <= p.cap6) {
+            // 8 candidates per pass (two halves of 4 rows × 16 lanes), every load of both halves issued before
+            // any is used: one round trip per 8 candidates (the first 8 came with the descriptor)
+            for (int c0 = 0; c0 < nc; c0 += 8) {
+#ifdef OSK_TESTING
+                ++n_pass;
+#endif
+                bool v[2];
+                uint32_t r[2];
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
-    const size_t l = (size_t)p.q0 * p.n_lists + list;
-    if (lane < kKQ) {
-        p.cand[l * kKQ + lane] = lk0;
-        p.cand_lb[l * kKQ + lane] = lp0;
+                for (int h = 0; h < 2; ++h) {   // (a slot past the count reads row 0: a valid address, masked after)
+                    v[h] = c0 + 4 * h + cg < nc;
+                    r[h] = !v[h] ? 0u : c0 == 0 ? c8[h] : cbuf[c0 + 4 * h + cg];
+                }
+                int4 xv[2][C];
+                float4 ax[2];
+                float xnd[2] = {0.0f, 0.0f};
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {   // unconditional loads of clamped rows, masked after
+                    const int4* xr = X8 + (int64_t)r[h] * u8;
+#pragma unroll
+                    for (int i = 0; i < C; ++i) xv[h][i] = ct + 16 * i < u8 ? xr[ct + 16 * i] : make_int4(0, 0, 0, 0);
+                    ax[h] = AX8[r[h]];
+                    if (sim == SIM_COSINE) xnd[h] = XN[r[h]];
+                }
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    int a8 = 0;
+#pragma unroll
+                    for (int i = 0; i < C; ++i) {
+                        const int4 qv = qv8[i];
+                        a8 = __builtin_amdgcn_sdot4(xv[h][i].x, qv.x, a8, false);
+                        a8 = __builtin_amdgcn_sdot4(xv[h][i].y, qv.y, a8, false);
+                        a8 = __builtin_amdgcn_sdot4(xv[h][i].z, qv.z, a8, false);
+                        a8 = __builtin_amdgcn_sdot4(xv[h][i].w, qv.w, a8, false);
+                    }
+                    a8 = lane_sum<16>(a8);
+                    float lo, hi;
+                    sq8_bounds(sim, (float)a8, ax[h], qc, p.gam, p.g2, lo, hi);
+                    const float sx = sim == SIM_COSINE ? __builtin_amdgcn_sqrtf(ax[h].w) : 0.0f;
+                    const bool pass = v[h] && sq8_pass(sim, lo, hi, tq0, sx);
+                    if (__ballot(pass && ct == 0)) {
+                        const float ub = sim == SIM_EUCLIDEAN ? score_f32_l2(lo) : score_f32(sim, hi, qnd0, xnd[h]);
+                        const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qnd0, xnd[h]);
+                        const uint64_t key = pass ? make_key(ub, vbase + r[h]) : 0ull;
+                        wave_offer2(key, float_to_sortable(lb), pass && ct == 0, lk0, lp0, thr0, lane, kKQ);
+                        tq0 = sq8_quick(sim, max(thr0, fkey), sqn0, p.cos_slack);
+                    }
+                }
+            }
+        } else if (lane == kKQ - 1) {
+            lk0 = ~0ull;   // overflowed: above every threshold → the settle re-scans the list's rows exactly
+            lp0 = 0u;
+        }
+        uint32_t m = (lane < kKQ && lk0 && lk0 != ~0ull) ? lp0 : 0u;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+        const size_t l = cnt_base + list;
+        if (lane < kKQ) {
+            p.cand[l * kKQ + lane] = lk0;
+            p.cand_lb[l * kKQ + lane] = lp0;
+        }
+        if (lane == 0) p.list_lbmax[l] = m;
     }
-    if (lane == 0) p.list_lbmax[l] = m;
-    // the tile's visited rows (every row: the 6-bit pass is unfiltered) and its candidates, one atomic
-    // each per workgroup, here rather than at the end of every 6-bit wave (same-address atomics queue)
-    __shared__ int s_nc;
-    if (tid == 0) s_nc = 0;
-    __syncthreads();
-    if (lane == 0 && nc) atomicAdd(&s_nc, nc);
-    __syncthreads();
-    if (tid == 0) {
-        if (p.visited && p.q0 == 0) atomicAdd(&p.visited[tile.seg], (unsigned long long)(tile.row_end - tile.row_begin));
-        if (p.counters && s_nc) atomicAdd(&p.counters[3], (unsigned long long)s_nc);
-        if (p.seg_rebound && s_nc) atomicAdd(&p.seg_rebound[tile.seg], (unsigned long long)s_nc);
+    flush_seg();
+    // the wave's re-bound total, and (LDS mode) the workgroup's per-segment counts: one atomic each
+    // (same-address atomics queue at L2: per list they would serialise)
+    if (lane == 0 && p.counters && reb) atomicAdd(&p.counters[3], reb);
+#ifdef OSK_TESTING
+    if (lane == 0 && p.counters) {   // [11] the slowest wave's passes, [12] all passes, [13] the slowest wave's clocks
+        atomicMax(&p.counters[11], n_pass);
+        atomicAdd(&p.counters[12], n_pass);
+        atomicMax(&p.counters[13], (unsigned long long)(clock64() - t_begin));
+    }
+#endif
+    if (seg_lds) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < p.n_segs; i += kBlock) {
+            if (p.visited && p.q0 == 0 && s_vis[i]) atomicAdd(&p.visited[i], s_vis[i]);
+            if (p.seg_rebound && s_reb[i]) atomicAdd(&p.seg_rebound[i], s_reb[i]);
+        }
     }
 }
 
@@ -524,7 +612,9 @@ hipError_t launch_sq6_scan(const Sq8Params& p, int dim, hipStream_t s, hipEvent_
         hipExtLaunchKernelGGL(kSq6[C - 2], dim3(p.n_tiles), dim3(kBlock), 0, s, ev_start, ev_stop, 0, p);
     else
         hipLaunchKernelGGL(kSq6[C - 2], dim3(p.n_tiles), dim3(kBlock), 0, s, p);
-    hipLaunchKernelGGL(kSq6Rebound[C - 2], dim3(p.n_tiles), dim3(kBlock), 0, s, p);
+    // the re-bound: persistent waves, a few lists each (4 workgroups of 4 waves per CU at most)
+    const int rb_grid = std::max(1, std::min(p.n_tiles, 4 * (p.wide_grid > 0 ? p.wide_grid : 256)));
+    hipLaunchKernelGGL(kSq6Rebound[C - 2], dim3(rb_grid), dim3(kBlock), 0, s, p);
     return hipGetLastError();
 }
 

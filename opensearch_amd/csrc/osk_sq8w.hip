@@ -356,6 +356,11 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
     uint32_t* s_floor = reinterpret_cast<uint32_t*>(s_qc + kWideQ);       // [S][kWideQ] the pilot's floor scores
     int32_t* s_cnt = reinterpret_cast<int32_t*>(s_floor + (floor_lds ? S * kWideQ : 0));   // [kWideQ] list fill
     WideQuarter* s_quart = reinterpret_cast<WideQuarter*>(s_cnt + kWideQ);
+    // the deferred insertions (p.wide_qcap > 0): per wave, qcap entries {int32 dot, row in quarter << 8 | query
+    // in wave}, drained when the quarter ends (every wave at the same step) or when full
+    // (EUCLIDEAN at KS = 2 keeps the immediate insertions: the queue's code spills there)
+    const int qcap = (SIM == SIM_EUCLIDEAN && KS == 2) ? 0 : p.wide_qcap;
+    uint2* s_q = reinterpret_cast<uint2*>(s_quart + n_mine) + (size_t)wave * qcap;
     for (int i = tid; i < kWideQ * kKQ; i += kWideThreads) {
         s_lk[i] = 0ull;
         s_lp[i] = 0u;
@@ -380,7 +385,8 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
         d.xt = p.rows8t[tile.seg] + (rb >> 4) * (KS * 64);
         d.at = p.auxt[tile.seg] + (rb >> 4) * kAuxGroupF4;
         d.vrow0 = (uint32_t)(p.seg_vrow[tile.seg] + rb);
-        d.nrows = (int32_t)(pilot ? min<int64_t>(kWidePilotRows, re - rb) : re - rb);   // the pilot: its first rows
+        d.nrows = (int32_t)(pilot ? min<int64_t>(p.pilot_rows > 0 ? p.pilot_rows : kWidePilotRows, re - rb)
+                                  : re - rb);   // the pilot: its first rows
         d.list = tix * 4 + quarter;
         d.shard = tile.shard;
         d.seg = tile.seg;
@@ -580,6 +586,94 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
         i32x4 acc[GPS][QB];
         uint64_t pbest[QB];   // the pilot: the current quarter's best lower-bound key per query so far
         float4 bm = make_float4(0.f, 0.f, 0.f, 0.f);
+        int qn = 0;   // (wave-uniform) entries in this wave's deferred queue
+        // The deferred insertions of quarter d, 64 at a time, one entry per lane: its row's bound terms from the
+        // quarter's tiled terms in global memory (the ring slot is long gone), the precise bound, and above the
+        // floor an append to its (quarter, query) list; lists that would fill take the ordered insertion, one
+        // query at a time.  Same lists, same thresholds as the immediate path.
+        auto drain = [&](const WideQuarter& d) {
+            const int sh = d.shard;
+            for (int i0 = 0; i0 < qn; i0 += 64) {
+                const bool ok = i0 + lane < qn;
+                const uint2 en = ok ? s_q[i0 + lane] : make_uint2(0u, 0u);
+                const int qw = (int)(en.y & 255u), rowq = (int)(en.y >> 8);
+                const int qi = wq0 + qw;
+                const float* af = reinterpret_cast<const float*>(d.at + (rowq >> 4) * kAuxGroupF4);
+                const int rr = rowq & 15;
+                const float4 ax = ok ? make_float4(af[rr], af[16 + rr], af[32 + rr], af[48 + rr]) : make_float4(0.f, 0.f, 0.f, 0.f);
+                float xnd = 0.0f, qndq = 0.0f;
+                if constexpr (SIM == SIM_COSINE) {
+                    xnd = ok ? af[72 + rr] : 0.0f;
+                    qndq = ok ? p.qn_dev[qi] : 0.0f;
+                }
+                uint64_t key = 0ull;
+                uint32_t lbs = 0u;
+                bool ovf = false;
+                if (ok) {
+                    const float4 qcb = s_qc[qi];
+                    float lo, hi;
+                    sq8_bounds(sim, (float)(int32_t)en.x, ax, qcb, p.gam, p.g2, lo, hi);
+                    const float ub = SIM == SIM_EUCLIDEAN ? score_f32_l2(lo) : score_f32(sim, hi, qndq, xnd);
+                    const float lb = SIM == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qndq, xnd);
+                    const uint64_t kr = make_key(ub, d.vrow0 + (uint32_t)rowq);
+                    const uint64_t tk = (uint64_t)(floor_lds ? s_floor[sh * kWideQ + qi] : floor_of(qi, sh)) << 32;
+                    if (kr > tk) {   // below the floor: cannot enter the top k
+#ifdef OSK_TESTING
+                        ++n_pairs;
+#endif
+                        const int pos = atomicAdd(&s_cnt[qi], 1);
+                        if (pos < kKQ - 1) {
+                            s_lk[qi * kKQ + pos] = kr;
+                            s_lp[qi * kKQ + pos] = float_to_sortable(lb);
+                        } else {
+                            key = kr;
+                            lbs = float_to_sortable(lb);
+                            ovf = true;
+                        }
+                    }
+                }
+                uint64_t om = __ballot(ovf);
+                while (om) {   // the overflowed queries, one at a time
+                    const int Q = __builtin_amdgcn_readlane(qw, (int)__builtin_ctzll(om));
+                    const int qo_g = wq0 + Q, o0 = qo_g * kKQ;
+                    uint64_t lkb = lane < kKQ ? s_lk[o0 + lane] : 0ull;
+                    uint32_t lpb = lane < kKQ ? s_lp[o0 + lane] : 0u;
+                    if (s_cnt[qo_g] < kWideSorted) {   // first overflow: sort the appended rows (zeros last)
+                        int rank = 0;
+#pragma unroll 2
+                        for (int j = 0; j < kKQ; ++j) {
+                            const uint64_t kj = s_lk[o0 + j];
+                            rank += (kj > lkb) || (kj == lkb && j < lane);
+                        }
+                        if (lane < kKQ) {
+                            s_lk[o0 + rank] = lkb;
+                            s_lp[o0 + rank] = lpb;
+                        }
+                        lkb = lane < kKQ ? s_lk[o0 + lane] : 0ull;
+                        lpb = lane < kKQ ? s_lp[o0 + lane] : 0u;
+                    }
+                    uint64_t thrb = readlane64(lkb, kKQ - 1);
+                    wave_offer2(key, lbs, ovf && qw == Q, lkb, lpb, thrb, lane, kKQ);
+                    if (lane < kKQ) {
+                        s_lk[o0 + lane] = lkb;
+                        s_lp[o0 + lane] = lpb;
+                    }
+                    if (lane == 0) s_cnt[qo_g] = kWideSorted;
+                    if (col == (Q & 15) && thrb) {   // full: its 16th key joins the floor under the threshold
+#pragma unroll
+                        for (int qb = 0; qb < QB; ++qb)
+                            if (qb == (Q >> 4)) {
+                                tq[qb] = sq8_quick(sim, thrb > tkey[qb] ? thrb : tkey[qb], sqrtf(qnd[qb]), p.cos_slack);
+                                quick_consts<SIM>(tq[qb], sb[qb], inv[qb], QY[qb], QZ[qb], Q0[qb], QW, zq[qb], ig2m, bm,
+                                                  ca[qb], cb[qb]);
+                            }
+                    }
+                    om = __ballot(ovf && qw != Q);
+                    ovf = ovf && qw != Q;
+                }
+            }
+            qn = 0;
+        };
         // the step's quick tests and insertions
         auto quick_phase = [&]() __attribute__((always_inline)) {
             const WideQuarter& hd = s_quart[hq];
@@ -592,6 +686,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
             // test itself (its threshold is affine in each row's |x|²), reduced to one vote per step.
             float tf[GPS][QB];
             bool zg[GPS];
+            uint32_t pbits[GPS];   // EUCLIDEAN: bit qb·4 + r = row r of the group passed for query block qb
 #pragma unroll
             for (int g = 0; g < GPS; ++g) {
                 const char* ga = hslot + g * GB + KS * 1024;
@@ -605,6 +700,9 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                         f32x2 t01, t23;
                         quick_t(acc[g][qb], ar, wr, ca[qb], cb[qb], t01, t23);
                         tf[g][qb] = fmaxf(fmaxf(t01.x, t01.y), fmaxf(t23.x, t23.y));
+                        pbits[g] = (qb ? pbits[g] : 0u) | (uint32_t)!(t01.x < 0.0f) << (qb * 4) |
+                                   (uint32_t)!(t01.y < 0.0f) << (qb * 4 + 1) | (uint32_t)!(t23.x < 0.0f) << (qb * 4 + 2) |
+                                   (uint32_t)!(t23.y < 0.0f) << (qb * 4 + 3);
                     }
                 } else {
                     const float4 gf = *reinterpret_cast<const float4*>(ga + 17 * 16);   // {s_g, f_cos, zero row, 0}
@@ -631,6 +729,69 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
 #ifdef OSK_TESTING
             ++n_slow;
 #endif
+            if (!(SIM == SIM_EUCLIDEAN && KS == 2) && qcap > 0 && !(ablate & 32)) {
+                // deferred mode: the passing pairs of each (group, query block) whose vote passed go to the wave's
+                // queue — the per-row test on the step's accumulators (static indices), a ballot per row and an
+                // LDS write per pair; bounds and list insertions wait for the quarter's end (drain)
+#pragma unroll
+                for (int g = 0; g < GPS; ++g) {
+                    if (g >= hgroups) continue;   // (wave-uniform: the quarter's last step)
+#pragma unroll
+                    for (int qb = 0; qb < QB; ++qb) {
+                        if (!(__ballot(!(tf[g][qb] < 0.0f) || zg[g]) & qvm[qb])) continue;
+#ifdef OSK_TESTING
+                        ++n_events;
+#endif
+                        const char* ga = hslot + g * GB + KS * 1024;
+                        float arg[4] = {0.0f, 0.0f, 0.0f, 0.0f}, wrg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+                        if constexpr (SIM != SIM_EUCLIDEAN) {
+                            const float4 Ag = *reinterpret_cast<const float4*>(ga + grp * 16);
+                            const float4 Wg = *reinterpret_cast<const float4*>(ga + 192 + grp * 16);
+                            arg[0] = Ag.x, arg[1] = Ag.y, arg[2] = Ag.z, arg[3] = Ag.w;
+                            wrg[0] = Wg.x, wrg[1] = Wg.y, wrg[2] = Wg.z, wrg[3] = Wg.w;
+                        }
+                        if constexpr (SIM == SIM_COSINE) {
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) arg[r] = arg[r] * __builtin_amdgcn_rsqf(wrg[r]);   // (0 · ∞ = NaN: passes)
+                        }
+                        const int r0 = 16 * (GPS * hst + g);
+                        const int nr = min(16, hd.nrows - r0);
+                        bool pass[4];
+                        if constexpr (SIM == SIM_EUCLIDEAN) {   // the fast test was the per-row test: its bits
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) pass[r] = (pbits[g] >> (qb * 4 + r)) & 1u;
+                        } else {
+                            f32x2 t01, t23;
+                            quick_t(acc[g][qb], arg, wrg, ca[qb], cb[qb], t01, t23);
+                            pass[0] = !(t01.x < 0.0f), pass[1] = !(t01.y < 0.0f);
+                            pass[2] = !(t23.x < 0.0f), pass[3] = !(t23.y < 0.0f);
+                        }
+                        const bool qv = (qvm[qb] >> lane) & 1ull;
+                        bool pr[4];
+                        uint64_t b[4];
+                        int tot = 0;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            pr[r] = pass[r] && 4 * grp + r < nr && qv;
+                            b[r] = __ballot(pr[r]);
+                            tot += __popcll(b[r]);
+                        }
+                        if (qn + tot > qcap) drain(hd);   // (tot ≤ 256 ≤ qcap)
+                        int base = qn;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(b[r] >> 32),
+                                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)b[r], 0u));
+                            if (pr[r])
+                                s_q[base + below] = make_uint2((uint32_t)acc[g][qb][r],
+                                                               (uint32_t)(r0 + 4 * grp + r) << 8 | (uint32_t)(qb * 16 + col));
+                            base += __popcll(b[r]);
+                        }
+                        qn = base;
+                    }
+                }
+                return;
+            }
             // (2) the slow path: per group the wave's queries with a group that may pass (wave-uniform)
             uint32_t qmg[GPS];
 #pragma unroll
@@ -798,7 +959,10 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
             }
             if (ablate & 64) continue;   // (A/B: the ring alone)
             if (pq < 0 || ++pst == steps_of(pq)) {   // a new quarter: flush the last one, take its floors
-                if (pq >= 0 && !pilot) flush(s_quart[pq]);
+                if (pq >= 0 && !pilot) {
+                    if (qn) drain(s_quart[pq]);
+                    flush(s_quart[pq]);
+                }
                 do ++pq; while (steps_of(pq) == 0);
                 pst = 0;
                 const int sh = s_quart[pq].shard;
@@ -912,7 +1076,10 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
 #ifdef OSK_TESTING
         cyc_loop += clock64() - c_loop0;
 #endif
-        if (pq >= 0 && !pilot) flush(s_quart[pq]);
+        if (pq >= 0 && !pilot) {
+            if (qn) drain(s_quart[pq]);
+            flush(s_quart[pq]);
+        }
     }
 #ifdef OSK_TESTING
     if (!pilot && p.counters) {
@@ -961,11 +1128,17 @@ hipError_t launch_sq8_wide(const Sq8Params& p, hipStream_t s, hipEvent_t ev_star
     int grid = std::min(p.wide_grid, std::max(1, nq4));
     // more workgroups (rounds of the chip) when one CU's share of quarter descriptors does not fit
     while (sq8_wide_lds(ks, p.sim, p.n_shards, (nq4 + grid - 1) / grid) > kLdsCap) grid *= 2;
-    const size_t lds = sq8_wide_lds(ks, p.sim, p.n_shards, (nq4 + grid - 1) / grid);
+    size_t lds = sq8_wide_lds(ks, p.sim, p.n_shards, (nq4 + grid - 1) / grid);
+    // the deferred-insertion queues in what LDS is left: ≥ 256 entries per wave (one (group, query block) adds at
+    // most 64 lanes × 4 rows), else the immediate insertions (and always for the pilot)
+    Sq8Params q = p;
+    const int room = (int)((kLdsCap - lds) / (kWideWaves * sizeof(uint2))) / 64 * 64;
+    q.wide_qcap = (!p.pilot && p.wide_defer && room >= 256) ? std::min(room, 512) : 0;
+    lds += (size_t)kWideWaves * q.wide_qcap * sizeof(uint2);
     if (ev_start || ev_stop)
-        hipExtLaunchKernelGGL(fn, dim3(grid), dim3(kWideThreads), lds, s, ev_start, ev_stop, 0, p);
+        hipExtLaunchKernelGGL(fn, dim3(grid), dim3(kWideThreads), lds, s, ev_start, ev_stop, 0, q);
     else
-        hipLaunchKernelGGL(fn, dim3(grid), dim3(kWideThreads), lds, s, p);
+        hipLaunchKernelGGL(fn, dim3(grid), dim3(kWideThreads), lds, s, q);
     return hipGetLastError();
 }
 

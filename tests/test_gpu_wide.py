@@ -245,3 +245,29 @@ def test_wide_many_shards_global_floors_and_grid_doubling(sim):
         _oracle_check(small, rows_list, shard_of, shard_index, queries, 10, sim, every=29)
     finally:
         close_all(ds, readers)
+
+
+@pytest.mark.parametrize("defer", [0, 1])
+@pytest.mark.parametrize("sim", SIMS, ids=lambda s: s.name)
+def test_wide_immediate_and_deferred_insertions_agree(sim, defer):
+    """The wide kernel defers its list insertions to each quarter's end when LDS allows (sq8_wide_defer 1, the
+    default) or inserts at once (0); both equal sq8_mfma, the fp32 scan and the oracle.  Quarters of 256 rows
+    and a 1-workgroup grid give each wave many quarters, drains and (few floors yet) full queues."""
+    dim = {0: 128, 1: 96, 2: 768, 3: 200}[int(sim)]
+    rows_list = [corpus(n, dim, sim, 300 + i) for i, n in enumerate([20000, 7777])]
+    queries = corpus(140, dim, sim, 301)
+    _lib.tune("sq8_wide_quarter_rows", 256)
+    try:
+        ds, readers = view_of(rows_list, sim, [0, 1], [1, 0])
+        ds.search(queries[:64], 10, 0, 10)   # builds the wide table under the knob
+    finally:
+        _lib.tune("sq8_wide_quarter_rows", 0)
+    _lib.tune("sq8_wide_defer", defer)
+    try:
+        out = three_ways(ds, queries, 10)
+        small = tuned("sq8_wide_grid", 1, 0, lambda: ds.search(queries, 10, 0, 10))
+        assert_same(small, out)
+        _oracle_check(out, rows_list, [0, 1], [1, 0], queries, 10, sim, every=23)
+    finally:
+        _lib.tune("sq8_wide_defer", 1)
+        close_all(ds, readers)
