@@ -320,10 +320,13 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         {"sq8_wide_pilot_rows", &g_tuning.sq8_wide_pilot_rows, 0, 1 << 16, false},
         {"sq8_wide_defer", &g_tuning.sq8_wide_defer, 0, 1, false},
         {"sq6_rebound_stride", &g_tuning.sq6_rebound_stride, 0, 1, false},
+        {"sq6_rebound_retest", &g_tuning.sq6_rebound_retest, 0, 1, false},
+        {"sq6_rebound_wgs", &g_tuning.sq6_rebound_wgs, 0, 16, false},
         {"sq8_mfma_ring", &g_tuning.sq8_mfma_ring, -1, 8, false},
         {"i8_stream", &g_tuning.i8_stream, 0, 1, false},
         {"call_timing", &g_tuning.call_timing, 0, 1, false},
-        {"sq8_mfma_ablate", &g_tuning.sq8_mfma_ablate, 0, 127, true},   // (also sq6_scan's: 1 no re-bound, 2 no floor, 16 loads only)
+        {"sq8_mfma_ablate", &g_tuning.sq8_mfma_ablate, 0, 1023, true},   // (also sq6_scan's: 1 no re-bound, 2 no floor,
+                                                                          // 16 loads only; sq6_rebound's: 256 no list work)
         {"sq8_force_fallback", &g_tuning.sq8_force_fallback, 0, 1, true},
         {"settle_trace", &g_tuning.settle_trace, 0, 1, true},
         {"mfma_ablate", &g_tuning.mfma_ablate, 0, 255, true},
@@ -1702,9 +1705,13 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             p.wide_grid = v->n_cus;   // (the persistent re-bound's grid: 4 workgroups per CU)
             p.n_segs = ns;
             p.rb_stride = g_tuning.sq6_rebound_stride;
+            p.rb_retest = g_tuning.sq6_rebound_retest;
+            p.rb_wg_per_cu = g_tuning.sq6_rebound_wgs;
             OSK_HIP(v->ws_cand6.reserve(sizeof(uint32_t) * (size_t)p.n_lists * kSq6Cap));
+            OSK_HIP(v->ws_cand6v.reserve(sizeof(float2) * (size_t)p.n_lists * kSq6Cap));
             OSK_HIP(v->ws_cnt6.reserve(sizeof(int32_t) * (size_t)nq * p.n_lists));
             p.cand6 = v->ws_cand6.as<uint32_t>();
+            p.cand6v = v->ws_cand6v.as<float2>();
             p.cnt6 = v->ws_cnt6.as<int32_t>();
             p.cap6 = kSq6Cap;
             p.seg_rebound = probe6 ? v->d_seg_rebound.as<unsigned long long>() : nullptr;
@@ -2179,8 +2186,8 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
                      n == "sq6_rebound_rows" || n == "sq8_wide_events" || n == "sq8_wide_pairs" ||
                      n == "sq8_wide_wait_cycles" || n == "sq8_wide_slow_steps" || n == "sq8_wide_loop_cycles" ||
                      n == "sq8_wide_quarter_cycles" || n == "sq8_wide_consts_cycles" ||
-                     n == "sq6_rebound_max_wave_passes" || n == "sq6_rebound_passes" ||
-                     n == "sq6_rebound_max_wave_cycles";
+                     n == "sq6_rebound_gathered_rows" || n == "sq6_rebound_passes" ||
+                     n == "sq6_rebound_max_wg_cycles";
     OSK_REQUIRE(dev || n == "mfma_calls" || n == "mfma_fallback_queries" || n == "sq8_calls" || n == "sq6_calls" ||
                     n == "select_calls" || n == "sq8_wide_calls",
                 "unknown counter: " + n);
@@ -2200,7 +2207,7 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
                              : n == "sq8_wide_events" ? c[4] : n == "sq8_wide_pairs" ? c[5]
                              : n == "sq8_wide_wait_cycles" ? c[6] : n == "sq8_wide_slow_steps" ? c[7]
                              : n == "sq8_wide_loop_cycles" ? c[8] : n == "sq8_wide_quarter_cycles" ? c[9]
-                             : n == "sq8_wide_consts_cycles" ? c[10] : n == "sq6_rebound_max_wave_passes" ? c[11]
+                             : n == "sq8_wide_consts_cycles" ? c[10] : n == "sq6_rebound_gathered_rows" ? c[11]
                              : n == "sq6_rebound_passes" ? c[12] : c[13]);
         } else {
             sum += n == "mfma_calls" ? s->mfma_calls : n == "mfma_fallback_queries" ? s->mfma_fallback_queries

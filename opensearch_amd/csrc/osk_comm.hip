@@ -316,6 +316,10 @@ int32_t lb_allgather(Loopback* L, const void* d_send, void* d_recv, size_t bytes
 int32_t local_allgather(osk_comm* c, const void* const* sends, void* const* recvs, size_t bytes) {
     const size_t n = c->devices.size();
     OSK_REQUIRE(n == (size_t)c->world, "local all-gather: one rank per local device");
+    // Ordering: every caller of gather_blocks first makes each exchange stream wait on the stream that
+    // produced its rank's send block (enter_xstream in osk_shards_search_merge_device / osk_shards_search_merge),
+    // so draining the exchange streams here also drains the send blocks' producers — the same event chain
+    // the RCCL all-gather relies on.  A caller that skipped enter_xstream would fail both transports alike.
     for (size_t i = 0; i < n; ++i) {
         OSK_HIP(hipSetDevice(c->devices[i]));
         OSK_HIP(hipStreamSynchronize(c->xstreams[i]));

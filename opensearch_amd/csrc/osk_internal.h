@@ -178,11 +178,14 @@ struct Sq8Params {
     const int32_t* tile_order;       // sq6_scan: the tile of each workgroup (tiles interleaved over shards)
     uint32_t* cand6;                 // sq6_scan → sq6_rebound: per list, the rows that passed the 6-bit test
     int32_t* cnt6;                   // [q][n_lists] their count (> cap6: overflowed)
+    float2* cand6v;                  // per list, each candidate's 6-bit test inputs {bound side, √|x|² (COSINE)}
     int cap6;
     const float4* const* auxt;       // sq8_wide: per segment, the 16-row groups' bound terms (launch_sq8w_build)
     int wide_grid;                   // sq8_wide: persistent workgroups (the device's CUs)
     int n_segs;                      // sq6_rebound: the view's segments (LDS per-segment counts when ≤ 64)
     int rb_stride;                   // sq6_rebound: 1 = wave gw takes lists gw, gw + W, … (tune sq6_rebound_stride)
+    int rb_wg_per_cu;                // sq6_rebound: workgroups per CU (0 = as many as fit; tune sq6_rebound_wgs)
+    int rb_retest;                   // sq6_rebound: re-test candidates at the 6-bit level against the final floor
     int quarter_begin, quarter_end;  // sq8_wide: the launch's quarters in tile order (end 0: all)
     int pilot_rows;                  // sq8_wide pilot: rows bounded per quarter (0 = kWidePilotRows)
     int wide_defer;                  // sq8_wide: defer insertions to the quarter's end when LDS allows (tune)
@@ -450,7 +453,9 @@ struct Tuning {
                                           // its cost model beats sq8_mfma's (0 = never)
     std::atomic<int> sq8_wide_grid{0};    // wide kernel's persistent workgroups (0 = one per CU)
     std::atomic<int> sq8_wide_pilot_rows{0};   // wide pilot rows per quarter (0 = 128)
+    std::atomic<int> sq6_rebound_retest{1};   // sq6_rebound: the final-floor 6-bit re-test (0: gather every candidate)
     std::atomic<int> sq6_rebound_stride{1};   // sq6_rebound: strided list assignment (0: contiguous)
+    std::atomic<int> sq6_rebound_wgs{0};      // sq6_rebound: workgroups per CU (0: as many as fit)
     std::atomic<int> sq8_wide_defer{1};   // wide kernel: defer list insertions to each quarter's end (0: immediate)
     std::atomic<int> sq8_wide_quarter_rows{0};   // rows per wide quarter, read when a view builds its table (0 = auto)
     std::atomic<int> sq8_wide_force{0};   // (tests) the wide kernel for every eligible batch, whatever the model says

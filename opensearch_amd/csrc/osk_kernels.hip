@@ -824,8 +824,9 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {   // splitmix64 finalise
 // and the byte count): order-independent, so identical bytes give identical fingerprints on every rank,
 // and a batch that differs in any word — its last query only, say — almost surely does not.  (A strided
 // sample of 16384 words left up to half of a 22–42-query batch at 768 dims unhashed.)  kXhdrWords per
-// workgroup; each adds its partial sum into w[5] (zeroed first by launch_xhdr_fill) with one atomic;
-// workgroup 0 writes the other header words and the shard indices.
+// workgroup; each adds its partial sum into w[5] (zeroed first by launch_xhdr_fill) with one atomic —
+// or, when one workgroup covers the query bytes (≤ 64 KiB: every single-query call), stores it, with no
+// memset before; workgroup 0 writes the other header words and the shard indices.
 constexpr int64_t kXhdrWords = 16384;
 __global__ __launch_bounds__(256) void xhdr_fill(uint64_t* __restrict__ hdr, XHdrWords w,
                                                  const uint8_t* __restrict__ q, int64_t qbytes,
@@ -848,8 +849,13 @@ __global__ __launch_bounds__(256) void xhdr_fill(uint64_t* __restrict__ hdr, XHd
     for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o);
     if ((tid & 63) == 0) s_part[tid >> 6] = h;
     __syncthreads();
-    if (tid == 0) atomicAdd(reinterpret_cast<unsigned long long*>(hdr + 5),
-                            (unsigned long long)(s_part[0] + s_part[1] + s_part[2] + s_part[3]));
+    if (tid == 0) {
+        const uint64_t sum = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+        if (gridDim.x == 1)
+            hdr[5] = sum;
+        else
+            atomicAdd(reinterpret_cast<unsigned long long*>(hdr + 5), (unsigned long long)sum);
+    }
     if (blockIdx.x != 0) return;
     if (tid < kXHdrWords && tid != 5) hdr[tid] = w.w[tid];
     int32_t* si = reinterpret_cast<int32_t*>(hdr + kXHdrWords);
@@ -860,9 +866,11 @@ hipError_t launch_xhdr_fill(uint64_t* hdr, const uint64_t* w, const void* querie
                             const int32_t* shard_index, int n_shards, int sl, hipStream_t s) {
     XHdrWords hw;
     for (int i = 0; i < kXHdrWords; ++i) hw.w[i] = w[i];
-    hipError_t e = hipMemsetAsync(hdr + 5, 0, sizeof(uint64_t), s);
-    if (e != hipSuccess) return e;
     const int64_t blocks = std::max<int64_t>(1, ((query_bytes >> 2) + kXhdrWords - 1) / kXhdrWords);
+    if (blocks > 1) {   // (one workgroup stores the fingerprint itself)
+        hipError_t e = hipMemsetAsync(hdr + 5, 0, sizeof(uint64_t), s);
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(xhdr_fill, dim3((unsigned)blocks), dim3(256), 0, s, hdr, hw,
                        static_cast<const uint8_t*>(queries), query_bytes, shard_index, n_shards, sl);
     return hipGetLastError();

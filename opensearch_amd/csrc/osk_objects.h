@@ -199,7 +199,7 @@ struct osk_view {
     bool sq6_ready = false;                           // the view does not use it)
     int64_t sq6_calls = 0;
     osk::DevBuf ws_q6, ws_qc6, ws_floor;              // its query (nibble split, bound terms), floor buckets,
-    osk::DevBuf ws_cand6, ws_cnt6;                    // the streaming pass's candidates per list
+    osk::DevBuf ws_cand6, ws_cnt6, ws_cand6v;         // the streaming pass's candidates per list (+ test inputs)
     // the tier's calibration (per segment, osk_seg::sq6_state): a probe call of this view counts its int8
     // re-bounds per segment into d_seg_rebound, copies them to h_seg_rebound on its stream and records
     // ev_probe; a later call folds them into the segments once the event has completed — nothing waits

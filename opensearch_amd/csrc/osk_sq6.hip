@@ -41,6 +41,8 @@
 // one shift + and: (w & 0x33333333) pairs with query dword 2w, ((w >> 2) & 0x33333333) with 2w + 1).
 #include <hip/hip_ext.h>
 
+#include <atomic>
+
 #include "osk_device.h"
 #include "osk_internal.h"
 #include "osk_wave.h"
@@ -382,7 +384,10 @@ __global__ __launch_bounds__(kBlock, 4) void sq6_scan(Sq8Params p) {   // ≤ 12
         // the passing rows (one lane per row) → the candidate buffer, and their 6-bit lower bounds
         const int slot = nc + __popcll(pm & ((1ull << lane) - 1ull));
         if (pass6) {
-            if (slot < p.cap6 && !(ablate & 4)) cbuf[slot] = (uint32_t)row;
+            if (slot < p.cap6 && !(ablate & 4)) {   // the row and its 6-bit test inputs (the re-bound re-tests)
+                cbuf[slot] = (uint32_t)row;
+                if (p.rb_retest) p.cand6v[(size_t)list * p.cap6 + slot] = make_float2(side6, sx);
+            }
             if (!(ablate & 8)) {
                 float lo, hi;
                 sq8_bounds(sim, (float)acc, ax, qc6, p.gam, p.g2, lo, hi);
@@ -399,25 +404,29 @@ __global__ __launch_bounds__(kBlock, 4) void sq6_scan(Sq8Params p) {   // ≤ 12
     }
 }
 
-// The int8 re-bound pass: one wave per scan wave's list.  Its candidates (4 rows × 16 lanes per pass)
-// get their int8 interval (sq8_bounds, exact device-order norms) and go through sq8_scan's quick test
-// and list insertion, with the shard's final floor under the list threshold; the list, its lower bounds
-// and its best lower bound are written as sq8_scan writes them.  A list whose candidates overflowed the
-// buffer gets a 16th key above every threshold, so the settle re-scans its rows exactly (its entries are
-// then not re-scored).
+// The int8 re-bound pass.  Each list's candidates are first re-tested at the 6-bit level against the
+// shard's FINAL floor (the scan tested them against the floor as it stood when their tile ran, lower for
+// the tiles scanned first; sq8_pass is monotone in the threshold and the final floor is as valid as any
+// earlier one), and only the survivors are gathered from the int8 copy: their int8 interval (sq8_bounds,
+// exact device-order norms), sq8_scan's quick test and the list insertion; the list, its lower bounds and
+// its best lower bound are written as sq8_scan writes them.  A list whose candidates overflowed the buffer
+// gets a 16th key above every threshold, so the settle re-scans its rows exactly (its entries are then not
+// re-scored).
+//
+// Persistent waves (round 5): W waves walk the list table, each with the NEXT list's descriptor — its tile,
+// candidate count, and its first 64 candidates with their 6-bit test inputs, one per lane — loaded before
+// the current list's rows, so a list costs one dependent round trip (its survivors' rows and bound terms).
+// Assignment (p.rb_stride): contiguous (wave gw: lists [gw·per, (gw+1)·per)) or strided (lists gw, gw + W,
+// …).  The shards' floors (≤ 64 shards) and the per-segment counts (≤ 64 segments) live in LDS, and the
+// workgroup's counters leave with one global atomic each: same-address atomics queue at L2 (≈ 4 ns apiece;
+// one per wave, 4,096 of them, cost ≈ 16 µs per launch, profiles/r05e/).
 template <int C>
 __global__ __launch_bounds__(kBlock) void sq6_rebound(Sq8Params p) {
-    // Persistent waves (round 5): W waves walk the list table, each with the NEXT list's descriptor loads —
-    // its tile, candidate count and first 8 candidates — issued before the current list's rows are read, so
-    // each list costs one dependent round trip (rows + bound terms) instead of the 4–5 of a one-list-per-wave
-    // launch.  Assignment (p.rb_stride): contiguous (wave gw: lists [gw·per, (gw+1)·per)) or strided (lists
-    // gw, gw + W, …).  The lists scanned first (the first tiles of every shard, under the pilot's floor)
-    // carry the most candidates, and a contiguous split hands them to the same few waves; the strided one
-    // spreads them.  The shards' floors (≤ 64 shards) and the per-segment counts (≤ 64 segments) live in LDS,
-    // so neither changes of shard nor of segment cost a global round trip or a same-address atomic per list.
     constexpr int kMaxLds = 64;
     __shared__ uint32_t s_floor[kMaxLds];
     __shared__ unsigned long long s_vis[kMaxLds], s_reb[kMaxLds];
+    __shared__ unsigned long long s_tot[4];   // the workgroup's re-bounds, gathered rows (testing: passes, max clocks)
+    __shared__ uint32_t s_sel[4][kSq6Cap];    // each wave's surviving candidates of its current list
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int cg = lane >> 4, ct = lane & 15;
     const int W = gridDim.x * 4, gw = blockIdx.x * 4 + wave;
@@ -446,23 +455,29 @@ __global__ __launch_bounds__(kBlock) void sq6_rebound(Sq8Params p) {
         }
     if (seg_lds)
         for (int i = threadIdx.x; i < kMaxLds; i += kBlock) s_vis[i] = 0ull, s_reb[i] = 0ull;
+    if (threadIdx.x < 4) s_tot[threadIdx.x] = 0ull;
     __syncthreads();
-    // the next list's descriptor, loaded one list ahead
-    auto load_desc = [&](int list, TileDev& td, int& nc, uint32_t (&c8)[2]) {
+    struct Desc {
+        TileDev tile;
+        int nc;
+        uint32_t c64;   // candidate `lane` (if < nc)
+        float2 v64;     // its 6-bit test inputs {bound side, √|x|² (COSINE)}
+    };
+    auto load_desc = [&](int list, Desc& d) {
         const int l = list < l1 ? list : l0;   // (clamped: a valid address, unused)
-        td = p.tiles[l >> 2];
-        nc = p.cnt6[cnt_base + l];
-        const uint32_t* cb = p.cand6 + (size_t)l * p.cap6;
-        c8[0] = cb[cg];
-        c8[1] = cb[4 + cg];
+        d.tile = p.tiles[l >> 2];
+        d.nc = p.cnt6[cnt_base + l];
+        d.c64 = p.cand6[(size_t)l * p.cap6 + lane];
+        d.v64 = p.cand6v[(size_t)l * p.cap6 + lane];
     };
     int cur_shard = -1, cur_seg = -1;
     uint64_t fkey = 0ull;
+    float tqf = 0.0f;   // the final floor's quick threshold (the 6-bit re-test)
     const int4* X8 = nullptr;
     const float4* AX8 = nullptr;
     const float* XN = nullptr;
     uint32_t vbase = 0;
-    unsigned long long vis = 0, reb = 0, reb_seg = 0;   // (current segment's) visited rows and re-bounds
+    unsigned long long vis = 0, reb = 0, reb_seg = 0, gathered = 0;   // (current segment's) visited rows, re-bounds
 #ifdef OSK_TESTING
     unsigned long long n_pass = 0;
     const long long t_begin = clock64();
@@ -477,17 +492,16 @@ __global__ __launch_bounds__(kBlock) void sq6_rebound(Sq8Params p) {
             if (p.seg_rebound && reb_seg) atomicAdd(&p.seg_rebound[cur_seg], reb_seg);
         }
     };
-    TileDev td_n;
-    int nc_n = 0;
-    uint32_t c8_n[2] = {0u, 0u};
-    if (l0 < l1) load_desc(l0, td_n, nc_n, c8_n);
+    uint32_t* sel = s_sel[wave];
+    Desc dn;
+    if (l0 < l1) load_desc(l0, dn);
     for (int list = l0; list < l1; list += dl) {
-        TileDev tile = td_n;   // (every lane loaded the same descriptor: keep it in SGPRs)
+        const Desc d = dn;
+        if (list + dl < l1) load_desc(list + dl, dn);
+        TileDev tile = d.tile;   // (every lane loaded the same descriptor: keep it in SGPRs)
         tile.seg = __builtin_amdgcn_readfirstlane(tile.seg);
         tile.shard = __builtin_amdgcn_readfirstlane(tile.shard);
-        const int nc = __builtin_amdgcn_readfirstlane(nc_n);
-        const uint32_t c8[2] = {c8_n[0], c8_n[1]};
-        if (list + dl < l1) load_desc(list + dl, td_n, nc_n, c8_n);
+        const int nc = __builtin_amdgcn_readfirstlane(d.nc);
         if (tile.seg != cur_seg) {   // (wave-uniform) the segment's pointers; flush its counts
             flush_seg();
             vis = 0;
@@ -498,22 +512,39 @@ __global__ __launch_bounds__(kBlock) void sq6_rebound(Sq8Params p) {
             XN = p.segs[tile.seg].xnorm_f;
             vbase = (uint32_t)p.seg_vrow[tile.seg];
         }
-        if (tile.shard != cur_shard) {   // the shard's floor
+        if (tile.shard != cur_shard) {   // the shard's final floor
             cur_shard = tile.shard;
             fkey = (uint64_t)(floor_lds ? s_floor[tile.shard] : shard_floor(tile.shard)) << 32;
             if (!(key_score(fkey) > 0.0f)) fkey = 0ull;
+            tqf = sq8_quick(sim, fkey, sqn0, p.cos_slack);
         }
         if ((list & 3) == 0) vis += (unsigned long long)(tile.row_end - tile.row_begin);   // (each tile once)
         reb += (unsigned long long)nc;
         reb_seg += (unsigned long long)nc;
         uint64_t lk0 = 0ull, thr0 = 0ull;
         uint32_t lp0 = 0u;
-        float tq0 = sq8_quick(sim, fkey, sqn0, p.cos_slack);
-        const uint32_t* cbuf = p.cand6 + (size_t)list * p.cap6;
         if (nc <= p.cap6) {
-            // 8 candidates per pass (two halves of 4 rows × 16 lanes), every load of both halves issued before
-            // any is used: one round trip per 8 candidates (the first 8 came with the descriptor)
-            for (int c0 = 0; c0 < nc; c0 += 8) {
+            // the 6-bit re-test against the final floor, survivors compacted into sel (64 candidates per
+            // round; the first 64 came with the descriptor)
+            int ns = 0;
+            for (int c0 = 0; c0 < nc; c0 += 64) {
+                uint32_t r = d.c64;
+                float2 v = d.v64;
+                if (c0 > 0 && c0 + lane < nc) {
+                    r = p.cand6[(size_t)list * p.cap6 + c0 + lane];
+                    v = p.cand6v[(size_t)list * p.cap6 + c0 + lane];
+                }
+                const bool keep = c0 + lane < nc && (!p.rb_retest || sq8_pass(sim, v.x, v.x, tqf, v.y));
+                const uint64_t km = __ballot(keep);
+                if (keep)
+                    sel[ns + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(km >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)km, 0u))] = r;
+                ns += __popcll(km);
+            }
+            gathered += (unsigned long long)ns;
+            float tq0 = tqf;
+            // 8 survivors per pass (two halves of 4 rows × 16 lanes), every load of a pass issued before any
+            // is used
+            for (int c0 = 0; c0 < ns; c0 += 8) {
 #ifdef OSK_TESTING
                 ++n_pass;
 #endif
@@ -521,14 +552,14 @@ __global__ __launch_bounds__(kBlock) void sq6_rebound(Sq8Params p) {
                 uint32_t r[2];
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {   // (a slot past the count reads row 0: a valid address, masked after)
-                    v[h] = c0 + 4 * h + cg < nc;
-                    r[h] = !v[h] ? 0u : c0 == 0 ? c8[h] : cbuf[c0 + 4 * h + cg];
+                    v[h] = c0 + 4 * h + cg < ns;
+                    r[h] = v[h] ? sel[c0 + 4 * h + cg] : 0u;
                 }
                 int4 xv[2][C];
                 float4 ax[2];
                 float xnd[2] = {0.0f, 0.0f};
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {   // unconditional loads of clamped rows, masked after
+                for (int h = 0; h < 2; ++h) {
                     const int4* xr = X8 + (int64_t)r[h] * u8;
 #pragma unroll
                     for (int i = 0; i < C; ++i) xv[h][i] = ct + 16 * i < u8 ? xr[ct + 16 * i] : make_int4(0, 0, 0, 0);
@@ -575,23 +606,29 @@ __global__ __launch_bounds__(kBlock) void sq6_rebound(Sq8Params p) {
         if (lane == 0) p.list_lbmax[l] = m;
     }
     flush_seg();
-    // the wave's re-bound total, and (LDS mode) the workgroup's per-segment counts: one atomic each
-    // (same-address atomics queue at L2: per list they would serialise)
-    if (lane == 0 && p.counters && reb) atomicAdd(&p.counters[3], reb);
+    // the workgroup's totals: reduced in LDS, then one global atomic each per workgroup
+    if (lane == 0) {
+        atomicAdd(&s_tot[0], reb);
+        atomicAdd(&s_tot[1], gathered);
 #ifdef OSK_TESTING
-    if (lane == 0 && p.counters) {   // [11] the slowest wave's passes, [12] all passes, [13] the slowest wave's clocks
-        atomicMax(&p.counters[11], n_pass);
-        atomicAdd(&p.counters[12], n_pass);
-        atomicMax(&p.counters[13], (unsigned long long)(clock64() - t_begin));
-    }
+        atomicAdd(&s_tot[2], n_pass);
+        atomicMax(&s_tot[3], (unsigned long long)(clock64() - t_begin));
 #endif
-    if (seg_lds) {
-        __syncthreads();
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && p.counters) {
+        if (s_tot[0]) atomicAdd(&p.counters[3], s_tot[0]);
+        if (s_tot[1]) atomicAdd(&p.counters[11], s_tot[1]);   // rows gathered from the int8 copy
+#ifdef OSK_TESTING
+        atomicAdd(&p.counters[12], s_tot[2]);   // 8-row passes
+        atomicMax(&p.counters[13], s_tot[3]);   // the slowest workgroup's clocks
+#endif
+    }
+    if (seg_lds)
         for (int i = threadIdx.x; i < p.n_segs; i += kBlock) {
             if (p.visited && p.q0 == 0 && s_vis[i]) atomicAdd(&p.visited[i], s_vis[i]);
             if (p.seg_rebound && s_reb[i]) atomicAdd(&p.seg_rebound[i], s_reb[i]);
         }
-    }
 }
 
 // row groups per wave-iteration by C: ≈ 12–14 KiB of loads in flight per wave
@@ -605,16 +642,31 @@ static const Sq6Fn kSq6Rebound[5] = {sq6_rebound<2>, sq6_rebound<3>, sq6_rebound
 hipError_t launch_sq6_scan(const Sq8Params& p, int dim, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
     const int C = sq6_chunks(dim);
     if (C < 2 || C > 6 || p.q_count != 1 || p.k < 1 || p.k > kKQ || !p.floor || !p.q6 || !p.cand6 || !p.cnt6 ||
-        !p.tile_order || p.cap6 < 1)
+        !p.tile_order || p.cap6 < 64 || p.cap6 > kSq6Cap || !p.cand6v)
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(kSq6Pilot[C - 2], dim3(p.n_tiles), dim3(kBlock), 0, s, p);
+    const Sq6Fn scan = kSq6[C - 2];
     if (ev_start || ev_stop)
-        hipExtLaunchKernelGGL(kSq6[C - 2], dim3(p.n_tiles), dim3(kBlock), 0, s, ev_start, ev_stop, 0, p);
+        hipExtLaunchKernelGGL(scan, dim3(p.n_tiles), dim3(kBlock), 0, s, ev_start, ev_stop, 0, p);
     else
-        hipLaunchKernelGGL(kSq6[C - 2], dim3(p.n_tiles), dim3(kBlock), 0, s, p);
-    // the re-bound: persistent waves, a few lists each (4 workgroups of 4 waves per CU at most)
-    const int rb_grid = std::max(1, std::min(p.n_tiles, 4 * (p.wide_grid > 0 ? p.wide_grid : 256)));
-    hipLaunchKernelGGL(kSq6Rebound[C - 2], dim3(rb_grid), dim3(kBlock), 0, s, p);
+        hipLaunchKernelGGL(scan, dim3(p.n_tiles), dim3(kBlock), 0, s, p);
+    // the re-bound: persistent waves, a few lists each — as many workgroups per CU as fit at once (the
+    // kernel's registers decide: 4 at ≤ 128 VGPRs), so no wave waits for another's lists to finish
+    const Sq6Fn rb = kSq6Rebound[C - 2];
+    static std::atomic<int> s_fit[5];   // (zero-initialised; the same value from every thread)
+    std::atomic<int>& fit_of = s_fit[C - 2];
+    int fit = fit_of.load(std::memory_order_relaxed);
+    if (fit == 0) {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(rb), kBlock, 0) != hipSuccess ||
+            n < 1)
+            n = 1;
+        fit = std::min(n, 8);
+        fit_of.store(fit, std::memory_order_relaxed);
+    }
+    const int per_cu = p.rb_wg_per_cu > 0 ? p.rb_wg_per_cu : fit;
+    const int rb_grid = std::max(1, std::min(p.n_tiles, per_cu * (p.wide_grid > 0 ? p.wide_grid : 256)));
+    hipLaunchKernelGGL(rb, dim3(rb_grid), dim3(kBlock), 0, s, p);
     return hipGetLastError();
 }
 

@@ -24,6 +24,11 @@
 //     query) list by an LDS atomic; lists that would fill go through sq8_mfma's ordered insertion.  The
 //     per-row test is relaxed to the quarter's row maxima (launch_wide_quarter_max) and is provably no
 //     stricter than sq8_bounds' upper side (derivation at quick_consts);
+//   * deferred insertions (main pass, when LDS allows: wide_qcap): the slow path only runs the per-row test
+//     on the step's accumulators and appends each passing pair {int32 dot, row << 8 | query} to the wave's
+//     LDS queue; the queue drains — precise bounds, floor check, list appends, 64 pairs per wave iteration —
+//     at the quarter's end (or when full).  The step's barrier then waits for a short per-row test, not for
+//     the slowest wave's bounds and atomics (C4 b256 9.0 → 7.5 ms, C3 b256 5.8 → 4.3 ms, profiles/r05d/);
 //   * floors: pilot = 1 bounds each quarter's first step of rows (the best lower-bound key per query; their k-th
 //     per (query, shard) floors the main pass); the main pass runs in two launches — 1/phase of the quarters
 //     first, then the rest under floors raised to the k-th best list maximum of the first (launch_wide_floor;

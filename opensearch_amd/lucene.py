@@ -318,17 +318,47 @@ class _GpuKnnVectorQuery:
     segment's reader closes (a refresh or merge dropped it), every cached view over it is released, so a
     view never pins the HBM of segments no searcher can reach.  Creation is under a lock, so concurrent
     rewrites of one leaf set share one view."""
-    _views: dict = {}
+    _views: dict = {}          # leaf-set key → _CachedView
     _views_lock = threading.Lock()
 
-    def _shard_view(self, leaves: Sequence[LeafReaderContext]) -> "DeviceShardSet":
+    class _CachedView:
+        """A cached view and its users: rewrites in flight hold a use, and an evicted view closes when the
+        last of them finishes (never under a search)."""
+        __slots__ = ("view", "users", "evicted")
+
+        def __init__(self, view):
+            self.view, self.users, self.evicted = view, 0, False
+
+    def _acquire_view(self, leaves: Sequence[LeafReaderContext]) -> "_GpuKnnVectorQuery._CachedView":
         key = tuple((id(lf.reader), lf.reader.handle, lf.doc_base) for lf in leaves)
+        C_ = _GpuKnnVectorQuery
+        with C_._views_lock:
+            e = C_._views.get(key)
+            if e is None:
+                e = C_._CachedView(DeviceShardSet([list(leaves)], [0]))
+                C_._views[key] = e
+            e.users += 1
+            return e
+
+    @staticmethod
+    def _release_view(e: "_GpuKnnVectorQuery._CachedView") -> None:
         with _GpuKnnVectorQuery._views_lock:
-            v = _GpuKnnVectorQuery._views.get(key)
-            if v is None:
-                v = DeviceShardSet([list(leaves)], [0])
-                _GpuKnnVectorQuery._views[key] = v
-            return v
+            e.users -= 1
+            close = e.evicted and e.users == 0
+        if close:
+            e.view.close()
+
+    @staticmethod
+    def _evict(entries) -> None:
+        """Evicted entries (already out of the cache): close the idle ones now, the busy ones on release."""
+        with _GpuKnnVectorQuery._views_lock:
+            idle = []
+            for e in entries:
+                e.evicted = True
+                if e.users == 0:
+                    idle.append(e)
+        for e in idle:
+            e.view.close()
 
     # (the cache is the base class's: subclasses' classmethods must not rebind it on themselves)
     @staticmethod
@@ -336,9 +366,8 @@ class _GpuKnnVectorQuery:
         C_ = _GpuKnnVectorQuery
         with C_._views_lock:
             gone = [k for k in C_._views if any(rid == id(reader) for rid, _, _ in k)]
-            views = [C_._views.pop(k) for k in gone]
-        for v in views:
-            v.close()
+            entries = [C_._views.pop(k) for k in gone]
+        C_._evict(entries)
 
     @staticmethod
     def cached_views() -> int:
@@ -347,23 +376,26 @@ class _GpuKnnVectorQuery:
 
     @staticmethod
     def release_views() -> None:
-        """Drop every cached view (the segments stay with their readers)."""
+        """Drop every cached view (the segments stay with their readers; a view in use closes when its
+        search finishes)."""
         C_ = _GpuKnnVectorQuery
         with C_._views_lock:
-            views = list(C_._views.values())
+            entries = list(C_._views.values())
             C_._views.clear()
-        for v in views:
-            v.close()
+        C_._evict(entries)
 
     def rewrite(self, leaves: Iterable[LeafReaderContext]) -> TopDocs:
         leaves = [lf for lf in leaves if lf.reader.field == self.field]
         if not leaves:
             return TopDocs(TotalHits(0), [])
-        view = self._shard_view(leaves)
-        accept = [self._accept(lf) for lf in leaves]
-        if all(a is None for a in accept):
-            accept = None
-        s, d, _, c, _, _ = view.search(self.target, self.k, 0, self.k, accept=accept)
+        e = self._acquire_view(leaves)
+        try:
+            accept = [self._accept(lf) for lf in leaves]
+            if all(a is None for a in accept):
+                accept = None
+            s, d, _, c, _, _ = e.view.search(self.target, self.k, 0, self.k, accept=accept)
+        finally:
+            self._release_view(e)
         n = int(c[0])
         return TopDocs(TotalHits(n), [ScoreDoc(int(d[0, i]), float(s[0, i])) for i in range(n)])
 

@@ -73,10 +73,12 @@ def test_one_call_per_shard_equals_per_leaf_and_oracle(shard, filtered):
     for qi in range(4):
         q = O.synth(0, 1, DIM, 950 + qi, 3)[0]
         gq = LU.GpuKnnFloatVectorQuery("v", q, K, filt)
-        view = gq._shard_view(leaves)
+        e = gq._acquire_view(leaves)
+        view = e.view
         calls = view.counter("sq8_calls") + view.counter("select_calls")
         one = gq.rewrite(leaves)
         assert view.counter("sq8_calls") + view.counter("select_calls") == calls + 1   # one device search per shard
+        gq._release_view(e)
         per_leaf = LU.KnnFloatVectorQuery("v", q, K, filt).rewrite(leaves)
         es, ed = oracle(leaves, rows, q, gq._accept)
         for td in (one, per_leaf):
@@ -126,6 +128,32 @@ def test_view_cache_is_evicted_when_a_reader_closes_and_shared_under_concurrency
         assert all([sd.doc for sd in o.score_docs] == [sd.doc for sd in outs[0].score_docs] for o in outs)
         readers[0].close()
         assert LU.GpuKnnFloatVectorQuery.cached_views() == 0
+    finally:
+        for r in readers:
+            r.close()
+        LU.GpuKnnFloatVectorQuery.release_views()
+
+
+def test_evicted_view_stays_open_until_its_last_search_finishes():
+    """A reader that closes while a rewrite holds its cached view evicts the entry at once, but the view
+    itself closes only when that rewrite releases it (no view closed under a search)."""
+    LU.GpuKnnFloatVectorQuery.release_views()
+    rows = [O.synth(0, n, DIM, 970 + i, 3) for i, n in enumerate([600, 500])]
+    readers = [LU.GpuFlatVectorsReader("v", r, COS) for r in rows]
+    leaves = [LU.LeafReaderContext(0, 0, readers[0]), LU.LeafReaderContext(1, 600, readers[1])]
+    q = O.synth(0, 1, DIM, 971, 3)[0]
+    gq = LU.GpuKnnFloatVectorQuery("v", q, K)
+    try:
+        e = gq._acquire_view(leaves)   # a rewrite in flight
+        readers[1].close()             # the reader-closed listener runs under it
+        assert LU.GpuKnnFloatVectorQuery.cached_views() == 0 and e.evicted
+        assert e.view._h.value         # still open: its user has not finished
+        s, d, _, c, _, _ = e.view.search(q, K, 0, K)
+        es, ed = oracle(leaves, rows, q, gq._accept)
+        assert np.array_equal(d[0, :c[0]], ed) and np.array_equal(np.asarray(s[0, :c[0]], np.float32).view(np.uint32),
+                                                                  es.view(np.uint32))
+        gq._release_view(e)
+        assert not e.view._h.value     # the last user closed it
     finally:
         for r in readers:
             r.close()

@@ -423,3 +423,64 @@ def test_tier_off_frees_its_copy_without_waiting_for_other_streams():
         for r in big:
             r.close()
         close_all(ds, readers)
+
+
+def _rebound_variants(ds, queries, k):
+    """sq6_rebound's schedules (list assignment × workgroups per CU) and its final-floor re-test on and off,
+    on single queries."""
+    outs = {}
+    try:
+        for stride, wgs, retest in [(1, 0, 1), (0, 0, 1), (1, 1, 1), (0, 1, 1), (1, 0, 0)]:
+            _lib.tune("sq6_rebound_stride", stride)
+            _lib.tune("sq6_rebound_wgs", wgs)
+            _lib.tune("sq6_rebound_retest", retest)
+            outs[(stride, wgs, retest)] = one_by_one(lambda q: ds.search(q, k, 0, k), queries)
+    finally:
+        _lib.tune("sq6_rebound_stride", 1)
+        _lib.tune("sq6_rebound_wgs", 0)
+        _lib.tune("sq6_rebound_retest", 1)
+    return outs
+
+
+@pytest.mark.parametrize("layout", ["ragged", "70_shards", "70_segments"])
+def test_rebound_schedules_agree_with_the_oracle(layout):
+    """sq6_rebound's schedules — contiguous or strided lists, as many workgroups per CU as fit or one (every
+    wave walks many lists), the final-floor re-test on or off — give identical results, equal to the oracle; with more than 64 shards the floors and with more than 64 segments the
+    per-segment counts leave LDS for their global fallbacks."""
+    sim, dim, k = COS, 768, 10
+    if layout == "ragged":
+        sizes = [9001, 5, 3333, 12000, 77]
+        shard_of = [0, 1, 1, 2, 0]
+    elif layout == "70_shards":
+        sizes = [450 + 7 * i for i in range(70)]
+        shard_of = list(range(70))
+    else:
+        sizes = [300 + 11 * i for i in range(70)]
+        shard_of = [i % 3 for i in range(70)]
+    segs = [corpus(n, dim, sim, 300 + i) for i, n in enumerate(sizes)]
+    n_shards = max(shard_of) + 1
+    ds, readers = view_of(segs, sim, shard_of, list(range(n_shards)))
+    queries = corpus(3, dim, sim, 399)
+    _lib.tune("sq6_probe_pct", 100)   # (the small segments keep the tier whatever their probes count)
+    try:
+        for i in range(4):   # the calibration probes
+            ds.search(queries[:1], k, 0, k)
+        c0 = ds.counter("sq6_calls")
+        outs = _rebound_variants(ds, queries, k)
+        assert ds.counter("sq6_calls") - c0 == 5 * len(queries)
+        ref = outs[(1, 0, 1)]
+        for o in outs.values():
+            assert_same(o, ref)
+        s, d, sh, c, t, _ = ref
+        for i in range(len(queries)):
+            lists = []
+            for si in range(n_shards):
+                rows = np.concatenate([segs[j] for j in range(len(segs)) if shard_of[j] == si])
+                sc, dc, _ = O.exact_search(rows, queries[i], k, int(sim), O.ORDER_DEVICE)
+                lists.append((sc, dc))
+            es, ed, esh, et, _ = O.topdocs_merge(lists, 0, k, list(range(n_shards)))
+            assert np.array_equal(d[i, :c[i]], ed) and np.array_equal(sh[i, :c[i]], esh)
+            assert np.array_equal(bits(s[i, :c[i]]), bits(es)) and t[i] == et
+    finally:
+        _lib.tune("sq6_probe_pct", 10)
+        close_all(ds, readers)

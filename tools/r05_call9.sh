@@ -1,0 +1,9 @@
+set -u
+cd $GRAFT_REPO_ROOT
+bash tools/gpu_run.sh "test:sq6 or full_size or shard_query" \
+  "cmd:150:rb_f1.log:OSK_TESTING_LIB=0 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rb_f1 -o run -- python -u tools/rebound_diag.py 48" \
+  "cmd:150:rb_f0.log:OSK_TESTING_LIB=0 TUNE=sq6_fused=0 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rb_f0 -o run -- python -u tools/rebound_diag.py 48" \
+  "bench:--steps+500+--warmup+20+--no-cpu-baseline" \
+  "cmd:300:bench_f1.log:python -u bench.py --steps 300 --warmup 10 --inflight 1 --no-cpu-baseline" \
+  "cmd:300:prof_f1.log:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_f1 -o run -- python bench.py --steps 200 --warmup 10 --inflight 1 --no-cpu-baseline" \
+  "cmd:400:wide_abl.log:ABLATE=0,1,2,64 python -u tools/wide_ablate.py C4 256 && ABLATE=0,1,2,64 python -u tools/wide_ablate.py C3 256"

@@ -1,10 +1,11 @@
-"""Single-query chain time on the 6-bit tier (C3 10M × 768 COSINE) and sq6_rebound's balance counters.
+"""Single-query chain time on the 6-bit tier (C3 10M × 768 COSINE) and sq6_rebound's counters.
 
     TUNE=sq6_rebound_stride=0 python tools/rebound_diag.py [n_queries]
 
-Runs on the testing build (the re-bound's per-wave pass counters).  Reports the GPU time of one search
-(HIP events around the whole chain, one in flight), the re-bound rows per search, and for sq6_rebound the
-slowest wave's 8-candidate passes against the mean, and the slowest wave's shader clocks."""
+Reports the GPU time of one search (HIP events around the whole chain, one in flight), the 6-bit candidates
+per search, how many of them survive the re-test against the final floor (the rows gathered from the int8
+copy), and on the testing build (OSK_TESTING_LIB=1, the default) the 8-row passes and the slowest
+workgroup's shader clocks."""
 import os
 os.environ.setdefault("OSK_TESTING_LIB", "1")
 import ctypes as C
@@ -40,7 +41,7 @@ def counter(name):
 for i in range(8):   # the calibration probes and warm-up
     shards.search(q[i].data_ptr(), 1, K, kk, cc, st)
 torch.cuda.synchronize()
-r0, p0 = counter("sq6_rebound_rows"), counter("sq6_rebound_passes")
+r0, g0, p0 = counter("sq6_rebound_rows"), counter("sq6_rebound_gathered_rows"), counter("sq6_rebound_passes")
 ms = []
 for i in range(NQ):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -50,10 +51,11 @@ for i in range(NQ):
     e1.synchronize()
     ms.append(e0.elapsed_time(e1))
 ms.sort()
-reb, passes = counter("sq6_rebound_rows") - r0, counter("sq6_rebound_passes") - p0
+reb, gat = counter("sq6_rebound_rows") - r0, counter("sq6_rebound_gathered_rows") - g0
+passes = counter("sq6_rebound_passes") - p0
 waves = 4 * 4 * 256
 print(f"{os.environ.get('TUNE', '')}: chain median {ms[len(ms) // 2] * 1e3:.1f} us, min {ms[0] * 1e3:.1f} us over "
       f"{NQ} queries; sq6 calls {counter('sq6_calls')}", flush=True)
-print(f"   re-bound rows/search {reb / NQ:.0f}; passes/search {passes / NQ:.0f} (mean per wave "
-      f"{passes / NQ / waves:.2f}); slowest wave ever: {counter('sq6_rebound_max_wave_passes')} passes, "
-      f"{counter('sq6_rebound_max_wave_cycles')} clocks", flush=True)
+print(f"   6-bit candidates/search {reb / NQ:.0f}, gathered after the final-floor re-test {gat / NQ:.0f}; "
+      f"passes/search {passes / NQ:.0f} (mean per wave {passes / NQ / waves:.2f}); slowest workgroup ever: "
+      f"{counter('sq6_rebound_max_wg_cycles')} clocks", flush=True)
