@@ -30,9 +30,10 @@ the wide int8 prefilter (≤ 256 dims, 256 queries per pass) or the bf16×3 MFMA
 roofline: the dominant kernel is HBM-bound; algorithmic bytes per launch = rows scanned × (576 + 16) B for
 sq6_scan (6-bit codes + 16-B bound terms, one query per launch; rows × (768 + 16) B for sq8_scan's int8 tier;
 rows × 768 × 4 B for the fp32 scan).  Its average duration is measured live from the kernel's own
-dispatch-packet timestamps (hipExtLaunchKernelGGL events, osk_view_profile) in the one-in-flight timed pass
-(overlapped launches share HBM with their neighbours, so their individual durations overstate the kernel's
-time); the whole step's sustained rate (bytes per step ÷ ms per step of the headline pass) is reported
+dispatch-packet timestamps (hipExtLaunchKernelGGL events, osk_view_profile) of every 8th search
+(`--profile-every`: a stamped launch costs a few µs of stream time, so the timed loop samples) in the
+one-in-flight timed pass (overlapped launches share HBM with their neighbours, so their individual durations
+overstate the kernel's time); the whole step's sustained rate (bytes per step ÷ ms per step of the headline pass) is reported
 beside it.  `--rank-share R/W` stages only the shards rank R of a W-GPU run owns (one shard of 1.25M rows
 at W = 8) on this one GPU: the per-GPU share of that run, without its all-gather.
 cpu_baseline: rank 0 at N = 1 only — the oracle's Lucene-equivalent restatement (Panama-512 order,
@@ -233,6 +234,9 @@ def main():
                     help="queries in flight: search threads issuing round-robin, each on its own stream with its "
                          "own view (workspace) over the shared segments; 1 = strictly one query after another")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-every", type=int, default=8,
+                    help="stamp the scan launches of every N-th search with HIP events (osk_view_profile N); the "
+                         "stamps cost a few µs of stream time around the stamped launch, so the timed loop samples")
     ap.add_argument("--no-sq8", action="store_true", help="measure the fp32 streaming scan as the main path")
     ap.add_argument("--exchange", choices=["osk", "torch"], default="osk",
                     help="osk: the C-ABI step osk_shards_search_merge_device (RCCL all-gather inside libosknn; "
@@ -343,7 +347,7 @@ def main():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        profile(1)
+        profile(max(1, a.profile_every))
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         if world > 1:
@@ -425,7 +429,7 @@ def main():
         bytes_per_launch = rows_local * (((DIM + 255) // 256) * 192 + 16)
         kernel_name = ("sq6_scan<C=3,U=3> the 6-bit pass of the certified prefilter (bytes = 6-bit codes + 16-B "
                        "bound terms per row, one query per launch; its pilot and int8 re-bound kernels read "
-                       "≈ 2 % more: sq6_pilot 0.041 GB, sq6_rebound 0.092 GB per launch, profiles/r04f/pmc/)")
+                       "≈ 2 % more: sq6_pilot 0.041 GB, sq6_rebound ≈ 0.07 GB after its final-floor re-test)")
     elif prefilter:
         passes = (B + 7) // 8
         bytes_per_launch = rows_local * (u8 * 16 + 16) * passes
@@ -523,7 +527,8 @@ def main():
                          "read_ceiling_source": os.path.relpath(READ_CEILING, ROOT) if ceiling else None,
                          "kernel": kernel_name, "scan_ms_avg": scan_avg_ms,
                          "scan_ms_measured_in": ("the one-in-flight pass of this run (isolated launches)" if F > 1
-                                                 else "the timed region"),
+                                                 else "the timed region")
+                         + f", every {max(1, a.profile_every)}th search's launch sampled",
                          "sustained_GBps": bytes_per_launch / (elapsed_max / a.steps) / 1e9,
                          "sustained_frac": bytes_per_launch / (elapsed_max / a.steps) / 1e9 / HBM_PEAK_GBS,
                          "overlapped_scan_ms_avg": ovl_scan_ms if F > 1 else None,

@@ -216,10 +216,11 @@ int32_t osk_merge_device_ranked(int32_t device, const uint64_t* d_keys, int32_t 
                                 int32_t* d_shard_out, int32_t* d_count, int64_t* d_total_hits,
                                 float* d_max_score, void* stream);
 
-/* Scan-kernel timing (benchmarks): enable/disable and reset; then read the summed duration of the
- * scan launches of every osk_view_search_device call since enabling (HIP events on the call's
- * stream) and the number of calls.  Enabling adds one event wait per call; keep it off in
- * production. */
+/* Scan-kernel timing (benchmarks): osk_view_profile(view, N) resets and, for N > 0, samples every N-th
+ * osk_view_search_device call (N = 1: every call; 0: off); osk_view_scan_time then reads the summed
+ * duration of the sampled calls' scan launches (HIP start/stop events stamped by the launches on the
+ * call's stream) and the number of sampled calls.  A sampled call pays a few µs of stream time for the
+ * stamps; keep it off in production. */
 int32_t osk_view_profile(osk_view* view, int32_t enable);
 int32_t osk_view_scan_time(osk_view* view, double* total_ms, int64_t* calls);
 

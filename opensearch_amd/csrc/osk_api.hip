@@ -1707,11 +1707,9 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             p.rb_stride = g_tuning.sq6_rebound_stride;
             p.rb_retest = g_tuning.sq6_rebound_retest;
             p.rb_wg_per_cu = g_tuning.sq6_rebound_wgs;
-            OSK_HIP(v->ws_cand6.reserve(sizeof(uint32_t) * (size_t)p.n_lists * kSq6Cap));
-            OSK_HIP(v->ws_cand6v.reserve(sizeof(float2) * (size_t)p.n_lists * kSq6Cap));
+            OSK_HIP(v->ws_cand6.reserve(sizeof(uint2) * (size_t)p.n_lists * kSq6Cap));
             OSK_HIP(v->ws_cnt6.reserve(sizeof(int32_t) * (size_t)nq * p.n_lists));
-            p.cand6 = v->ws_cand6.as<uint32_t>();
-            p.cand6v = v->ws_cand6v.as<float2>();
+            p.cand6 = v->ws_cand6.as<uint2>();
             p.cnt6 = v->ws_cnt6.as<int32_t>();
             p.cap6 = kSq6Cap;
             p.seg_rebound = probe6 ? v->d_seg_rebound.as<unsigned long long>() : nullptr;
@@ -1997,6 +1995,9 @@ int32_t view_search_device(osk_view* v, const void* d_queries, int nq, int k,
 
     int32_t rc;
     if ((prefilter || (select && sq8_on)) && (rc = ensure_sq8(v, st)) != OSK_OK) return rc;   // one-time build
+    // osk_view_profile(N): every N-th call stamps its scan launches (N = 1: every call); the event stamps cost
+    // a few µs of stream time around the stamped launch, so a long timed loop samples instead of stamping all
+    v->profile = v->profile_every > 0 && v->profile_tick++ % (uint64_t)v->profile_every == 0;
     if (v->profile && (rc = profile_begin(v, st, batched)) != OSK_OK) return rc;
     if (select) {
         rc = select_search(v, d_queries, nq, k, UP, d_accept, d_shard_keys, d_shard_counts, d_visited, st, sq8_on);
@@ -2094,8 +2095,11 @@ int32_t osk_view_profile(osk_view* v, int32_t enable) {
             OSK_HIP(hipEventCreate(&v->ev_stop[i]));
         }
     }
+    OSK_REQUIRE(enable >= 0, "enable must be >= 0");
     for (int i = 0; i < osk_view::kEvRing; ++i) v->ev_pending[i] = false;
-    v->profile = enable != 0;
+    v->profile = false;
+    v->profile_every = enable;
+    v->profile_tick = 0;
     v->scan_ms = 0.0;
     v->scan_calls = 0;
     v->ev_next = 0;

@@ -741,6 +741,12 @@ int32_t osk_shards_search_merge_device(osk_comm* comm, osk_view* view, const voi
         OSK_HIP(hipMemsetAsync(view->ws_xkeys.p, 0, sizeof(uint64_t) * B.keys, st));
         OSK_HIP(launch_xhdr_fill(view->ws_xkeys.as<uint64_t>() + B.keys, hw, d_queries, 0, view->d_shard_index.as<int32_t>(),
                                  view->n_shards, std::min(view->n_shards, comm->dev_max_spr), st));
+    } else if (comm->world == 1 && view->n_shards == shards_per_rank) {
+        // world 1 with no padding: the lists are the whole image and there is no other rank's header to
+        // compare, so neither the header nor the shard-index trailer is written (the reduce takes the view's
+        // shard indices directly) — one launch less per call
+        rc = search_padded(view, d_queries, n_queries, k, d_accept, shards_per_rank, st);
+        if (rc) return rc;
     } else {
         rc = fill_block(view, d_queries, n_queries, k, d_accept, shards_per_rank, hw, st, fixed ? &B : nullptr);
         if (rc) return rc;
@@ -758,7 +764,12 @@ int32_t osk_shards_search_merge_device(osk_comm* comm, osk_view* view, const voi
         image = view->ws_xgath.as<uint64_t>();
     }
     const int32_t* sidx = nullptr;
-    const XLayout x = image_layout(comm, image, B, &sidx);
+    XLayout x = image_layout(comm, image, B, &sidx);
+    if (comm->world == 1 && !over && view->n_shards == shards_per_rank) {   // (no header written: see above)
+        x.hdr = nullptr;
+        x.si_stride = shards_per_rank;
+        sidx = view->d_shard_index.as<int32_t>();
+    }
     // (a refusing rank reduces with the limits' shape: its outputs are count −1 like every other rank's)
     OSK_HIP(launch_coord_reduce(image, nullptr, sidx, over ? std::min(n_queries, comm->dev_max_nq) : n_queries,
                                comm->world, over ? comm->dev_max_spr : shards_per_rank, over ? std::min(k, comm->dev_max_k) : k,

@@ -176,9 +176,9 @@ struct Sq8Params {
     unsigned long long* counters;    // sq6_scan adds its int8 re-bounds to [3] (SettleParams::counters)
     unsigned long long* seg_rebound; // calibration probes: the int8 re-bounds per segment [n_segs], or null
     const int32_t* tile_order;       // sq6_scan: the tile of each workgroup (tiles interleaved over shards)
-    uint32_t* cand6;                 // sq6_scan → sq6_rebound: per list, the rows that passed the 6-bit test
+    uint2* cand6;                    // sq6_scan → sq6_rebound: per list, the rows that passed the 6-bit test
+                                     // {row, its 6-bit test value (osk_sq6.hip cand6_value)}
     int32_t* cnt6;                   // [q][n_lists] their count (> cap6: overflowed)
-    float2* cand6v;                  // per list, each candidate's 6-bit test inputs {bound side, √|x|² (COSINE)}
     int cap6;
     const float4* const* auxt;       // sq8_wide: per segment, the 16-row groups' bound terms (launch_sq8w_build)
     int wide_grid;                   // sq8_wide: persistent workgroups (the device's CUs)

@@ -199,7 +199,7 @@ struct osk_view {
     bool sq6_ready = false;                           // the view does not use it)
     int64_t sq6_calls = 0;
     osk::DevBuf ws_q6, ws_qc6, ws_floor;              // its query (nibble split, bound terms), floor buckets,
-    osk::DevBuf ws_cand6, ws_cnt6, ws_cand6v;         // the streaming pass's candidates per list (+ test inputs)
+    osk::DevBuf ws_cand6, ws_cnt6;                    // the streaming pass's candidates per list {row, 6-bit test}
     // the tier's calibration (per segment, osk_seg::sq6_state): a probe call of this view counts its int8
     // re-bounds per segment into d_seg_rebound, copies them to h_seg_rebound on its stream and records
     // ev_probe; a later call folds them into the segments once the event has completed — nothing waits
@@ -233,7 +233,9 @@ struct osk_view {
     // folded into scan_ms when a slot is reused (kEvRing calls later: long complete, no host wait) or
     // when the total is read — timing never blocks the host inside the timed loop
     static constexpr int kEvRing = 64;
-    bool profile = false;
+    bool profile = false;            // the current call stamps its scan launches (osk_view_profile)
+    int profile_every = 0;           // osk_view_profile(enable): 0 off, N = every N-th call is sampled
+    uint64_t profile_tick = 0;
     hipEvent_t ev_start[kEvRing] = {}, ev_stop[kEvRing] = {};
     bool ev_pending[kEvRing] = {};
     int64_t ev_next = 0;                  // calls started since enabling

@@ -239,8 +239,23 @@ __global__ __launch_bounds__(kBlock) void sq6_pilot(Sq8Params p) {
     if (lane == 0 && best) atomicMax(fb + ((tix * 4 + wave) & (kFloorBuckets - 1)) * kFloorStride, best);
 }
 
+// A candidate's 6-bit test in one float, for the re-bound's re-test against the final floor's quick
+// threshold tq (cand6_keep): the bound side itself (EUCLIDEAN: keep unless v > tq; dot kinds: unless v < tq),
+// COSINE the side over √|x|² rounded up (keep unless v < tq: never stricter than the real-valued
+// side ≥ tq·√|x|², which the quick threshold's slack covers like the scan's own test; a zero row keeps).
+__device__ __forceinline__ float cand6_value(int sim, float side6, float sx) {
+    if (sim != SIM_COSINE) return side6;
+    if (!(sx > 0.0f)) return __builtin_inff();
+    const float v = side6 / sx;
+    return v + fmaxf(fabsf(v) * 0x1p-22f, 0x1p-126f);   // (≥ 2 ulps up: covers the division's rounding)
+}
+__device__ __forceinline__ bool cand6_keep(int sim, float v, float tq) {
+    return sim == SIM_EUCLIDEAN ? !(v > tq) : !(v < tq);
+}
+
 // The streaming pass: 6-bit dot of every row, the 6-bit bound's upper side against the shard's floor,
-// and the rows that pass appended to the wave's candidate buffer (cand6[list][cap6], count in cnt6;
+// and the rows that pass appended to the wave's candidate buffer (cand6[list][cap6]: {row, its 6-bit test
+// value (cand6_value)}, count in cnt6;
 // cnt6 > cap6 = overflowed) for the int8 re-bound pass.  A row dropped here has ub6 < T ≤ the shard's
 // k-th best exact score: it cannot enter the top k.  The best 6-bit lower bound among a wave's passing
 // rows raises its floor bucket as the pass goes (a distinct row per bucket, as for the pilot's).
@@ -280,7 +295,7 @@ __global__ __launch_bounds__(kBlock, 4) void sq6_scan(Sq8Params p) {   // ≤ 12
 
     const int list = tix * 4 + wave;
     uint32_t* fb = p.floor + ((size_t)p.q0 * p.n_shards + tile.shard) * (kFloorBuckets + 1) * kFloorStride;
-    uint32_t* cbuf = p.cand6 + (size_t)list * p.cap6;
+    uint2* cbuf = p.cand6 + (size_t)list * p.cap6;
     uint64_t fkey = 0ull;
     uint32_t best = 0u;
     float tq0 = sq8_quick(sim, 0ull, 0.0f, 0.0f);
@@ -385,8 +400,7 @@ __global__ __launch_bounds__(kBlock, 4) void sq6_scan(Sq8Params p) {   // ≤ 12
         const int slot = nc + __popcll(pm & ((1ull << lane) - 1ull));
         if (pass6) {
             if (slot < p.cap6 && !(ablate & 4)) {   // the row and its 6-bit test inputs (the re-bound re-tests)
-                cbuf[slot] = (uint32_t)row;
-                if (p.rb_retest) p.cand6v[(size_t)list * p.cap6 + slot] = make_float2(side6, sx);
+                cbuf[slot] = make_uint2((uint32_t)row, __float_as_uint(cand6_value(sim, side6, sx)));
             }
             if (!(ablate & 8)) {
                 float lo, hi;
@@ -460,15 +474,13 @@ __global__ __launch_bounds__(kBlock) void sq6_rebound(Sq8Params p) {
     struct Desc {
         TileDev tile;
         int nc;
-        uint32_t c64;   // candidate `lane` (if < nc)
-        float2 v64;     // its 6-bit test inputs {bound side, √|x|² (COSINE)}
+        uint2 c64;      // candidate `lane` (if < nc): {row, its 6-bit test value}
     };
     auto load_desc = [&](int list, Desc& d) {
         const int l = list < l1 ? list : l0;   // (clamped: a valid address, unused)
         d.tile = p.tiles[l >> 2];
         d.nc = p.cnt6[cnt_base + l];
         d.c64 = p.cand6[(size_t)l * p.cap6 + lane];
-        d.v64 = p.cand6v[(size_t)l * p.cap6 + lane];
     };
     int cur_shard = -1, cur_seg = -1;
     uint64_t fkey = 0ull;
@@ -528,13 +540,10 @@ __global__ __launch_bounds__(kBlock) void sq6_rebound(Sq8Params p) {
             // round; the first 64 came with the descriptor)
             int ns = 0;
             for (int c0 = 0; c0 < nc; c0 += 64) {
-                uint32_t r = d.c64;
-                float2 v = d.v64;
-                if (c0 > 0 && c0 + lane < nc) {
-                    r = p.cand6[(size_t)list * p.cap6 + c0 + lane];
-                    v = p.cand6v[(size_t)list * p.cap6 + c0 + lane];
-                }
-                const bool keep = c0 + lane < nc && (!p.rb_retest || sq8_pass(sim, v.x, v.x, tqf, v.y));
+                uint2 c = d.c64;
+                if (c0 > 0 && c0 + lane < nc) c = p.cand6[(size_t)list * p.cap6 + c0 + lane];
+                const uint32_t r = c.x;
+                const bool keep = c0 + lane < nc && (!p.rb_retest || cand6_keep(sim, __uint_as_float(c.y), tqf));
                 const uint64_t km = __ballot(keep);
                 if (keep)
                     sel[ns + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(km >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)km, 0u))] = r;
@@ -642,7 +651,7 @@ static const Sq6Fn kSq6Rebound[5] = {sq6_rebound<2>, sq6_rebound<3>, sq6_rebound
 hipError_t launch_sq6_scan(const Sq8Params& p, int dim, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
     const int C = sq6_chunks(dim);
     if (C < 2 || C > 6 || p.q_count != 1 || p.k < 1 || p.k > kKQ || !p.floor || !p.q6 || !p.cand6 || !p.cnt6 ||
-        !p.tile_order || p.cap6 < 64 || p.cap6 > kSq6Cap || !p.cand6v)
+        !p.tile_order || p.cap6 < 64 || p.cap6 > kSq6Cap)
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(kSq6Pilot[C - 2], dim3(p.n_tiles), dim3(kBlock), 0, s, p);
     const Sq6Fn scan = kSq6[C - 2];
