@@ -1461,15 +1461,15 @@ int32_t fold_probe(osk_view* v, hipStream_t st) {
 // The prefilter's two int8 MFMA kernels, in µs for this view's R rows (measured end to end on MI355X,
 // DESIGN.md §3c): sq8_mfma per launch of ≤ 32 queries streams R·(int8 row + 16-B bound terms) at ≈ 4.3 TB/s
 // + ≈ 165 µs + 0.28 µs per dim (pilot, merge, settle, re-score); the wide kernel per launch of ≤ 256 queries
-// ≈ R·KS·0.0454 ns (it is issue-bound, not HBM-bound: C4 9.4 ms per 256) + ≈ 300 µs (pilot, two passes,
-// floors, settle: C2 0.39 ms per 256).
+// ≈ R·KS·0.031 ns (it is issue-bound, not HBM-bound: C4 6.35 ms per 256 at b1024, C3 4.07 ms at b256, round 5
+// with deferred insertions, profiles/r05d/) + ≈ 300 µs (pilot, two passes, floors, settle: C2 0.33 ms per 256).
 double sq8_narrow_us(double R, int nq, int u8, int dim) {
     return (double)((nq + 31) / 32) * (R * (16.0 * u8 + 16.0) / 4.3e6 + 165.0 + 0.28 * dim);
 }
 double sq8_wide_us(double R, int nq, int u8) {
-    return (double)((nq + kWideQ - 1) / kWideQ) * (R * sq8_wide_ks(u8) * 0.0454e-3 + 300.0);
+    return (double)((nq + kWideQ - 1) / kWideQ) * (R * sq8_wide_ks(u8) * 0.031e-3 + 300.0);
 }
-// the wide kernel takes an unfiltered batch of ≥ sq8_wide_min queries of ≤ 256 dims when the model has it
+// the wide kernel takes an unfiltered batch of ≥ sq8_wide_min queries of ≤ 768 dims when the model has it
 // cheaper than sq8_mfma (C4: from about 96 queries)
 bool sq8_wide_pick(const osk_view* v, int nq, bool filtered) {
     const int u8 = (v->dim + 15) / 16;

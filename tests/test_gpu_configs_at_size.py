@@ -86,7 +86,7 @@ def _wide_ks(dim):
 
 
 def _wide_us(rows, dim, nq):
-    return ((nq + 255) // 256) * (rows * _wide_ks(dim) * 0.0454e-3 + 300.0)
+    return ((nq + 255) // 256) * (rows * _wide_ks(dim) * 0.031e-3 + 300.0)
 
 
 def _narrow_us(rows, dim, nq):
