@@ -2189,7 +2189,7 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
     const bool dev = n == "sq8_fallback_queries" || n == "sq8_rescored_rows" || n == "sq8_exact_tiles" ||
                      n == "sq6_rebound_rows" || n == "sq8_wide_events" || n == "sq8_wide_pairs" ||
                      n == "sq8_wide_wait_cycles" || n == "sq8_wide_slow_steps" || n == "sq8_wide_loop_cycles" ||
-                     n == "sq8_wide_quarter_cycles" || n == "sq8_wide_consts_cycles" ||
+                     n == "sq8_wide_slow_cycles" || n == "sq8_wide_drain_cycles" ||
                      n == "sq6_rebound_gathered_rows" || n == "sq6_rebound_passes" ||
                      n == "sq6_rebound_max_wg_cycles";
     OSK_REQUIRE(dev || n == "mfma_calls" || n == "mfma_fallback_queries" || n == "sq8_calls" || n == "sq6_calls" ||
@@ -2210,8 +2210,8 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
                              : n == "sq8_exact_tiles" ? c[2] : n == "sq6_rebound_rows" ? c[3]
                              : n == "sq8_wide_events" ? c[4] : n == "sq8_wide_pairs" ? c[5]
                              : n == "sq8_wide_wait_cycles" ? c[6] : n == "sq8_wide_slow_steps" ? c[7]
-                             : n == "sq8_wide_loop_cycles" ? c[8] : n == "sq8_wide_quarter_cycles" ? c[9]
-                             : n == "sq8_wide_consts_cycles" ? c[10] : n == "sq6_rebound_gathered_rows" ? c[11]
+                             : n == "sq8_wide_loop_cycles" ? c[8] : n == "sq8_wide_slow_cycles" ? c[9]
+                             : n == "sq8_wide_drain_cycles" ? c[10] : n == "sq6_rebound_gathered_rows" ? c[11]
                              : n == "sq6_rebound_passes" ? c[12] : c[13]);
         } else {
             sum += n == "mfma_calls" ? s->mfma_calls : n == "mfma_fallback_queries" ? s->mfma_fallback_queries

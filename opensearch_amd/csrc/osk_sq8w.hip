@@ -538,6 +538,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
 #ifdef OSK_TESTING
     uint32_t n_events = 0, n_pairs = 0, n_slow = 0;   // insertion events, quick-test passes, slow-path steps
     uint64_t cyc_wait = 0, cyc_loop = 0;   // wave 0's clocks: the step loop's waits, the whole loop
+    uint64_t cyc_slow = 0, cyc_drain = 0;  // …the slow path's (deferred) enqueues, the quarter-end drains + flushes
 #endif
     float ca[QB], cb[QB];   // the current quarter's quick-test constants
     // a quarter ends: its lists (this wave's queries, 4 per pass of 16 lanes) → the settle's arrays, zeroed
@@ -733,6 +734,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
             if (!__ballot(!(run < 0.0f)) && !zany) return;
 #ifdef OSK_TESTING
             ++n_slow;
+            const uint64_t c_slow0 = clock64();
 #endif
             if (!(SIM == SIM_EUCLIDEAN && KS == 2) && qcap > 0 && !(ablate & 32)) {
                 // deferred mode: the passing pairs of each (group, query block) whose vote passed go to the wave's
@@ -795,6 +797,9 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                         qn = base;
                     }
                 }
+#ifdef OSK_TESTING
+                cyc_slow += clock64() - c_slow0;
+#endif
                 return;
             }
             // (2) the slow path: per group the wave's queries with a group that may pass (wave-uniform)
@@ -965,8 +970,14 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
             if (ablate & 64) continue;   // (A/B: the ring alone)
             if (pq < 0 || ++pst == steps_of(pq)) {   // a new quarter: flush the last one, take its floors
                 if (pq >= 0 && !pilot) {
+#ifdef OSK_TESTING
+                    const uint64_t c_dr0 = clock64();
+#endif
                     if (qn) drain(s_quart[pq]);
                     flush(s_quart[pq]);
+#ifdef OSK_TESTING
+                    cyc_drain += clock64() - c_dr0;
+#endif
                 }
                 do ++pq; while (steps_of(pq) == 0);
                 pst = 0;
@@ -1097,6 +1108,8 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
             if (wave == 0) {
                 atomicAdd(&p.counters[6], (unsigned long long)cyc_wait);
                 atomicAdd(&p.counters[8], (unsigned long long)cyc_loop);
+                atomicAdd(&p.counters[9], (unsigned long long)cyc_slow);
+                atomicAdd(&p.counters[10], (unsigned long long)cyc_drain);
             }
         }
     }

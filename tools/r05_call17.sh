@@ -1,0 +1,3 @@
+set -u
+cd $GRAFT_REPO_ROOT
+bash tools/gpu_run.sh "cmd:400:wide_cnt.log:ABLATE=0 python -u tools/wide_ablate.py C4 256 && ABLATE=0 python -u tools/wide_ablate.py C3 256 && ABLATE=0 python -u tools/wide_ablate.py C2 256"

@@ -52,7 +52,7 @@ for ab in [int(x) for x in os.environ.get("ABLATE", "0,1,2,3").split(",")]:
     torch.cuda.synchronize()
     e0, p0, w0 = counter("sq8_wide_events"), counter("sq8_wide_pairs"), counter("sq8_wide_calls")
     x0 = [counter(c) for c in ("sq8_fallback_queries", "sq8_exact_tiles", "sq8_rescored_rows")]
-    cyc0 = [counter("sq8_wide_" + c + "_cycles") for c in ("wait", "loop")]
+    cyc0 = [counter("sq8_wide_" + c + "_cycles") for c in ("wait", "loop", "slow", "drain")]
     slow0 = counter("sq8_wide_slow_steps")
     check(lib().osk_view_profile(shards.view, 1))
     n = 5
@@ -69,7 +69,7 @@ for ab in [int(x) for x in os.environ.get("ABLATE", "0,1,2,3").split(",")]:
     x1 = [counter(c) - c0 for c0, c in zip(x0, ("sq8_fallback_queries", "sq8_exact_tiles", "sq8_rescored_rows"))]
     print(f"   settle per search: fallback queries {x1[0] / n:.1f}, exactly re-scanned lists {x1[1] / n:.1f}, "
           f"re-scored rows {x1[2] / n:.0f}", flush=True)
-    cyc = [counter("sq8_wide_" + c + "_cycles") - c0 for c0, c in zip(cyc0, ("wait", "loop"))]
+    cyc = [counter("sq8_wide_" + c + "_cycles") - c0 for c0, c in zip(cyc0, ("wait", "loop", "slow", "drain"))]
     slow = counter("sq8_wide_slow_steps") - slow0
     rows = NS * RPS
     wave_steps = launches * (rows / 16.0) * 8 / ({96: 8, 128: 8, 768: 2}.get(DIM, 4))
@@ -78,6 +78,7 @@ for ab in [int(x) for x in os.environ.get("ABLATE", "0,1,2,3").split(",")]:
     # wave 0's shader clocks summed over workgroups (pilot + main): per workgroup per search, and the split
     wgs = 256 * 2 * n
     print(f"   clocks per wg-launch (wave 0): loop {cyc[1] / wgs:.0f}, wait+barrier {cyc[0] / wgs:.0f} "
-          f"({cyc[0] / max(1, cyc[1]):.2f})", flush=True)
+          f"({cyc[0] / max(1, cyc[1]):.2f}), slow-path enqueues {cyc[2] / wgs:.0f} ({cyc[2] / max(1, cyc[1]):.2f}), "
+          f"quarter-end drains + flushes {cyc[3] / wgs:.0f} ({cyc[3] / max(1, cyc[1]):.2f})", flush=True)
 _lib.tune("sq8_mfma_ablate", 0)
 shards.close()
