@@ -1,0 +1,8 @@
+set -u
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 1130 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu_full.log 2>&1
+rc=$?
+tail -5 gpurun_out/pytest_gpu_full.log
+exit $rc
