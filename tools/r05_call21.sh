@@ -1,0 +1,3 @@
+set -u
+cd $GRAFT_REPO_ROOT
+bash tools/gpu_run.sh smoke "bench" prof pmc
