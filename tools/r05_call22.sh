@@ -1,0 +1,6 @@
+set -u
+cd $GRAFT_REPO_ROOT
+bash tools/gpu_run.sh "test:sq6 or full_size" \
+  "cmd:150:rb_p.log:OSK_TESTING_LIB=0 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rb_p -o run -- python -u tools/rebound_diag.py 64" \
+  "cmd:300:bench_f1.log:python -u bench.py --steps 300 --warmup 10 --inflight 1 --no-cpu-baseline" \
+  "bench:--steps+300+--warmup+20+--no-cpu-baseline"
