@@ -365,7 +365,8 @@ int sq8_wide_ks(int units8);                    // its 64-dim slabs per row: 2, 
 hipError_t launch_sq8_wide(const Sq8Params& p, hipStream_t s, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
 // The wide kernel's copy of a segment's fp32 rows (units float4 per row): int8 codes with ONE scale per
 // 16-row group (s_g = the group's max |x| / 127), in the MFMA-tiled layout (16-row blocks × sq8_wide_ks slabs of
-// 1 KiB, chunk-major), and per group kAuxGroupF4 float4 of bound terms (352 B): s_g[16], (s_g|q_x|)[16], |δ_x|[16],
+// 1 KiB, chunk-major), and per group kAuxGroupF4 float4 of bound terms (352 B): s_g[16] (COSINE: each row's
+// quick-test factor s_g / √|x|² instead), (s_g|q_x|)[16], |δ_x|[16],
 // |x|²[16] (struct of arrays: a lane reads its 4 rows' terms in one ds_read_b128), {max s|q|, max |δ|, max |x|²,
 // min |x|²}, {s_g, f_cos, zero-row flag, 0} (the quick test's per-group factor) and (COSINE) the rows' device-order
 // |x|² (xnorm; zeros without).  Rows past the last: zero codes and terms, not in the extrema.  The kernel stages

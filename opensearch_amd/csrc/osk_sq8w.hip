@@ -52,7 +52,8 @@ int sq8_wide_supported(int u8) { return u8 >= 1 && u8 <= 48 ? 1 : 0; }
 // q = clamp(rint(x / s_g), ±127) written in the MFMA-tiled layout (lane l of slab j: row l & 15, 16-B unit
 // 4j + (l >> 4) — the lane-linear A operand), and the group's bound terms in the tiled struct-of-arrays layout
 // of kAuxGroupF4 float4 (osk_internal.h): per row {s_g, s_g·|q| ↑, |x − s_g·q| ↑, |x|²} (sq8_quantize's terms,
-// computed in double, ↑ = rounded up), {max s|q|, max |δ|, max |x|², min |x|²}, {s_g, f_cos, zero-row flag, 0}
+// computed in double, ↑ = rounded up; COSINE stores each row's per-row quick-test factor s_g / √|x|² in place of
+// s_g, which the kernel reads from the next-but-one slot), {max s|q|, max |δ|, max |x|², min |x|²}, {s_g, f_cos, zero-row flag, 0}
 // and (COSINE) the rows' device-order |x|².  f_cos ≥ s_g / √|x|² of every row (rounded up, + 2^-20): the
 // COSINE quick test's per-group factor; a group with a zero row (COSINE) sets the flag instead (its pairs
 // always take the per-row test).  Rows past the last: zero codes and terms, not in the extrema.
@@ -119,7 +120,9 @@ __global__ __launch_bounds__(kBlock) void sq8w_build(const float4* __restrict__ 
         }
         float* af = reinterpret_cast<float*>(auxt + g * kAuxGroupF4);
         if (c == 0) {
-            af[r] = valid ? sg : 0.0f;
+            // COSINE keeps each row's quick-test factor s_g / √|x|² here instead of s_g (which every valid row
+            // shares: slot 17 holds it); round to nearest from double (a zero row: +∞, its pairs pass)
+            af[r] = !valid ? 0.0f : !cosine ? sg : W > 0.0f ? (float)((double)sg / sqrt((double)W)) : __builtin_inff();
             af[16 + r] = A;
             af[32 + r] = B;
             af[48 + r] = W;
@@ -509,7 +512,14 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
 
     // the full bound terms {a, y, z, w} of the lane's 4 rows (4·grp + r) of a group (pilot and insertions)
     auto row_terms = [&](const char* ga, float4 (&ax)[4]) {
-        const float4 A = *reinterpret_cast<const float4*>(ga + grp * 16);
+        // (COSINE: slot 0 holds the rows' quick-test factors; the scale s_g is the group's, in slot 17)
+        float4 A;
+        if constexpr (SIM == SIM_COSINE) {
+            const float sg = *reinterpret_cast<const float*>(ga + 17 * 16);
+            A = make_float4(sg, sg, sg, sg);
+        } else {
+            A = *reinterpret_cast<const float4*>(ga + grp * 16);
+        }
         const float4 Y = *reinterpret_cast<const float4*>(ga + 64 + grp * 16);
         const float4 Z = *reinterpret_cast<const float4*>(ga + 128 + grp * 16);
         const float4 W = *reinterpret_cast<const float4*>(ga + 192 + grp * 16);
@@ -606,7 +616,8 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                 const int qi = wq0 + qw;
                 const float* af = reinterpret_cast<const float*>(d.at + (rowq >> 4) * kAuxGroupF4);
                 const int rr = rowq & 15;
-                const float4 ax = ok ? make_float4(af[rr], af[16 + rr], af[32 + rr], af[48 + rr]) : make_float4(0.f, 0.f, 0.f, 0.f);
+                const float a_r = SIM == SIM_COSINE ? af[68] : af[rr];   // (COSINE: the group's s_g, slot 17)
+                const float4 ax = ok ? make_float4(a_r, af[16 + rr], af[32 + rr], af[48 + rr]) : make_float4(0.f, 0.f, 0.f, 0.f);
                 float xnd = 0.0f, qndq = 0.0f;
                 if constexpr (SIM == SIM_COSINE) {
                     xnd = ok ? af[72 + rr] : 0.0f;
@@ -693,6 +704,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
             float tf[GPS][QB];
             bool zg[GPS];
             uint32_t pbits[GPS];   // EUCLIDEAN: bit qb·4 + r = row r of the group passed for query block qb
+            float sgs[GPS];        // DOT / MIP: the group's scale s_g (every valid row's per-row factor)
 #pragma unroll
             for (int g = 0; g < GPS; ++g) {
                 const char* ga = hslot + g * GB + KS * 1024;
@@ -713,6 +725,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                 } else {
                     const float4 gf = *reinterpret_cast<const float4*>(ga + 17 * 16);   // {s_g, f_cos, zero row, 0}
                     const float f = SIM == SIM_COSINE ? gf.y : gf.x;
+                    sgs[g] = gf.x;
                     if constexpr (SIM == SIM_COSINE) zg[g] = gf.z != 0.0f;   // (wave-uniform: one LDS word)
 #pragma unroll
                     for (int qb = 0; qb < QB; ++qb) {
@@ -750,16 +763,13 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                         ++n_events;
 #endif
                         const char* ga = hslot + g * GB + KS * 1024;
-                        float arg[4] = {0.0f, 0.0f, 0.0f, 0.0f}, wrg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-                        if constexpr (SIM != SIM_EUCLIDEAN) {
-                            const float4 Ag = *reinterpret_cast<const float4*>(ga + grp * 16);
-                            const float4 Wg = *reinterpret_cast<const float4*>(ga + 192 + grp * 16);
-                            arg[0] = Ag.x, arg[1] = Ag.y, arg[2] = Ag.z, arg[3] = Ag.w;
-                            wrg[0] = Wg.x, wrg[1] = Wg.y, wrg[2] = Wg.z, wrg[3] = Wg.w;
-                        }
+                        // the per-row factors: DOT / MIP the group's s_g (no LDS read), COSINE each row's
+                        // s_g / √|x|² (slot 0; a zero row's +∞ makes its pairs pass)
+                        float arg[4] = {sgs[g], sgs[g], sgs[g], sgs[g]};
+                        const float wrg[4] = {0.0f, 0.0f, 0.0f, 0.0f};   // (EUCLIDEAN only)
                         if constexpr (SIM == SIM_COSINE) {
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) arg[r] = arg[r] * __builtin_amdgcn_rsqf(wrg[r]);   // (0 · ∞ = NaN: passes)
+                            const float4 Ag = *reinterpret_cast<const float4*>(ga + grp * 16);
+                            arg[0] = Ag.x, arg[1] = Ag.y, arg[2] = Ag.z, arg[3] = Ag.w;
                         }
                         const int r0 = 16 * (GPS * hst + g);
                         const int nr = min(16, hd.nrows - r0);
