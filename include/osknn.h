@@ -232,6 +232,7 @@ int32_t osk_view_scan_time(osk_view* view, double* total_ms, int64_t* calls);
  *   "tile_slots_per_cu", "tile_max_rounds"  ...its resident workgroups per CU (4) and rounds cap (4)
  *   "tile_min_rows"   ...with at least this many rows per tile (default 1024; at view create)
  *   "tile_large_slots" views of >= CUs x this x tile_min_rows rows get CUs x this tiles (24; 0 = off)
+ *   "tile_large_slots_512" the same for views of >= 512-dim rows (12)
  *   "mfma_min_batch"  batches of at least this many float32 queries (and k ≤ 12) may take the bf16×3
  *                     MFMA path (default 96; 0 = never)...
  *   "sq8_cost_pct"    ...when its 256-query blocks cost no more than the int8 prefilter's launches for

@@ -298,6 +298,7 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         {"tile_slots_per_cu", &g_tuning.tile_slots_per_cu, 1, 64, false},
         {"tile_max_rounds", &g_tuning.tile_max_rounds, 1, 1024, false},
         {"tile_large_slots", &g_tuning.tile_large_slots, 0, 1024, false},
+        {"tile_large_slots_512", &g_tuning.tile_large_slots_512, 0, 1024, false},
         {"tile_min_rows", &g_tuning.tile_min_rows, 1, 1 << 24, false},
         {"mfma_min_batch", &g_tuning.mfma_min_batch, 0, 1 << 30, false},
         {"sq8_cost_pct", &g_tuning.sq8_cost_pct, 0, 100000, false},
@@ -627,8 +628,14 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
         // of a tail round.  cus × tile_large_slots tiles (24 = 2 · lcm(3, 4)) are 6 full sq8_scan rounds
         // and 8 full sq8_mfma rounds (profiles/r01l/tiles_ab.txt: C3 b32 2.72 -> 2.47 ms, C4 b32
         // 7.2 -> 6.5 ms, C3 b1 within 1%).
-        const int64_t large = (int64_t)cus * g_tuning.tile_large_slots;
-        if (g_tuning.tile_large_slots > 0 && total >= large * min_rows) target = large;
+        // Rows of ≥ 512 dims (the 6-bit tier's views, C3/C5i-shaped) take half as many (12 = lcm(3, 4): 3 full
+        // sq8_scan rounds, 4 sq8_mfma rounds): their tiles are heavy enough that fewer, fuller workgroups win —
+        // the 6-bit tier's pilot, re-bound and settle run over fewer lists (C3 b1 +2.0 % at 4 in flight and one
+        // in flight, 3 interleaved A/B pairs, profiles/r05m/), C3 b32 and C5i gained too; C4 b32 (96 dims)
+        // lost 9 % with 12 (profiles/r05j/), so lighter rows keep tile_large_slots.
+        const int slots_large = v->dim >= 512 ? (int)g_tuning.tile_large_slots_512 : (int)g_tuning.tile_large_slots;
+        const int64_t large = (int64_t)cus * slots_large;
+        if (slots_large > 0 && total >= large * min_rows) target = large;
         // views smaller than one round at tile_min_rows (C1: 100k rows): latency-bound, so spread them
         // over more of the chip with tiles down to 8 row groups per wave (≥ 256 rows): C1's scan
         // 34 -> 16 µs (profiles/r02o/tile_min_rows.txt); a full round is unaffected (C2: 1024 tiles)

@@ -423,6 +423,7 @@ struct Tuning {
                               // resident slots (osk_view_create)
     std::atomic<int> tile_slots_per_cu{4};    // resident scan workgroups per CU (4 waves/SIMD, 256-thread groups)
     std::atomic<int> tile_large_slots{24};    // views of ≥ CUs × this × tile_min_rows rows: CUs × this tiles (0 = off)
+    std::atomic<int> tile_large_slots_512{12};   // …the same for views of ≥ 512-dim rows
     std::atomic<int> tile_max_rounds{4};      // at most this many rounds (10M rows: 4096 tiles, profiles/r01e)
     std::atomic<int> tile_min_rows{1024}; // ...and at least this many rows per tile (1.25M rows: 1024 tiles of 1221
                               // rows, 4360 QPS vs 3968 for 4096 tiles of 305 rows — profiles/r01e/tiles_ab.txt)

@@ -484,3 +484,39 @@ def test_rebound_schedules_agree_with_the_oracle(layout):
     finally:
         _lib.tune("sq6_probe_pct", 10)
         close_all(ds, readers)
+
+
+def test_scan_profile_samples_every_nth_call():
+    """osk_view_profile(view, N) stamps the scan launches of every N-th device search (bench.py's
+    --profile-every): N = 3 over 9 calls gives 3 sampled calls, N = 1 every call, N = 0 none; N < 0 is refused."""
+    import torch
+    sim = COS
+    rows = corpus(6000, 768, sim, 510)
+    queries = torch.from_numpy(corpus(9, 768, sim, 511)).cuda()
+    ds, readers = view_of([rows], sim)
+    L = _lib.lib()
+    try:
+        view = ds._h
+        keys = torch.empty((1, 1, 10), dtype=torch.int64, device="cuda")
+        counts = torch.empty((1, 1), dtype=torch.int32, device="cuda")
+        st = torch.cuda.Stream()
+
+        def run(n):
+            _lib.check(L.osk_view_profile(view, n))
+            for i in range(9):
+                _lib.check(L.osk_view_search_device(view, queries[i].data_ptr(), 1, 10, None, keys.data_ptr(),
+                                                    counts.data_ptr(), None, st.cuda_stream))
+            st.synchronize()
+            ms, calls = C.c_double(), C.c_int64()
+            _lib.check(L.osk_view_scan_time(view, C.byref(ms), C.byref(calls)))
+            return ms.value, calls.value
+
+        ms3, c3 = run(3)
+        assert c3 == 3 and ms3 > 0.0
+        ms1, c1 = run(1)
+        assert c1 == 9 and ms1 > 0.0
+        assert run(0) == (0.0, 0)
+        assert L.osk_view_profile(view, -1) != 0
+    finally:
+        _lib.check(L.osk_view_profile(ds._h, 0))
+        close_all(ds, readers)
