@@ -87,7 +87,7 @@ def pmc_traffic(rows_local: int, batch: int, prefilter: bool, six: bool = False)
 
 READ_CEILING = os.path.join(ROOT, "profiles", "r02j", "hbm_read_ceiling.json")
 # the 6-bit tier's pass (tools/gpu_run.sh pmc: FETCH_SIZE / WRITE_SIZE of this bench at N = 1, round 4)
-PMC_SUMMARY_SQ6 = os.path.join(ROOT, "profiles", "r05l", "pmc", "pmc_traffic.json")
+PMC_SUMMARY_SQ6 = os.path.join(ROOT, "profiles", "r05o", "pmc", "pmc_traffic.json")
 
 
 def read_ceiling():
