@@ -429,7 +429,7 @@ def main():
         bytes_per_launch = rows_local * (((DIM + 255) // 256) * 192 + 16)
         kernel_name = ("sq6_scan<C=3,U=3> the 6-bit pass of the certified prefilter (bytes = 6-bit codes + 16-B "
                        "bound terms per row, one query per launch; its pilot and int8 re-bound kernels read "
-                       "≈ 2 % more: sq6_pilot 0.041 GB, sq6_rebound ≈ 0.07 GB after its final-floor re-test)")
+                       "≈ 1 % more: sq6_pilot 0.021 GB, sq6_rebound 0.047 GB after its final-floor re-test, profiles/r05o/pmc/)")
     elif prefilter:
         passes = (B + 7) // 8
         bytes_per_launch = rows_local * (u8 * 16 + 16) * passes
