@@ -473,19 +473,31 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
     };
     int iq = 0, ist = 0;   // the next step to issue: quarter iq of mine, its step ist
     while (iq < n_mine && steps_of(iq) == 0) ++iq;
-    // this wave's part of the step → slot; groups past the quarter load its first group (valid, skipped)
     auto rfl_ptr = [](const void* ptr) {
         const uint64_t v = (uint64_t)ptr;
         return (const char*)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
                              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v));
     };
-    auto issue = [&](int slot) {
-        // the quarter's descriptor in SGPRs first (each DMA's asm clobbers memory: re-reading it from LDS
-        // between DMAs would put an LDS wait before each)
+    // the issuing quarter's descriptor, held in SGPRs while its steps are issued: a step reads no descriptor
+    // from LDS (each such read is a round trip queued behind the other waves' fragment reads, and the DMAs'
+    // asm clobbers memory, so it would be re-read between them)
+    int i_nrows = 0, i_steps = 0;
+    const int4* i_xt = nullptr;
+    const float4* i_at = nullptr;
+    auto load_iq = [&]() {
+        if (iq >= n_mine) return;
         const WideQuarter& d = s_quart[iq];
-        const int nrows = __builtin_amdgcn_readfirstlane(d.nrows);
-        const int4* xt = reinterpret_cast<const int4*>(rfl_ptr(d.xt));
-        const float4* at = reinterpret_cast<const float4*>(rfl_ptr(d.at));
+        i_nrows = __builtin_amdgcn_readfirstlane(d.nrows);
+        i_steps = __builtin_amdgcn_readfirstlane((i_nrows + 16 * GPS - 1) / (16 * GPS));
+        i_xt = reinterpret_cast<const int4*>(rfl_ptr(d.xt));
+        i_at = reinterpret_cast<const float4*>(rfl_ptr(d.at));
+    };
+    load_iq();
+    // this wave's part of the step → slot; groups past the quarter load its first group (valid, skipped)
+    auto issue = [&](int slot) {
+        const int nrows = i_nrows;
+        const int4* xt = i_xt;
+        const float4* at = i_at;
         const uint32_t base = ring_lds + (uint32_t)(slot * SLOT);
         if (dma_rows) {
 #pragma unroll
@@ -504,9 +516,10 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                 glds16(at + gv * kAuxGroupF4 + lane, base + (uint32_t)(g * GB + KS * 1024));
             }
         }
-        if (++ist == steps_of(iq)) {
+        if (++ist == i_steps) {
             ist = 0;
             do ++iq; while (iq < n_mine && steps_of(iq) == 0);
+            load_iq();
         }
     };
 
@@ -597,6 +610,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
         for (int st = 0; st < NS - 1 && st < total; ++st) issue(st);
         int s_issue = (NS - 1) % NS, s_read = 0;
         int pq = -1, pst = 0;   // the quarter of mine and its step the current step belongs to
+        int p_nrows = 0, p_steps = 0;   // (its rows and steps, in SGPRs: see load_iq)
         const char* hslot = smem;
         int hst = 0, hgroups = 0, hq = 0;
         i32x4 acc[GPS][QB];
@@ -978,7 +992,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                 s_issue = s_issue + 1 == NS ? 0 : s_issue + 1;
             }
             if (ablate & 64) continue;   // (A/B: the ring alone)
-            if (pq < 0 || ++pst == steps_of(pq)) {   // a new quarter: flush the last one, take its floors
+            if (pq < 0 || ++pst == p_steps) {   // a new quarter: flush the last one, take its floors
                 if (pq >= 0 && !pilot) {
 #ifdef OSK_TESTING
                     const uint64_t c_dr0 = clock64();
@@ -991,6 +1005,8 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                 }
                 do ++pq; while (steps_of(pq) == 0);
                 pst = 0;
+                p_nrows = __builtin_amdgcn_readfirstlane(s_quart[pq].nrows);
+                p_steps = __builtin_amdgcn_readfirstlane((p_nrows + 16 * GPS - 1) / (16 * GPS));
                 const int sh = s_quart[pq].shard;
 #pragma unroll
                 for (int qb = 0; qb < QB; ++qb) {
@@ -1011,7 +1027,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
             s_read = s_read + 1 == NS ? 0 : s_read + 1;
             hq = pq;
             hst = pst;
-            hgroups = __builtin_amdgcn_readfirstlane(min(GPS, ((s_quart[pq].nrows + 15) >> 4) - GPS * pst));   // (< GPS: the quarter's last step)
+            hgroups = __builtin_amdgcn_readfirstlane(min(GPS, ((p_nrows + 15) >> 4) - GPS * pst));   // (< GPS: the quarter's last step)
             if (pilot) {   // the quarter's first rows: per query the best lower-bound key → pilot_keys
                 const WideQuarter& hd = s_quart[hq];
                 if (pst == 0) {
@@ -1052,7 +1068,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                         pbest[qb] = best > pbest[qb] ? best : pbest[qb];
                     }
                 }
-                if (pst + 1 < steps_of(pq)) continue;   // (the quarter's last pilot step writes its keys)
+                if (pst + 1 < p_steps) continue;   // (the quarter's last pilot step writes its keys)
 #pragma unroll
                 for (int qb = 0; qb < QB; ++qb) {
                     const int qi = wq0 + qb * 16 + col;
