@@ -786,7 +786,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                             arg[0] = Ag.x, arg[1] = Ag.y, arg[2] = Ag.z, arg[3] = Ag.w;
                         }
                         const int r0 = 16 * (GPS * hst + g);
-                        const int nr = min(16, hd.nrows - r0);
+                        const int nr = min(16, p_nrows - r0);
                         bool pass[4];
                         if constexpr (SIM == SIM_EUCLIDEAN) {   // the fast test was the per-row test: its bits
 #pragma unroll
@@ -858,7 +858,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                     for (int r = 0; r < 4; ++r) arg[r] = arg[r] * __builtin_amdgcn_rsqf(wrg[r]);   // (0 · ∞ = NaN: passes)
                 }
                 const int r0 = 16 * (GPS * hst + g);   // rows of the quarter
-                const int nr = min(16, hd.nrows - r0);
+                const int nr = min(16, p_nrows - r0);
                 float4 ax[4];
                 row_terms(ga, ax);
 #pragma unroll
@@ -1038,7 +1038,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                 for (int g = 0; g < hgroups; ++g) {
                     const char* gb = hslot + g * GB;
                     const char* ga = gb + KS * 1024;
-                    const int r0 = 16 * (GPS * hst + g), nr = min(16, hd.nrows - r0);
+                    const int r0 = 16 * (GPS * hst + g), nr = min(16, p_nrows - r0);
                     i32x4 pacc[QB];
                     group_dots(gb, pacc);
                     float4 ax[4];
