@@ -135,6 +135,40 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_byte) {
                  : "v"(gsrc), "s"(lds_byte)
                  : "memory");
 }
+// N such DMAs in one statement (M0 saved once): the k-th from gbase + voff + k·GS (GS·(N−1) ≤ 4095: the
+// instruction's immediate offset; gbase wave-uniform, in SGPRs) into LDS at lds[k].  The immediate offset
+// moves the LDS destination too (M0 + offset + lane·16: tools/glds_offset_probe.hip), so M0 = lds[k] − k·GS.
+template <int N, int GS>
+__device__ __forceinline__ void glds16_run(const void* gbase, uint32_t voff, const uint32_t (&ldsk)[N]) {
+    static_assert((N == 1 || N == 2 || N == 4) && GS * (N - 1) <= 4095, "glds16_run: 1, 2 or 4 DMAs");
+    uint32_t lds[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) lds[k] = ldsk[k] - (uint32_t)(k * GS);
+    const uint64_t sb = (uint64_t)gbase;
+    unsigned keep;
+    if constexpr (N == 1) {
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 offset:0 nt\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(voff), "s"(sb), "s"(lds[0])
+                     : "memory");
+    } else if constexpr (N == 2) {
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 offset:0 nt\n\t"
+                     "s_mov_b32 m0, %4\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 offset:%5 nt\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(voff), "s"(sb), "s"(lds[0]), "s"(lds[1]), "n"(GS)
+                     : "memory");
+    } else {
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 offset:0 nt\n\t"
+                     "s_mov_b32 m0, %4\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 offset:%7 nt\n\t"
+                     "s_mov_b32 m0, %5\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 offset:%8 nt\n\t"
+                     "s_mov_b32 m0, %6\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 offset:%9 nt\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(voff), "s"(sb), "s"(lds[0]), "s"(lds[1]), "s"(lds[2]), "s"(lds[3]), "n"(GS), "n"(2 * GS),
+                       "n"(3 * GS)
+                     : "memory");
+    }
+}
 template <int N>
 __device__ __forceinline__ void vm_wait() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");

@@ -499,7 +499,28 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
         const int4* xt = i_xt;
         const float4* at = i_at;
         const uint32_t base = ring_lds + (uint32_t)(slot * SLOT);
-        if (dma_rows) {
+        // a step inside the quarter (every step but possibly its last): one DMA statement per wave over
+        // contiguous memory — the row waves' LPW consecutive 1 KiB units u = LPW·wave + j, the term waves' APW
+        // consecutive groups — from one SGPR base with immediate offsets (no per-DMA address arithmetic)
+        if (LPW <= 4 && 16 * GPS * (ist + 1) <= nrows) {
+            if (dma_rows) {
+                const int u0 = LPW * wave;   // (KS ≥ 4: the units stay inside one group; KS = 2: 2 groups)
+                uint32_t l[LPW <= 4 ? LPW : 1];
+#pragma unroll
+                for (int j = 0; j < (LPW <= 4 ? LPW : 1); ++j) {
+                    const int u = u0 + j, g = u / KS, sl = u - g * KS;
+                    l[j] = base + (uint32_t)(g * GB + sl * 1024);
+                }
+                glds16_run<(LPW <= 4 ? LPW : 1), 1024>(reinterpret_cast<const char*>(xt) + ((size_t)(GPS * KS * ist + u0) << 10),
+                                                      (uint32_t)lane * 16u, l);
+            } else if (dma_aux && lane < AUXF4) {
+                const int g0 = APW * (wave - 4);
+                uint32_t l[APW];
+#pragma unroll
+                for (int h = 0; h < APW; ++h) l[h] = base + (uint32_t)((g0 + h) * GB + KS * 1024);
+                glds16_run<APW, kAuxGroupF4 * 16>(at + (size_t)(GPS * ist + g0) * kAuxGroupF4, (uint32_t)lane * 16u, l);
+            }
+        } else if (dma_rows) {
 #pragma unroll
             for (int j = 0; j < LPW; ++j) {
                 const int u = wave + 4 * j, g = u / KS, s = u - g * KS;   // (wave-uniform)
