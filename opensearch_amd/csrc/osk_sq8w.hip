@@ -502,17 +502,19 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
         // a step inside the quarter (every step but possibly its last): one DMA statement per wave over
         // contiguous memory — the row waves' LPW consecutive 1 KiB units u = LPW·wave + j, the term waves' APW
         // consecutive groups — from one SGPR base with immediate offsets (no per-DMA address arithmetic)
-        if (LPW <= 4 && 16 * GPS * (ist + 1) <= nrows) {
+        if ((LPW <= 4 || LPW == 6) && 16 * GPS * (ist + 1) <= nrows) {
             if (dma_rows) {
                 const int u0 = LPW * wave;   // (KS ≥ 4: the units stay inside one group; KS = 2: 2 groups)
-                uint32_t l[LPW <= 4 ? LPW : 1];
+                constexpr int N0 = LPW <= 4 ? LPW : 4, N1 = LPW - N0;   // (6 units: 4 + 2, the offset field is 12-bit)
+                uint32_t l0[N0], l1[N1 > 0 ? N1 : 1];
 #pragma unroll
-                for (int j = 0; j < (LPW <= 4 ? LPW : 1); ++j) {
+                for (int j = 0; j < LPW; ++j) {
                     const int u = u0 + j, g = u / KS, sl = u - g * KS;
-                    l[j] = base + (uint32_t)(g * GB + sl * 1024);
+                    (j < N0 ? l0[j] : l1[j - N0 < 0 ? 0 : j - N0]) = base + (uint32_t)(g * GB + sl * 1024);
                 }
-                glds16_run<(LPW <= 4 ? LPW : 1), 1024>(reinterpret_cast<const char*>(xt) + ((size_t)(GPS * KS * ist + u0) << 10),
-                                                      (uint32_t)lane * 16u, l);
+                const char* gb = reinterpret_cast<const char*>(xt) + ((size_t)(GPS * KS * ist + u0) << 10);
+                glds16_run<N0, 1024>(gb, (uint32_t)lane * 16u, l0);
+                if constexpr (N1 > 0) glds16_run<N1, 1024>(gb + N0 * 1024, (uint32_t)lane * 16u, l1);
             } else if (dma_aux && lane < AUXF4) {
                 const int g0 = APW * (wave - 4);
                 uint32_t l[APW];
