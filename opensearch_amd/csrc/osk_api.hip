@@ -1642,7 +1642,10 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             p.ablate = g_tuning.sq8_mfma_ablate;
             p.counters = v->d_counters.as<unsigned long long>();   // (testing build: event counts)
             p.pilot = 1;
-            p.pilot_rows = g_tuning.sq8_wide_pilot_rows;
+            // (0: 128 rows per quarter, 256 at ≥ 512 dims, where the pilot's steps are 32 rows and the better
+            // floors pay: C3 b256 3.76 → 3.71 ms, C4's 96 dims 22.98 → 23.27 ms, profiles/r05p/tune50_*)
+            const int prows = g_tuning.sq8_wide_pilot_rows.load();
+            p.pilot_rows = prows > 0 ? prows : (sq8_wide_ks(u8) >= 8 ? 256 : 0);
             p.wide_defer = g_tuning.sq8_wide_defer;
             p.pilot_keys = v->ws_pilot.as<uint64_t>();
             p.quarter_begin = 0;

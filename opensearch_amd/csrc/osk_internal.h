@@ -454,7 +454,7 @@ struct Tuning {
     std::atomic<int> sq8_wide_min{64};    // ...and unfiltered batches ≥ this on the wide kernel, kWideQ per launch, when
                                           // its cost model beats sq8_mfma's (0 = never)
     std::atomic<int> sq8_wide_grid{0};    // wide kernel's persistent workgroups (0 = one per CU)
-    std::atomic<int> sq8_wide_pilot_rows{0};   // wide pilot rows per quarter (0 = 128)
+    std::atomic<int> sq8_wide_pilot_rows{0};   // wide pilot rows per quarter (0 = 128, 256 at ≥ 512 dims)
     std::atomic<int> sq6_rebound_retest{1};   // sq6_rebound: the final-floor 6-bit re-test (0: gather every candidate)
     std::atomic<int> sq6_rebound_stride{1};   // sq6_rebound: strided list assignment (0: contiguous)
     std::atomic<int> sq6_rebound_wgs{0};      // sq6_rebound: workgroups per CU (0: as many as fit)
