@@ -305,6 +305,19 @@ struct WideQuarter {
     int32_t pad[3];
     float4 bm;            // the quarter's row maxima {max s|q|, max |δ|, max |x|², min |x|²} (launch_wide_quarter_max)
 };
+// The parameters only the cold paths use (quarter-end flushes and drains, list overflows, the pilot's key
+// stores), held in LDS: read from there they are not live across the step loop, whose hot values then keep
+// their SGPRs instead of spilling to VGPR lanes.
+struct WideCold {
+    uint64_t* cand;
+    uint32_t* cand_lb;
+    uint32_t* list_lbmax;
+    unsigned long long* visited;
+    const float* qn_dev;
+    uint64_t* pilot_keys;
+    int q0, n_lists, q_count;
+    float cos_slack;
+};
 constexpr int kWideMaxFloorShards = 16;   // per-(shard, query) floors held in LDS up to this many shards
 constexpr int kWideThreads = kWideWaves * 64;
 constexpr int kWideSorted = 1 << 20;      // s_cnt of a list the ordered insertion has sorted
@@ -358,6 +371,9 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
     const bool floor_lds = S <= kWideMaxFloorShards;
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ WideCold s_cold;
+    if (tid == 0) s_cold = WideCold{p.cand, p.cand_lb, p.list_lbmax, p.visited, p.qn_dev, p.pilot_keys, p.q0, p.n_lists,
+                                    p.q_count, p.cos_slack};
     uint64_t* s_lk = reinterpret_cast<uint64_t*>(smem + NS * SLOT);      // [kWideQ][kKQ] upper-bound keys
     uint32_t* s_lp = reinterpret_cast<uint32_t*>(s_lk + kWideQ * kKQ);   // their lower bounds
     float4* s_qc = reinterpret_cast<float4*>(s_lp + kWideQ * kKQ);        // [kWideQ] query bound terms
@@ -589,7 +605,8 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
     float ca[QB], cb[QB];   // the current quarter's quick-test constants
     // a quarter ends: its lists (this wave's queries, 4 per pass of 16 lanes) → the settle's arrays, zeroed
     auto flush = [&](const WideQuarter& d) {
-        const int q_end = min(wq0 + 16 * QB, p.q_count);
+        const WideCold& c = s_cold;
+        const int q_end = min(wq0 + 16 * QB, c.q_count);
         for (int q0 = wq0; q0 < q_end; q0 += 4) {
             const int qg = q0 + (lane >> 4), e = lane & 15;
             const uint64_t lkb = s_lk[qg * kKQ + e];
@@ -598,17 +615,17 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
 #pragma unroll
             for (int o = 8; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
             if (qg < q_end && !(ablate & 16)) {
-                const size_t l = (size_t)(p.q0 + qg) * p.n_lists + d.list;
-                p.cand[l * kKQ + e] = lkb;
-                p.cand_lb[l * kKQ + e] = lpb;
-                if (e == 0) p.list_lbmax[l] = m;
+                const size_t l = (size_t)(c.q0 + qg) * c.n_lists + d.list;
+                c.cand[l * kKQ + e] = lkb;
+                c.cand_lb[l * kKQ + e] = lpb;
+                if (e == 0) c.list_lbmax[l] = m;
                 s_lk[qg * kKQ + e] = 0ull;
                 s_lp[qg * kKQ + e] = 0u;
                 if (e == 0) s_cnt[qg] = 0;
             }
         }
-        if (p.visited && p.q0 == 0 && tid == 0 && d.nrows > 0)
-            atomicAdd(&p.visited[d.seg], (unsigned long long)d.nrows);
+        if (c.visited && c.q0 == 0 && tid == 0 && d.nrows > 0)
+            atomicAdd(&c.visited[d.seg], (unsigned long long)d.nrows);
     };
 
     // empty quarters (tiles of a few rows) take no step, but the settle and the pilot merge read every
@@ -658,7 +675,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                 float xnd = 0.0f, qndq = 0.0f;
                 if constexpr (SIM == SIM_COSINE) {
                     xnd = ok ? af[72 + rr] : 0.0f;
-                    qndq = ok ? p.qn_dev[qi] : 0.0f;
+                    qndq = ok ? s_cold.qn_dev[qi] : 0.0f;
                 }
                 uint64_t key = 0ull;
                 uint32_t lbs = 0u;
@@ -717,7 +734,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
 #pragma unroll
                         for (int qb = 0; qb < QB; ++qb)
                             if (qb == (Q >> 4)) {
-                                tq[qb] = sq8_quick(sim, thrb > tkey[qb] ? thrb : tkey[qb], sqrtf(qnd[qb]), p.cos_slack);
+                                tq[qb] = sq8_quick(sim, thrb > tkey[qb] ? thrb : tkey[qb], sqrtf(qnd[qb]), s_cold.cos_slack);
                                 quick_consts<SIM>(tq[qb], sb[qb], inv[qb], QY[qb], QZ[qb], Q0[qb], QW, zq[qb], ig2m, bm,
                                                   ca[qb], cb[qb]);
                             }
@@ -964,7 +981,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                         }
                         if (lane == 0) s_cnt[qo_g] = kWideSorted;   // sorted: later rows all take this path
                         if (col == bc && thrb) {   // full: its 16th key joins the floor under the threshold
-                            tq[qb] = sq8_quick(sim, thrb > tkey[qb] ? thrb : tkey[qb], sqrtf(qnd[qb]), p.cos_slack);
+                            tq[qb] = sq8_quick(sim, thrb > tkey[qb] ? thrb : tkey[qb], sqrtf(qnd[qb]), s_cold.cos_slack);
                             quick_consts<SIM>(tq[qb], sb[qb], inv[qb], QY[qb], QZ[qb], Q0[qb], QW, zq[qb], ig2m, bm,
                                               ca[qb], cb[qb]);
                         }
@@ -1036,7 +1053,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                     const int qi = wq0 + qb * 16 + col;
                     const uint32_t f = floor_lds ? s_floor[sh * kWideQ + qi] : floor_of(qi, sh);
                     tkey[qb] = (uint64_t)f << 32;
-                    tq[qb] = sq8_quick(sim, tkey[qb], sqrtf(qnd[qb]), p.cos_slack);
+                    tq[qb] = sq8_quick(sim, tkey[qb], sqrtf(qnd[qb]), s_cold.cos_slack);
                 }
                 // the quarter's row maxima → its quick-test constants (the quick test relaxes each pair's
                 // error terms to the maxima of the rows it is taken over: here the quarter's)
@@ -1095,10 +1112,11 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
 #pragma unroll
                 for (int qb = 0; qb < QB; ++qb) {
                     const int qi = wq0 + qb * 16 + col;
-                    if (grp == 0 && qi < p.q_count && !(ablate & 16))
-                        p.pilot_keys[(size_t)qi * n_quarters + hd.list] = pbest[qb];
+                    if (grp == 0 && qi < s_cold.q_count && !(ablate & 16))
+                        s_cold.pilot_keys[(size_t)qi * n_quarters + hd.list] = pbest[qb];
                     // the two-pass main pass reads the second pass's list maxima as empty until it writes them
-                    if (grp == 0 && qi < p.q_count) p.list_lbmax[(size_t)(p.q0 + qi) * p.n_lists + hd.list] = 0u;
+                    if (grp == 0 && qi < s_cold.q_count)
+                        s_cold.list_lbmax[(size_t)(s_cold.q0 + qi) * s_cold.n_lists + hd.list] = 0u;
                 }
                 continue;
             }
@@ -1168,7 +1186,8 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
 using WideFn = void (*)(Sq8Params);
 #define OSK_WIDE_SIMS(KS) {sq8_wide<KS, 0>, sq8_wide<KS, 1>, sq8_wide<KS, 2>, sq8_wide<KS, 3>}
 static const WideFn kWide[4][4] = {OSK_WIDE_SIMS(2), OSK_WIDE_SIMS(4), OSK_WIDE_SIMS(8), OSK_WIDE_SIMS(12)};
-static constexpr size_t kLdsCap = 160 * 1024;
+static constexpr size_t kLdsCap = 160 * 1024 - 128;   // (the kernel's static LDS: WideCold)
+static_assert(sizeof(WideCold) <= 128, "WideCold: 128 B of static LDS reserved");
 
 template <int KS>
 static size_t wide_ring_bytes(int sim) {
