@@ -315,8 +315,8 @@ struct WideCold {
     unsigned long long* visited;
     const float* qn_dev;
     uint64_t* pilot_keys;
-    int q0, n_lists, q_count;
-    float cos_slack;
+    int q0, n_lists, q_count, n_quarters;
+    float cos_slack, gam, g2;
 };
 constexpr int kWideMaxFloorShards = 16;   // per-(shard, query) floors held in LDS up to this many shards
 constexpr int kWideThreads = kWideWaves * 64;
@@ -373,7 +373,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ WideCold s_cold;
     if (tid == 0) s_cold = WideCold{p.cand, p.cand_lb, p.list_lbmax, p.visited, p.qn_dev, p.pilot_keys, p.q0, p.n_lists,
-                                    p.q_count, p.cos_slack};
+                                    p.q_count, 4 * p.n_tiles, p.cos_slack, p.gam, p.g2};
     uint64_t* s_lk = reinterpret_cast<uint64_t*>(smem + NS * SLOT);      // [kWideQ][kKQ] upper-bound keys
     uint32_t* s_lp = reinterpret_cast<uint32_t*>(s_lk + kWideQ * kKQ);   // their lower bounds
     float4* s_qc = reinterpret_cast<float4*>(s_lp + kWideQ * kKQ);        // [kWideQ] query bound terms
@@ -683,7 +683,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                 if (ok) {
                     const float4 qcb = s_qc[qi];
                     float lo, hi;
-                    sq8_bounds(sim, (float)(int32_t)en.x, ax, qcb, p.gam, p.g2, lo, hi);
+                    sq8_bounds(sim, (float)(int32_t)en.x, ax, qcb, s_cold.gam, s_cold.g2, lo, hi);
                     const float ub = SIM == SIM_EUCLIDEAN ? score_f32_l2(lo) : score_f32(sim, hi, qndq, xnd);
                     const float lb = SIM == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qndq, xnd);
                     const uint64_t kr = make_key(ub, d.vrow0 + (uint32_t)rowq);
@@ -928,7 +928,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                             float xnd = 0.0f;
                             if constexpr (SIM == SIM_COSINE) xnd = *reinterpret_cast<const float*>(ga + 288 + rr * 4);
                             float lo, hi;
-                            sq8_bounds(sim, (float)ac[qb][r], ax[r], qcb, p.gam, p.g2, lo, hi);
+                            sq8_bounds(sim, (float)ac[qb][r], ax[r], qcb, s_cold.gam, s_cold.g2, lo, hi);
                             const float ub = SIM == SIM_EUCLIDEAN ? score_f32_l2(lo) : score_f32(sim, hi, qnd[qb], xnd);
                             const float lb = SIM == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qnd[qb], xnd);
                             const uint64_t kr = make_key(ub, hd.vrow0 + (uint32_t)(r0 + rr));
@@ -1094,7 +1094,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                             float xnd = 0.0f;
                             if constexpr (SIM == SIM_COSINE) xnd = *reinterpret_cast<const float*>(ga + 288 + rr * 4);
                             float lo, hi;
-                            sq8_bounds(sim, (float)pacc[qb][r], ax[r], qc, p.gam, p.g2, lo, hi);
+                            sq8_bounds(sim, (float)pacc[qb][r], ax[r], qc, s_cold.gam, s_cold.g2, lo, hi);
                             const float lb = SIM == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qnd[qb], xnd);
                             const uint64_t key = rr < nr ? make_key(lb, hd.vrow0 + (uint32_t)(r0 + rr)) : 0ull;
                             best = key > best ? key : best;
@@ -1113,7 +1113,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                 for (int qb = 0; qb < QB; ++qb) {
                     const int qi = wq0 + qb * 16 + col;
                     if (grp == 0 && qi < s_cold.q_count && !(ablate & 16))
-                        s_cold.pilot_keys[(size_t)qi * n_quarters + hd.list] = pbest[qb];
+                        s_cold.pilot_keys[(size_t)qi * s_cold.n_quarters + hd.list] = pbest[qb];
                     // the two-pass main pass reads the second pass's list maxima as empty until it writes them
                     if (grp == 0 && qi < s_cold.q_count)
                         s_cold.list_lbmax[(size_t)(s_cold.q0 + qi) * s_cold.n_lists + hd.list] = 0u;
