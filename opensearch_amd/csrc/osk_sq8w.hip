@@ -315,6 +315,7 @@ struct WideCold {
     unsigned long long* visited;
     const float* qn_dev;
     uint64_t* pilot_keys;
+    const uint32_t* floors;
     int q0, n_lists, q_count, n_quarters;
     float cos_slack, gam, g2;
 };
@@ -372,8 +373,8 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ WideCold s_cold;
-    if (tid == 0) s_cold = WideCold{p.cand, p.cand_lb, p.list_lbmax, p.visited, p.qn_dev, p.pilot_keys, p.q0, p.n_lists,
-                                    p.q_count, 4 * p.n_tiles, p.cos_slack, p.gam, p.g2};
+    if (tid == 0) s_cold = WideCold{p.cand, p.cand_lb, p.list_lbmax, p.visited, p.qn_dev, p.pilot_keys, p.floors, p.q0,
+                                    p.n_lists, p.q_count, 4 * p.n_tiles, p.cos_slack, p.gam, p.g2};
     uint64_t* s_lk = reinterpret_cast<uint64_t*>(smem + NS * SLOT);      // [kWideQ][kKQ] upper-bound keys
     uint32_t* s_lp = reinterpret_cast<uint32_t*>(s_lk + kWideQ * kKQ);   // their lower bounds
     float4* s_qc = reinterpret_cast<float4*>(s_lp + kWideQ * kKQ);        // [kWideQ] query bound terms
@@ -394,6 +395,10 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
     // the floor T of (query, shard) (launch_wide_floor; its score's sortable bits, 0 = none)
     auto floor_of = [&](int qi, int sh) -> uint32_t {
         return (pilot || !p.floors || qi >= p.q_count) ? 0u : p.floors[(size_t)qi * S + sh];
+    };
+    auto floor_of_cold = [&](int qi, int sh) -> uint32_t {   // (the same, in the step loop: from WideCold)
+        const WideCold& c = s_cold;
+        return (pilot || !c.floors || qi >= c.q_count) ? 0u : c.floors[(size_t)qi * S + sh];
     };
     if (floor_lds)
         for (int i = tid; i < S * kWideQ; i += kWideThreads) s_floor[i] = floor_of(i % kWideQ, i / kWideQ);
@@ -687,7 +692,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                     const float ub = SIM == SIM_EUCLIDEAN ? score_f32_l2(lo) : score_f32(sim, hi, qndq, xnd);
                     const float lb = SIM == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qndq, xnd);
                     const uint64_t kr = make_key(ub, d.vrow0 + (uint32_t)rowq);
-                    const uint64_t tk = (uint64_t)(floor_lds ? s_floor[sh * kWideQ + qi] : floor_of(qi, sh)) << 32;
+                    const uint64_t tk = (uint64_t)(floor_lds ? s_floor[sh * kWideQ + qi] : floor_of_cold(qi, sh)) << 32;
                     if (kr > tk) {   // below the floor: cannot enter the top k
 #ifdef OSK_TESTING
                         ++n_pairs;
@@ -1051,7 +1056,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
 #pragma unroll
                 for (int qb = 0; qb < QB; ++qb) {
                     const int qi = wq0 + qb * 16 + col;
-                    const uint32_t f = floor_lds ? s_floor[sh * kWideQ + qi] : floor_of(qi, sh);
+                    const uint32_t f = floor_lds ? s_floor[sh * kWideQ + qi] : floor_of_cold(qi, sh);
                     tkey[qb] = (uint64_t)f << 32;
                     tq[qb] = sq8_quick(sim, tkey[qb], sqrtf(qnd[qb]), s_cold.cos_slack);
                 }
