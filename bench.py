@@ -26,7 +26,7 @@ copy, sq6_scan streams 6-bit codes + 16-B bound terms and keeps the rows whose u
 sq6_rebound re-bounds them on the int8 copy, the settle re-scores the surviving candidates exactly in fp32);
 results are bit-identical to the fp32 streaming scan, which the bench re-runs on the same queries and
 compares.  Batches of 2…~160 take the int8 MFMA prefilter (sq8_mfma, 32 queries per corpus pass), larger ones
-the wide int8 prefilter (≤ 256 dims, 256 queries per pass) or the bf16×3 MFMA path, by the library's cost model.
+the wide int8 prefilter (≤ 768 dims, 256 queries per pass) or the bf16×3 MFMA path, by the library's cost model.
 roofline: the dominant kernel is HBM-bound; algorithmic bytes per launch = rows scanned × (576 + 16) B for
 sq6_scan (6-bit codes + 16-B bound terms, one query per launch; rows × (768 + 16) B for sq8_scan's int8 tier;
 rows × 768 × 4 B for the fp32 scan).  Its average duration is measured live from the kernel's own

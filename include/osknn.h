@@ -402,6 +402,10 @@ int32_t osk_comm_init_loopback(int32_t device, int32_t rank, int32_t world, cons
  * grouped all-gather is replaced by device copies, so devices may repeat — n local "devices" mapped to one
  * GPU run the multi-device code of osk_shards_search_merge on a one-GPU machine. */
 int32_t osk_comm_init_all_loopback(const int32_t* devices, int32_t n, osk_comm** out);
+/* Testing build only: runs the wide kernel's one-statement LDS-DMA helper (glds16_run, N = 1/2/4 DMAs at the
+ * slab and bound-term strides) into out-of-order LDS destinations and counts the 16-B LDS words that differ from
+ * the expected image (0 = every DMA landed exactly at its destination, nothing else written). */
+int32_t osk_testing_glds_probe(int32_t device, int64_t* out_mismatches);
 
 /* The whole multi-GPU query, host buffers, synchronous: every local view (views[i] on the
  * communicator's local device i) scans its shards, the per-shard top-k lists of every rank are
@@ -419,7 +423,12 @@ int32_t osk_shards_search_merge(osk_comm* comm, osk_view* const* views, int32_t 
  * number of list slots per rank (≥ the view's shards; slots past them are empty), outputs as
  * osk_merge_device.  shards_per_rank should be the same on every rank (the caller knows the shard
  * layout, e.g. the largest shard count of any rank); at world > 1 the all-gather moves the communicator's
- * fixed block (osk_comm_set_device_limits), so a rank that differs gets count −1, never a hang. */
+ * fixed block (osk_comm_set_device_limits), so a rank that differs gets count −1, never a hang.  A rank whose
+ * own arguments are wrong (more shards in the view than shards_per_rank, k outside [1, OSK_MAX_K], a bad
+ * from/size or batch) still issues that all-gather at world > 1, with a refusal header: every other rank's
+ * reduce reports count −1 (communicator poisoned), and this rank returns OSK_ERR_INVALID without writing its
+ * outputs.  Only null pointers and a view on another device return before the collective (a caller bug that
+ * no shape can describe).  At world 1 every argument error returns at once. */
 int32_t osk_shards_search_merge_device(osk_comm* comm, osk_view* view, const void* d_queries, int32_t n_queries,
                                        int32_t k, const uint64_t* const* d_accept, int32_t shards_per_rank,
                                        int32_t from, int32_t size, float* d_scores, int32_t* d_docs,

@@ -79,6 +79,7 @@ SIGNATURES = {
     "osk_comm_set_device_limits": (_I32, [_P, _I32, _I32, _I32]),
     "osk_comm_init_loopback": (_I32, [_I32, _I32, _I32, _P, _I64, C.POINTER(_P)]),
     "osk_comm_init_all_loopback": (_I32, [_P, _I32, C.POINTER(_P)]),
+    "osk_testing_glds_probe": (_I32, [_I32, _PI64]),
     "osk_shards_search_merge": (_I32, [_P, _P, _I32, _P, _I32, _I32, _P, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     "osk_shards_search_merge_device": (_I32, [_P, _P, _P, _I32, _I32, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P,
                                               _P]),

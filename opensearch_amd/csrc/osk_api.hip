@@ -207,10 +207,11 @@ void osk::seg_unref(osk_seg* s) {
 namespace {
 
 int32_t ensure_sq8_seg(osk_seg* s, hipStream_t st);
-int32_t ensure_sq8t_seg(osk_seg* s, hipStream_t st);
+int32_t ensure_sq8t_seg(osk_seg* s, hipStream_t st, bool wide);
 int32_t ensure_split(osk_seg* s, hipStream_t st);
 int32_t ensure_sq8(osk_view* v, hipStream_t st);
 int32_t ensure_sq8t(osk_view* v, hipStream_t st);
+int32_t ensure_sq8w(osk_view* v, hipStream_t st);
 int32_t ensure_mfma(osk_view* v, hipStream_t st);
 
 int32_t seg_finish(osk_seg* s, const int32_t* ord_to_doc, hipStream_t st) {
@@ -347,6 +348,55 @@ int32_t osk_tune_set(const char* key, int64_t value) {
     }
     set_error("unknown tuning key: " + k);
     return OSK_ERR_INVALID;
+    OSK_GUARD_END
+}
+
+int32_t osk_testing_glds_probe(int32_t device, int64_t* out_mismatches) {
+    OSK_GUARD_BEGIN
+    clear_error();
+#ifndef OSK_TESTING
+    (void)device; (void)out_mismatches;
+    set_error("osk_testing_glds_probe exists only in the testing build (libosknn_testing.so)");
+    return OSK_ERR_UNSUPPORTED;
+#else
+    OSK_REQUIRE(out_mismatches != nullptr, "out_mismatches is null");
+    int32_t rc = check_device(device);
+    if (rc) return rc;
+    constexpr int kSrc = 1024, kImg = 1024, kCases = 6;
+    std::vector<int4> h_src(kSrc), h_out((size_t)kCases * kImg);
+    for (int i = 0; i < kSrc; ++i) h_src[i] = make_int4(i, i ^ 0x5A5A, 3 * i + 1, 7);
+    int4 *d_src = nullptr, *d_out = nullptr;
+    OSK_HIP(hipMalloc(&d_src, kSrc * sizeof(int4)));
+    if (hipMalloc(&d_out, h_out.size() * sizeof(int4)) != hipSuccess) {
+        (void)hipFree(d_src);
+        set_error("hipMalloc failed");
+        return OSK_ERR_DEVICE;
+    }
+    hipError_t e = hipMemcpy(d_src, h_src.data(), kSrc * sizeof(int4), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_glds_probe(d_src, d_out, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(h_out.data(), d_out, h_out.size() * sizeof(int4), hipMemcpyDeviceToHost);
+    (void)hipFree(d_src);
+    (void)hipFree(d_out);
+    if (e != hipSuccess) {
+        set_error(std::string("glds probe: ") + hipGetErrorString(e));
+        return OSK_ERR_DEVICE;
+    }
+    // the expected image of each case: DMA k's 64 lanes at (N − 1 − k)·2048 + 512 + lane·16, all else −1
+    int64_t bad = 0;
+    const int ns[kCases] = {1, 2, 4, 1, 2, 4}, gs[kCases] = {1024, 1024, 1024, kAuxGroupF4 * 16, kAuxGroupF4 * 16,
+                                                             kAuxGroupF4 * 16};
+    for (int c = 0; c < kCases; ++c) {
+        std::vector<int4> want(kImg, make_int4(-1, -1, -1, -1));
+        for (int k = 0; k < ns[c]; ++k)
+            for (int l = 0; l < 64; ++l) want[((ns[c] - 1 - k) * 2048 + 512) / 16 + l] = h_src[(k * gs[c]) / 16 + l];
+        for (int i = 0; i < kImg; ++i) {
+            const int4 a = h_out[(size_t)c * kImg + i], b = want[i];
+            bad += a.x != b.x || a.y != b.y || a.z != b.z || a.w != b.w;
+        }
+    }
+    *out_mismatches = bad;
+    return OSK_OK;
+#endif
     OSK_GUARD_END
 }
 
@@ -547,7 +597,7 @@ int32_t osk_seg_warm(osk_seg* seg, int32_t what) {
         if (rc) return rc;
     }
     if ((what & OSK_WARM_PREFILTER_MFMA) && sq8_mfma_supported((seg->dim + 15) / 16)) {
-        rc = ensure_sq8t_seg(seg, st);
+        rc = ensure_sq8t_seg(seg, st, false);
         if (rc) return rc;
     }
     if (what & OSK_WARM_BATCHED) return ensure_split(seg, st);
@@ -1124,58 +1174,78 @@ int32_t ensure_sq8_seg(osk_seg* s, hipStream_t st) {
 // contiguous 1 KiB slab (chunk-major: 16-dim chunk c of row r at c·256 + r·16 B), so each of the scan's
 // load instructions reads 1 KiB contiguous and a 32-dim tail is the slab's first 512 B.  Built once, from
 // the row-major int8 copy.
-int32_t ensure_sq8t_seg(osk_seg* s, hipStream_t st) {
+int32_t ensure_sq8t_seg(osk_seg* s, hipStream_t st, bool wide) {
     std::lock_guard<std::mutex> lk(s->mu);
-    if (s->d_q8t) return OSK_OK;
     const int u8 = (s->dim + 15) / 16;
-    const int ks = sq8_mfma_ks(u8);
     const int64_t blocks = std::max<int64_t>(1, (s->n_rows + 15) / 16);
-    void* q8t = nullptr;
-    hipError_t e = hipMalloc(&q8t, (size_t)blocks * ks * 1024);
-    if (e != hipSuccess) {
-        set_error(std::string("hipMalloc of the tiled int8 copy failed: ") + hipGetErrorString(e));
-        return OSK_ERR_OOM;
+    if (!s->d_q8t) {
+        const int ks = sq8_mfma_ks(u8);
+        void* q8t = nullptr;
+        hipError_t e = hipMalloc(&q8t, (size_t)blocks * ks * 1024);
+        if (e != hipSuccess) {
+            set_error(std::string("hipMalloc of the tiled int8 copy failed: ") + hipGetErrorString(e));
+            return OSK_ERR_OOM;
+        }
+        OSK_HIP(launch_sq8_tile(s->d_q8, s->n_rows, u8, ks, q8t, st));
+        OSK_HIP(hipStreamSynchronize(st));
+        s->d_q8t = q8t;
     }
-    OSK_HIP(launch_sq8_tile(s->d_q8, s->n_rows, u8, ks, q8t, st));
     // the wide kernel's own copy (osk_sq8w.hip launch_sq8w_build): codes with one scale per 16-row group,
-    // tiled, and their bound terms per group (352 B per 16 rows)
-    void* q8w = nullptr;
-    float4* auxt = nullptr;
-    if (sq8_wide_supported(u8)) {
-        e = hipMalloc(&q8w, (size_t)blocks * sq8_wide_ks(u8) * 1024);
+    // tiled, and their bound terms per group (352 B per 16 rows).  Built the first time the cost model sends a
+    // batch of this segment's view to the wide kernel (a node whose batches never take it does not
+    // hold a second int8 copy — at 768 dims +768 B per row)
+    if (wide && !s->d_q8w && sq8_wide_supported(u8)) {
+        void* q8w = nullptr;
+        float4* auxt = nullptr;
+        hipError_t e = hipMalloc(&q8w, (size_t)blocks * sq8_wide_ks(u8) * 1024);
         if (e == hipSuccess) e = hipMalloc(&auxt, (size_t)blocks * kAuxGroupF4 * sizeof(float4));
         if (e != hipSuccess) {
             if (q8w) (void)hipFree(q8w);
-            (void)hipFree(q8t);
             set_error(std::string("hipMalloc of the wide prefilter copy failed: ") + hipGetErrorString(e));
             return OSK_ERR_OOM;
         }
         OSK_HIP(launch_sq8w_build(static_cast<const float4*>(s->d_rows), s->n_rows, s->units, u8,
                                   s->sim == SIM_COSINE ? s->d_xnorm_f : nullptr, s->sim == SIM_COSINE ? 1 : 0, q8w, auxt,
                                   st));
+        OSK_HIP(hipStreamSynchronize(st));
+        s->d_q8w = q8w;
+        s->d_q8auxt = auxt;
     }
-    OSK_HIP(hipStreamSynchronize(st));
-    s->d_q8t = q8t;
-    s->d_q8w = q8w;
-    s->d_q8auxt = auxt;
     return OSK_OK;
 }
 
 int32_t ensure_sq8t(osk_view* v, hipStream_t st) {
     if (v->sq8t_ready) return OSK_OK;
     const int ns = (int)v->segs.size();
-    std::vector<const void*> rows(ns), rows_w(ns), auxt(ns);
+    std::vector<const void*> rows(ns);
     for (int i = 0; i < ns; ++i) {
-        int32_t rc = ensure_sq8t_seg(v->segs[i], st);
+        int32_t rc = ensure_sq8t_seg(v->segs[i], st, false);
         if (rc) return rc;
         rows[i] = v->segs[i]->d_q8t;
+    }
+    OSK_HIP(v->d_sq8_rows_t.reserve(sizeof(void*) * ns));
+    OSK_HIP(hipMemcpyAsync(v->d_sq8_rows_t.p, rows.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
+    OSK_HIP(hipStreamSynchronize(st));
+    v->sq8t_ready = true;
+    return OSK_OK;
+}
+
+// The wide kernel's inputs for a view (first batch the cost model sends to it): every segment's group-scaled
+// copy and tiled bound terms, and the view's own tile table of quarters.
+int32_t ensure_sq8w(osk_view* v, hipStream_t st) {
+    if (v->sq8w_ready) return OSK_OK;
+    int32_t rc = ensure_sq8t(v, st);
+    if (rc) return rc;
+    const int ns = (int)v->segs.size();
+    std::vector<const void*> rows_w(ns), auxt(ns);
+    for (int i = 0; i < ns; ++i) {
+        rc = ensure_sq8t_seg(v->segs[i], st, true);
+        if (rc) return rc;
         rows_w[i] = v->segs[i]->d_q8w;
         auxt[i] = v->segs[i]->d_q8auxt;
     }
-    OSK_HIP(v->d_sq8_rows_t.reserve(sizeof(void*) * ns));
     OSK_HIP(v->d_sq8_rows_w.reserve(sizeof(void*) * ns));
     OSK_HIP(v->d_sq8_auxt.reserve(sizeof(void*) * ns));
-    OSK_HIP(hipMemcpyAsync(v->d_sq8_rows_t.p, rows.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
     OSK_HIP(hipMemcpyAsync(v->d_sq8_rows_w.p, rows_w.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
     OSK_HIP(hipMemcpyAsync(v->d_sq8_auxt.p, auxt.data(), sizeof(void*) * ns, hipMemcpyHostToDevice, st));
     if (sq8_wide_supported((v->segs.empty() ? 0 : v->segs[0]->units8)) && v->n_tiles > 0) {
@@ -1240,7 +1310,7 @@ int32_t ensure_sq8t(osk_view* v, hipStream_t st) {
                                         v->d_quarter_bm.as<float4>(), st));
     }
     OSK_HIP(hipStreamSynchronize(st));
-    v->sq8t_ready = true;
+    v->sq8w_ready = true;
     return OSK_OK;
 }
 
@@ -1502,11 +1572,11 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
     // scan, ≤ 8 per launch.  Filtered VALU scans run over the compacted accepted ordinals.  A single
     // unfiltered query scans the 6-bit tier where the view has one.
     const bool use_mfma = g_tuning.sq8_mfma_min > 0 && nq >= g_tuning.sq8_mfma_min && sq8_mfma_supported(u8);
-    // large unfiltered batches of ≤ 256-dim rows: one corpus pass per kWideQ queries (osk_sq8w.hip)
+    // large unfiltered batches of ≤ 768-dim rows: one corpus pass per kWideQ queries (osk_sq8w.hip)
     const bool use_wide = use_mfma && !g_tuning.sq8_force_fallback && sq8_wide_pick(v, nq, d_accept != nullptr);
     // the 6-bit tier: single unfiltered queries, every segment's calibration probing or on.  The shared
     // lock keeps a segment's copy alive from this check to the launches (fold_probe frees it under the
-    // exclusive one after a device synchronisation)
+    // exclusive one, with hipFreeAsync behind the events of the launches still reading it: no device wait)
     rc = fold_probe(v, st);
     if (rc) return rc;
     std::shared_lock<std::shared_mutex> tier_lock(g_sq6_free_mu, std::defer_lock);
@@ -1554,8 +1624,8 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
         if (rc) return rc;
     }
     int n_scan_tiles = gather ? v->n_gtiles : v->n_tiles;
-    if (use_wide) {   // its own tile table (ensure_sq8t)
-        rc = ensure_sq8t(v, st);
+    if (use_wide) {   // its own copy and tile table (ensure_sq8w)
+        rc = ensure_sq8w(v, st);
         if (rc) return rc;
         n_scan_tiles = v->n_wtiles;
     }

@@ -711,10 +711,22 @@ int32_t osk_shards_search_merge_device(osk_comm* comm, osk_view* view, const voi
     OSK_REQUIRE(d_scores && d_docs && d_shard_out && d_count && d_total_hits && d_max_score, "null output");
     OSK_REQUIRE(comm->devices.size() == 1, "the device entry serves one-device-per-process communicators");
     OSK_REQUIRE(view->device == comm->devices[0], "the view is not on the communicator's device");
-    OSK_REQUIRE(view->n_shards <= shards_per_rank, "the view holds more shards than shards_per_rank");
-    int32_t rc = check_merge_args(comm, n_queries, k, from, size, shards_per_rank);
-    if (rc) return rc;
-    rc = check_device(view->device);
+    // Argument errors of this rank alone (its shard count, batch, k, from/size).  At world 1 they return at
+    // once.  At world > 1 the other ranks are about to enter the all-gather, so this rank must still issue
+    // it: it sends the refusal header below (every rank's reduce then reports count −1 and the communicator
+    // is poisoned), skips its own reduce (its output buffers may not fit the shape it was given) and returns
+    // OSK_ERR_INVALID with the message.
+    std::string local_err;
+    if (view->n_shards > shards_per_rank) {
+        local_err = "the view holds more shards than shards_per_rank";
+    } else if (check_merge_args(comm, n_queries, k, from, size, shards_per_rank) != OSK_OK) {
+        local_err = osk_last_error();
+    }
+    if (!local_err.empty() && comm->world == 1) {
+        set_error(local_err);
+        return OSK_ERR_INVALID;
+    }
+    int32_t rc = check_device(view->device);
     if (rc) return rc;
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : device_stream(view->device);
     // No refusal on the poison flag here: the previous call's reduce writes it asynchronously, so a rank
@@ -730,7 +742,8 @@ int32_t osk_shards_search_merge_device(osk_comm* comm, osk_view* view, const voi
     // header (magic kXRefused) with empty lists, so every rank's reduce reports count −1 and no rank waits
     // alone in the all-gather; this rank returns OSK_ERR_INVALID after issuing it.
     const bool fixed = comm->world > 1;
-    const bool over = fixed && (n_queries > comm->dev_max_nq || k > comm->dev_max_k ||
+    const bool refuse_local = !local_err.empty();   // (world > 1 here)
+    const bool over = fixed && (refuse_local || n_queries > comm->dev_max_nq || k > comm->dev_max_k ||
                                 shards_per_rank > comm->dev_max_spr);
     const Block B = fixed ? fixed_block_of(comm) : block_of(n_queries, k, shards_per_rank);
     uint64_t hw[kXHdrWords];
@@ -762,6 +775,11 @@ int32_t osk_shards_search_merge_device(osk_comm* comm, osk_view* view, const voi
         if (rc) return rc;
         OSK_HIP(leave_xstream(comm, 0, st));
         image = view->ws_xgath.as<uint64_t>();
+    }
+    if (refuse_local) {
+        set_error("osk_shards_search_merge_device: " + local_err +
+                  " (refused on every rank: their reduce reports count -1, communicator poisoned)");
+        return OSK_ERR_INVALID;
     }
     const int32_t* sidx = nullptr;
     XLayout x = image_layout(comm, image, B, &sidx);

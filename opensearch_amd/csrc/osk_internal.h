@@ -363,6 +363,9 @@ constexpr int kAuxGroupF4 = 22;                 // float4 per 16-row group of th
 int sq8_wide_supported(int units8);
 int sq8_wide_ks(int units8);                    // its 64-dim slabs per row: 2, 4, 8 or 12
 hipError_t launch_sq8_wide(const Sq8Params& p, hipStream_t s, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
+#ifdef OSK_TESTING
+hipError_t launch_glds_probe(const int4* src, int4* out, hipStream_t s);   // (osk_testing_glds_probe)
+#endif
 // The wide kernel's copy of a segment's fp32 rows (units float4 per row): int8 codes with ONE scale per
 // 16-row group (s_g = the group's max |x| / 127), in the MFMA-tiled layout (16-row blocks × sq8_wide_ks slabs of
 // 1 KiB, chunk-major), and per group kAuxGroupF4 float4 of bound terms (352 B): s_g[16] (COSINE: each row's

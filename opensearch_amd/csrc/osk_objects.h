@@ -190,11 +190,12 @@ struct osk_view {
     osk::DevBuf d_sq8_rows_w;                         // per segment: the wide kernel's group-scaled copy
     osk::DevBuf d_sq8_auxt, d_shard_quarter_begin;    // per segment: its tiled bound terms (sq8_wide); 4·shard_tile_begin
     osk::DevBuf d_quarter_bm;                         // per (wide tile, quarter): its rows' bound-term maxima
-    // sq8_wide's own tiles (ensure_sq8t: quarters of ≈ R / (2·CUs) rows), their shard ranges and dispatch order
+    // sq8_wide's own tiles (ensure_sq8w: quarters of ≈ R / (2·CUs) rows), their shard ranges and dispatch order
     osk::DevBuf d_wtiles, d_wtile_order, d_wshard_tile_begin;
     std::vector<int32_t> wshard_tile_begin;
     int n_wtiles = 0;
-    bool sq8t_ready = false;
+    bool sq8t_ready = false;   // sq8_mfma's tiled copy pointers (ensure_sq8t)
+    bool sq8w_ready = false;   // the wide kernel's copies, pointers and tile table (ensure_sq8w)
     osk::DevBuf d_sq6_rows, d_sq6_aux;                // per segment: the 6-bit tier (every segment has one or
     bool sq6_ready = false;                           // the view does not use it)
     int64_t sq6_calls = 0;

@@ -1233,4 +1233,39 @@ hipError_t launch_sq8_wide(const Sq8Params& p, hipStream_t s, hipEvent_t ev_star
     return hipGetLastError();
 }
 
+#ifdef OSK_TESTING
+// glds16_run's destination contract, kept as a GPU test (tests/test_gpu_wide.py::test_glds16_run_destinations;
+// round 5 built the one-statement DMAs on the wrong reading of the immediate offset and faulted a box): for
+// N = 1, 2, 4 DMAs at both strides the kernel uses (1 KiB slabs, kAuxGroupF4 bound-term groups), each DMA k
+// reads gbase + lane·16 + k·GS and must land at ldsk[k] + lane·16 — the destinations here are out of order and
+// not GS apart — with every other LDS byte untouched.  One 64-lane workgroup; out: 6 images of the 16 KiB LDS.
+template <int N, int GS>
+__device__ void glds_probe_case(const int4* src, int4* lds, int4* out) {
+    for (int i = threadIdx.x; i < 1024; i += 64) lds[i] = make_int4(-1, -1, -1, -1);
+    __syncthreads();
+    const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(__attribute__((address_space(3))) char*)lds);
+    uint32_t ldsk[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) ldsk[k] = base + (uint32_t)((N - 1 - k) * 2048 + 512);
+    glds16_run<N, GS>(src, (uint32_t)threadIdx.x * 16u, ldsk);
+    vm_wait<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    for (int i = threadIdx.x; i < 1024; i += 64) out[i] = lds[i];
+    __syncthreads();
+}
+__global__ __launch_bounds__(64) void glds_probe(const int4* src, int4* out) {
+    __shared__ __attribute__((aligned(16))) int4 lds[1024];
+    glds_probe_case<1, 1024>(src, lds, out);
+    glds_probe_case<2, 1024>(src, lds, out + 1024);
+    glds_probe_case<4, 1024>(src, lds, out + 2048);
+    glds_probe_case<1, kAuxGroupF4 * 16>(src, lds, out + 3072);
+    glds_probe_case<2, kAuxGroupF4 * 16>(src, lds, out + 4096);
+    glds_probe_case<4, kAuxGroupF4 * 16>(src, lds, out + 5120);
+}
+hipError_t launch_glds_probe(const int4* src, int4* out, hipStream_t s) {
+    hipLaunchKernelGGL(glds_probe, dim3(1), dim3(64), 0, s, src, out);
+    return hipGetLastError();
+}
+#endif
+
 }  // namespace osk

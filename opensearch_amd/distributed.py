@@ -29,6 +29,9 @@ from . import _lib
 from ._lib import check, lib, ptr
 
 
+DEFAULT_DEVICE_LIMITS = (1, 100, 8)   # osk_comm_set_device_limits' defaults (include/osknn.h)
+
+
 class DeviceComm:
     """An RCCL communicator owned by libosknn (`osk_comm`, include/osknn.h)."""
 
@@ -94,14 +97,30 @@ class DeviceComm:
         osk_shards_search_merge_device call all-gathers a block of this fixed size, so ranks whose calls
         differ get count −1 instead of an all-gather of mismatched counts.  Same values on every rank."""
         check(lib().osk_comm_set_device_limits(self._h, max_queries, max_k, max_shards_per_rank))
+        self._limits = (max_queries, max_k, max_shards_per_rank)
+
+    @property
+    def device_limits(self) -> tuple[int, int, int]:
+        """(max queries, max k, max shards per rank) of the device entry's exchange block."""
+        return getattr(self, "_limits", DEFAULT_DEVICE_LIMITS)
+
+    def fits_device_limits(self, nq: int, k: int, shards_per_rank: int) -> bool:
+        mq, mk, ms = self.device_limits
+        return nq <= mq and k <= mk and shards_per_rank <= ms
 
     @classmethod
-    def from_process_group(cls, device: int, group=None) -> "DeviceComm":
-        """Rank 0 makes the id; torch.distributed (any backend) hands it to the other ranks."""
+    def from_process_group(cls, device: int, group=None, device_limits: tuple[int, int, int] | None = None
+                           ) -> "DeviceComm":
+        """Rank 0 makes the id; torch.distributed (any backend) hands it to the other ranks.  device_limits
+        (max queries, max k, max shards per rank), when given, are set right after init — pass the same
+        values on every rank."""
         rank, world = dist.get_rank(group), dist.get_world_size(group)
         obj = [cls.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0, group=group)
-        return cls.init_rank(device, rank, world, obj[0])
+        comm = cls.init_rank(device, rank, world, obj[0])
+        if device_limits is not None:
+            comm.set_device_limits(*device_limits)
+        return comm
 
     @property
     def handle(self):
@@ -124,9 +143,17 @@ class ShardSearchMerge:
     are preallocated and overwritten by the next call."""
 
     def __init__(self, comm: DeviceComm, view, shards_per_rank: int, nq: int, k: int, from_: int, size: int,
-                 device: int):
+                 device: int, check_limits: bool = True):
         self.comm, self.view, self.spr = comm, view, shards_per_rank
         self.nq, self.k, self.from_, self.size = nq, k, from_, size
+        # at world > 1 the exchange block must hold this call's shape (osk_comm_set_device_limits).  Checked here,
+        # before any collective: a call beyond the limits would be refused on every rank (count −1, communicator
+        # poisoned).  The limits are never raised implicitly — a rank that raised them alone would all-gather a
+        # block of another size than its peers (undefined under RCCL: a hang).
+        if check_limits and comm.world > 1 and not comm.fits_device_limits(nq, k, shards_per_rank):
+            raise ValueError(f"ShardSearchMerge(nq={nq}, k={k}, shards_per_rank={shards_per_rank}) exceeds the "
+                             f"communicator's device limits {comm.device_limits}: call "
+                             f"comm.set_device_limits(...) with the same values on every rank first")
         dev = torch.device("cuda", device)
         self.out = (torch.empty((nq, size), dtype=torch.float32, device=dev),
                     torch.empty((nq, size), dtype=torch.int32, device=dev),

@@ -107,3 +107,18 @@ def test_shard_ownership_is_contiguous_and_complete():
         owned = [D.owned_shards(r, 8, world) for r in range(world)]
         assert sorted(s for o in owned for s in o) == list(range(8))
         assert all(o == list(range(o[0], o[0] + len(o))) for o in owned if o)
+
+
+def test_shard_search_merge_checks_the_device_limits_before_any_collective():
+    """The Python step refuses a shape beyond the communicator's device limits at construction (world > 1),
+    with the call to make, instead of a refused, poisoning collective later."""
+    from opensearch_amd import distributed as D
+
+    class _Comm:
+        world, device_limits = 2, D.DEFAULT_DEVICE_LIMITS
+
+        def fits_device_limits(self, nq, k, spr):
+            return D.DeviceComm.fits_device_limits(self, nq, k, spr)
+
+    with pytest.raises(ValueError, match="set_device_limits"):
+        D.ShardSearchMerge(_Comm(), None, 1, 2, 10, 0, 10, device=0)

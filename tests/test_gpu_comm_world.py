@@ -86,10 +86,11 @@ def _worker(rank, world, name, mode, out_q):
                 comm.set_device_limits(165, 100, spr)
             stream = torch.cuda.Stream()
 
-            def device_call(nq, k, from_, size, qs):
+            def device_call(nq, k, from_, size, qs, spr=spr):
                 dq = torch.from_numpy(_queries(nq, qs)).cuda()
                 torch.cuda.synchronize()
-                step = D.ShardSearchMerge(comm, view, spr, nq, k, from_, size, device=0)
+                # (check_limits off: these calls test the library's own refusal, past the Python-side check)
+                step = D.ShardSearchMerge(comm, view, spr, nq, k, from_, size, device=0, check_limits=False)
                 res = step(dq.data_ptr(), stream.cuda_stream)
                 stream.synchronize()
                 return [t.cpu().numpy().copy() for t in res]
@@ -142,6 +143,22 @@ def _worker(rank, world, name, mode, out_q):
                 nq = 1 if rank == 0 else 2
                 try:
                     first = device_call(nq, 10, 0, 10, 5)
+                    results = ["ok", first[3].tolist()]
+                except _lib.OskError as e:
+                    stream.synchronize()
+                    results = [e.code, str(e)]
+                rc, info = comm.status()
+                results += [rc, info[0]]
+            elif mode in ("badspr", "badfrom"):
+                # rank 1's own arguments are wrong (its view holds more shards than the shards_per_rank it
+                # passes / a negative from): it must still issue the all-gather (refusal header), so rank 0 is
+                # not left waiting in it; rank 1 returns OSK_ERR_INVALID, rank 0 reports count −1
+                bad = rank == 1
+                try:
+                    if mode == "badspr":
+                        first = device_call(1, 10, 0, 10, 5, spr=len(shards) - 1 if bad else spr)
+                    else:
+                        first = device_call(1, 10, -1 if bad else 0, 10, 5)
                     results = ["ok", first[3].tolist()]
                 except _lib.OskError as e:
                     stream.synchronize()
@@ -282,6 +299,17 @@ def test_device_entry_call_beyond_the_limits_is_refused_on_every_rank():
     assert out[0][2] == -1 and out[0][3] == 1
     assert out[1][0] == -1 and "device limits" in out[1][1], out[1]
     assert out[1][2] == -1 and out[1][3] == 1
+
+
+@pytest.mark.parametrize("mode", ["badspr", "badfrom"])
+def test_device_entry_rank_local_argument_error_still_issues_the_gather(mode):
+    """a rank whose own arguments fail (shards_per_rank below its view's shard count, a bad from)
+    used to return before the all-gather and leave the other ranks inside it.  It now sends a refusal header:
+    the other rank's reduce reports count −1 (no hang), the failing rank returns OSK_ERR_INVALID."""
+    out = _run(2, mode)
+    assert out[0][0] == "ok" and out[0][1] == [-1], out[0]
+    assert out[0][2] == -1 and out[0][3] == 1
+    assert out[1][0] == -1 and "refused on every rank" in out[1][1], out[1]
 
 
 def test_mismatched_batch_size_fails_the_host_entry_before_the_gather():

@@ -10,7 +10,13 @@ bench and `tools/bench_configs.py` time them, on the same corpora:
 * C5: the C3 corpus under 1 % and 50 % Bernoulli filters (compacted gather scan), and the 10M × 768
   byte-vector corpus (EUCLIDEAN, `scan_i8_stream`), batch 1.
 * C4: 100M × 96 DOT_PRODUCT, 8 shards × 12.5M: batch 1024 on the wide int8 prefilter (32 sampled
-  queries), batch 1 and batch 32.
+  queries), batch 1 and batch 32; the same size under MAXIMUM_INNER_PRODUCT (raw rows), b1024 and b1.
+* C1: 100k × 128 EUCLIDEAN, one shard, all 1,000 queries through `GpuKnnFloatVectorQuery.rewrite`, Lucene's
+  per-leaf `KnnFloatVectorQuery` route over the GPU reader, and one batched C-ABI call.
+* C2: 1M × 128 EUCLIDEAN (SIFT-like), one shard, single queries on `sq8_scan`.
+
+The sampled batches are then checked whole: every query of C3 b256 and C4 b1024 equals the fp32 streaming
+scan (`sq8` off), itself bit-exact to the oracle at these sizes (b1 cases above).
 
 Every check is docs, shard indices and score bits of the coordinator merge against the oracle's
 per-shard [L] exactSearch (device summation order) + TopDocs.merge
@@ -101,13 +107,13 @@ def c3():
     q = {"b1": pool[:6], "b32": pool[:32], "b256": pool}
     samp = {"b1": list(range(6)), "b32": list(range(32)), "b256": list(_sample(256, 16, 11))}
     rng = np.random.default_rng(17)
-    accepts = [[rng.random(C3_RPS) < sel for _ in range(N_SHARDS)] for sel in (0.01, 0.50)]
+    accepts = [[rng.random(C3_RPS) < sel for _ in range(N_SHARDS)] for sel in (0.01, 0.10, 0.50)]
     fq = O.synth(0, 1, C3_DIM, 907, DIST_UNIT)
     names = list(q)
     res =_oracle(C3_RPS, C3_DIM, SIM.COSINE, 42, DIST_UNIT, [q[n][samp[n]] for n in names])
     want = dict(zip(names, res))
     filt = _oracle(C3_RPS, C3_DIM, SIM.COSINE, 42, DIST_UNIT, [fq], accepts=accepts)
-    want["f1"], want["f50"] = filt[0][0], filt[1][0]
+    want["f1"], want["f10"], want["f50"] = filt[0][0], filt[1][0], filt[2][0]
     yield ds, q, samp, want, fq, accepts
     ds.close()
     for r in readers:
@@ -141,13 +147,32 @@ def test_c3_full_b256_library_path(c3):
     out, d = _counted(ds, q["b256"], ("sq8_calls", "mfma_calls", "sq8_wide_calls"))
     assert d["sq8_calls"] + d["mfma_calls"] == 1, d
     _check(out, want["b256"], samp["b256"])
+    _equals_fp32_scan(ds, q["b256"], out)
 
 
-@pytest.mark.parametrize("which", ["f1", "f50"])
+_MFMA_MIN_BATCH = 96   # the library's default (osk_internal.h)
+
+
+def _equals_fp32_scan(ds, queries, out):
+    """Every query of the batch (not only the oracle's sample) against the fp32 streaming scan — the
+    prefilter off, `scan_f32`'s exact device order — docs, shard indices and score bits."""
+    _lib.tune("sq8", 0)
+    _lib.tune("mfma_min_batch", 0)   # and not the bf16×3 blocks: scan_f32, ≤ 8 queries per launch
+    try:
+        ref = ds.search(queries, K, 0, K)
+    finally:
+        _lib.tune("sq8", 1)
+        _lib.tune("mfma_min_batch", _MFMA_MIN_BATCH)
+    for a, b in zip(out, ref):
+        a, b = np.asarray(a), np.asarray(b)
+        assert np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+@pytest.mark.parametrize("which", ["f1", "f10", "f50"])
 def test_c5_full_filtered_b1(c3, which):
-    """C5: 1 % and 50 % accept bitsets over the 10M corpus (compacted gather scan)."""
+    """C5: 1 %, 10 % and 50 % accept bitsets over the 10M corpus (compacted gather scan)."""
     ds, _, _, want, fq, accepts = c3
-    acc = accepts[0 if which == "f1" else 1]
+    acc = accepts[{"f1": 0, "f10": 1, "f50": 2}[which]]
     out, d = _counted(ds, fq, ("sq8_calls",), accept=acc)
     assert d == {"sq8_calls": 1}, d
     _check(out, want[which], [0])
@@ -185,6 +210,7 @@ def test_c4_full_b1024_wide_b32_b1():
         out, d = _counted(ds, q1024, counters)
         assert d == {"sq8_calls": 1, "mfma_calls": 0, "sq8_wide_calls": 1, "sq8_fallback_queries": 0}, d
         _check(out, w1024, s1024)
+        _equals_fp32_scan(ds, q1024, out)
         out, d = _counted(ds, q32, counters)
         assert d["sq8_calls"] == 1 and d["sq8_wide_calls"] == 0, d
         _check(out, w32, range(32))
@@ -196,3 +222,101 @@ def test_c4_full_b1024_wide_b32_b1():
         ds.close()
         for r in readers:
             r.close()
+
+
+def test_c4_full_mip_b1024_wide_b1():
+    """C4 at its size under MAXIMUM_INNER_PRODUCT (raw, unnormalised rows: the score transform's two branches):
+    b1024 on the wide kernel (32 sampled queries, then all 1,024 against the fp32 scan) and b1."""
+    rps, dim, seed, dist = 12_500_000, 96, 4242, _lib.DIST_NORMALISH
+    readers = _readers(rps, dim, SIM.MAXIMUM_INNER_PRODUCT, seed, dist)
+    ds = LU.DeviceShardSet([[LU.LeafReaderContext(0, 0, r)] for r in readers], SHARD_INDEX)
+    counters = ("sq8_calls", "mfma_calls", "sq8_wide_calls", "sq8_fallback_queries")
+    try:
+        q1024 = O.synth(0, 1024, dim, 46, dist)
+        s1024 = list(_sample(1024, 32, 13))
+        q1 = O.synth(0, 2, dim, 47, dist)
+        w1024, w1 = _oracle(rps, dim, SIM.MAXIMUM_INNER_PRODUCT, seed, dist, [q1024[s1024], q1])
+        out, d = _counted(ds, q1024, counters)
+        assert d == {"sq8_calls": 1, "mfma_calls": 0, "sq8_wide_calls": 1, "sq8_fallback_queries": 0}, d
+        _check(out, w1024, s1024)
+        _equals_fp32_scan(ds, q1024, out)
+        for i in range(2):
+            out, d = _counted(ds, q1[i:i + 1], counters)
+            assert d["sq8_calls"] == 1 and d["sq8_wide_calls"] == 0, d
+            _check(out, [w1[i]], [0])
+    finally:
+        ds.close()
+        for r in readers:
+            r.close()
+
+
+# ---------------------------------------------------------------------------------------------------
+# C1 (100k × 128 L2, one shard, 1k queries) and C2 batch 1 (1M × 128 L2): tools/bench_configs.py's corpora
+# ---------------------------------------------------------------------------------------------------
+def _one_shard_oracle(n, dim, seed, dist, queries):
+    rows = O.synth_par(0, n, dim, seed, dist, THREADS)
+    sc, dc, cc = O.knn_batch(rows, queries, K, int(SIM.EUCLIDEAN), O.ORDER_DEVICE, THREADS)
+    return sc, dc, cc
+
+
+def test_c1_full_1k_queries():
+    """BASELINE configs[0] on the HIP path: all 1,000 queries (seeds 42 / 43) three ways —
+    (1) the plugin's `GpuKnnFloatVectorQuery.rewrite` (one device call per shard, ContextIndexSearcher.rewrite,
+        `server/src/main/java/org/opensearch/search/internal/ContextIndexSearcher.java:203-218`) over a shard
+        of three segments, then the shard's query phase;
+    (2) Lucene's per-leaf `KnnFloatVectorQuery.rewrite` over the same leaves (one `KnnVectorsReader.search`
+        per leaf on the GPU reader, `TopDocs.merge(k, perLeaf)`);
+    (3) one batched C-ABI call over the single-segment shard (`osk_view_search`, 1,000 queries).
+    Each equals the oracle's exactSearch over the whole 100k rows: docs and score bits."""
+    n, dim, nq = 100_000, 128, 1_000
+    dist = _lib.DIST_UNIFORM01
+    queries = O.synth(0, nq, dim, 43, dist)
+    sc, dc, cc = _one_shard_oracle(n, dim, 42, dist, queries)
+    assert np.all(cc == K)
+    bounds = (0, 37_000, 71_500, n)
+    segs = [LU.GpuFlatVectorsReader.synthetic("v", bounds[i + 1] - bounds[i], dim, SIM.EUCLIDEAN, seed=42,
+                                              dist=dist, row0=bounds[i]) for i in range(3)]
+    leaves = [LU.LeafReaderContext(i, bounds[i], segs[i]) for i in range(3)]
+    whole = LU.GpuFlatVectorsReader.synthetic("v", n, dim, SIM.EUCLIDEAN, seed=42, dist=dist)
+    ds = LU.DeviceShardSet([[LU.LeafReaderContext(0, 0, whole)]], [0])
+    try:
+        def same(td, i):
+            d = np.array([h.doc for h in td.score_docs], np.int32)
+            s = np.array([h.score for h in td.score_docs], np.float32)
+            assert np.array_equal(d, dc[i]), (i, d, dc[i])
+            assert np.array_equal(s.view(np.uint32), sc[i].view(np.uint32)), i
+
+        for i in range(nq):
+            same(LU.shard_query_phase(LU.GpuKnnFloatVectorQuery("v", queries[i], K), leaves, 0, K), i)
+        for i in range(0, nq, 7):          # the per-leaf route: 3 reader calls per query
+            same(LU.KnnFloatVectorQuery("v", queries[i], K).rewrite(leaves), i)
+        s, d, sh, c, t, _ = ds.search(queries, K, 0, K)
+        assert np.all(c == K) and np.all(sh == 0)
+        assert np.array_equal(d, dc) and np.array_equal(s.view(np.uint32), sc.view(np.uint32))
+    finally:
+        LU.GpuKnnFloatVectorQuery.release_views()
+        ds.close()
+        whole.close()
+        for r in segs:
+            r.close()
+
+
+def test_c2_full_b1():
+    """C2 batch 1: 1M × 128 SIFT-like EUCLIDEAN rows, single queries on `sq8_scan` (the bench's corpus and
+    query pool)."""
+    n, dim = 1_000_000, 128
+    dist = _lib.DIST_UNIFORM01_X128
+    q = O.synth(0, 8, dim, 43, dist)
+    sc, dc, cc = _one_shard_oracle(n, dim, 42, dist, q)
+    r = LU.GpuFlatVectorsReader.synthetic("v", n, dim, SIM.EUCLIDEAN, seed=42, dist=dist)
+    ds = LU.DeviceShardSet([[LU.LeafReaderContext(0, 0, r)]], [0])
+    try:
+        for i in range(len(q)):
+            out, d = _counted(ds, q[i:i + 1], ("sq8_calls", "mfma_calls", "sq8_wide_calls"))
+            assert d == {"sq8_calls": 1, "mfma_calls": 0, "sq8_wide_calls": 0}, d
+            s, dd, sh, c, t, _ = out
+            assert c[0] == K and np.array_equal(dd[0], dc[i]), (i, dd[0], dc[i])
+            assert np.array_equal(s[0].view(np.uint32), sc[i].view(np.uint32)), i
+    finally:
+        ds.close()
+        r.close()

@@ -271,3 +271,46 @@ def test_wide_immediate_and_deferred_insertions_agree(sim, defer):
     finally:
         _lib.tune("sq8_wide_defer", 1)
         close_all(ds, readers)
+
+
+def test_glds16_run_destinations():
+    """The one-statement LDS-DMA helper the wide kernel's ring runs on (glds16_run, osk_device.h): N = 1, 2, 4
+    DMAs at the slab stride (1 KiB) and the bound-term stride (kAuxGroupF4 · 16 B) land exactly at their own
+    out-of-order LDS destinations (M0 + immediate offset + lane·16 = the destination), nothing else written.
+    Round 5's first one-statement build read the offset as global-only and faulted a box (DESIGN §3g item 6);
+    a compiler or ISA change to that semantics fails here, not as a parity failure elsewhere."""
+    import ctypes as C
+    with _lib.testing() as T:
+        bad = C.c_int64(-1)
+        _lib.check(T.osk_testing_glds_probe(0, C.byref(bad)))
+        assert bad.value == 0, f"{bad.value} LDS words differ from the expected DMA image"
+
+
+def test_wide_copy_is_built_only_when_a_batch_takes_the_wide_kernel():
+    """The group-scaled copy (codes + tiled bound terms, osk_sq8w.hip launch_sq8w_build) is the wide kernel's
+    alone: warming the MFMA prefilter and running sq8_mfma batches leave it unbuilt; the first batch the cost
+    model sends to the wide kernel builds it."""
+    import ctypes as C
+    n, dim = 5000, 96
+    rows = corpus(n, dim, SIMS[1], 2601)
+    q = corpus(64, dim, SIMS[1], 2602)
+    ds, readers = view_of([rows], SIMS[1], [0])
+    r = readers[0]
+
+    def footprint():
+        b = C.c_int64()
+        _lib.check(_lib.lib().osk_seg_footprint(r.handle, C.byref(b)))
+        return b.value
+
+    try:
+        _lib.check(_lib.lib().osk_view_warm(ds.handle, _lib.OSK_WARM_PREFILTER_MFMA))
+        warmed = footprint()
+        narrow = tuned("sq8_wide_min", 0, WIDE_MIN, lambda: ds.search(q, 10, 0, 10))
+        assert footprint() == warmed and ds.counter("sq8_wide_calls") == 0
+        wide = ds.search(q, 10, 0, 10)
+        assert ds.counter("sq8_wide_calls") == 1
+        groups = (n + 15) // 16
+        assert footprint() == warmed + groups * 2 * 1024 + groups * 22 * 16   # KS = 2 slabs + kAuxGroupF4 terms
+        assert_same(wide, narrow)
+    finally:
+        close_all(ds, readers)
