@@ -321,6 +321,8 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         {"sq8_wide_quarter_rows", &g_tuning.sq8_wide_quarter_rows, 0, 1 << 20, false},
         {"sq8_wide_pilot_rows", &g_tuning.sq8_wide_pilot_rows, 0, 1 << 16, false},
         {"sq8_wide_defer", &g_tuning.sq8_wide_defer, 0, 1, false},
+        {"sq8_wide_rows", &g_tuning.sq8_wide_rows, 0, 1, false},
+        {"sq8_wide_rows_qcap", &g_tuning.sq8_wide_rows_qcap, 0, 1 << 20, false},
         {"sq6_rebound_stride", &g_tuning.sq6_rebound_stride, 0, 1, false},
         {"sq6_rebound_retest", &g_tuning.sq6_rebound_retest, 0, 1, false},
         {"sq6_rebound_wgs", &g_tuning.sq6_rebound_wgs, 0, 16, false},
@@ -381,14 +383,14 @@ int32_t osk_testing_glds_probe(int32_t device, int64_t* out_mismatches) {
         set_error(std::string("glds probe: ") + hipGetErrorString(e));
         return OSK_ERR_DEVICE;
     }
-    // the expected image of each case: DMA k's 64 lanes at (N − 1 − k)·2048 + 512 + lane·16, all else −1
+    // the expected image of each case: DMA k's 64 lanes at 3072 + (N − 1 − k)·2048 + 512 + lane·16, all else −1
     int64_t bad = 0;
     const int ns[kCases] = {1, 2, 4, 1, 2, 4}, gs[kCases] = {1024, 1024, 1024, kAuxGroupF4 * 16, kAuxGroupF4 * 16,
                                                              kAuxGroupF4 * 16};
     for (int c = 0; c < kCases; ++c) {
         std::vector<int4> want(kImg, make_int4(-1, -1, -1, -1));
         for (int k = 0; k < ns[c]; ++k)
-            for (int l = 0; l < 64; ++l) want[((ns[c] - 1 - k) * 2048 + 512) / 16 + l] = h_src[(k * gs[c]) / 16 + l];
+            for (int l = 0; l < 64; ++l) want[(3072 + (ns[c] - 1 - k) * 2048 + 512) / 16 + l] = h_src[(k * gs[c]) / 16 + l];
         for (int i = 0; i < kImg; ++i) {
             const int4 a = h_out[(size_t)c * kImg + i], b = want[i];
             bad += a.x != b.x || a.y != b.y || a.z != b.z || a.w != b.w;
@@ -1739,16 +1741,22 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             // would idle the chip, and a partial round leaves a tail)
             const int rounds = std::max(1, (int)std::lround((double)nql / ((double)phase * wgrid)));
             const int n_a = phase > 1 ? std::min(nql / 2, rounds * wgrid) : 0;
+            // ≤ 128 dims: the main passes without a step barrier (sq8_wide_rows, osk_sq8w.hip)
+            const bool rows = g_tuning.sq8_wide_rows && sq8_wide_rows_supported(u8);
+            p.wide_qcap = rows ? (int)g_tuning.sq8_wide_rows_qcap : 0;
+            auto main_pass = [&](hipEvent_t ev) {
+                return rows ? launch_sq8_wide_rows(p, st, nullptr, ev) : launch_sq8_wide(p, st, nullptr, ev);
+            };
             if (n_a > 0) {   // (the pilot zeroed every list maximum: the second pass's read as empty)
                 uint32_t* lbm = p.list_lbmax + (size_t)q0 * nql;
                 p.quarter_end = n_a;
-                OSK_HIP(launch_sq8_wide(p, st, nullptr, nullptr));
+                OSK_HIP(main_pass(nullptr));
                 OSK_HIP(launch_wide_floor(lbm, nullptr, nql, sqb, S, p.q_count, k, floor_a, floor_b, st));
                 p.quarter_begin = n_a;
                 p.quarter_end = 0;
                 p.floors = floor_b;
             }
-            OSK_HIP(launch_sq8_wide(p, st, nullptr, e1));
+            OSK_HIP(main_pass(e1));
         } else if (use_mfma) {
             // pilot: 16 sampled rows per wave → per (query, tile) the top k sampled lower bounds →
             // per (query, shard) the top k; its k-th floors the main pass's quick thresholds

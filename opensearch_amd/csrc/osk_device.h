@@ -137,7 +137,9 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_byte) {
 }
 // N such DMAs in one statement (M0 saved once): the k-th from gbase + voff + k·GS (GS·(N−1) ≤ 4095: the
 // instruction's immediate offset; gbase wave-uniform, in SGPRs) into LDS at lds[k].  The immediate offset
-// moves the LDS destination too (M0 + offset + lane·16: tools/glds_offset_probe.hip), so M0 = lds[k] − k·GS.
+// moves the LDS destination too (M0 + offset + lane·16: tools/glds_offset_probe.hip), so M0 = lds[k] − k·GS,
+// which must not go below 0: lds[k] ≥ k·GS (an M0 that wraps does not land — osk_testing_glds_probe; every
+// caller's destinations grow by ≥ GS per DMA from the ring's base).
 template <int N, int GS>
 __device__ __forceinline__ void glds16_run(const void* gbase, uint32_t voff, const uint32_t (&ldsk)[N]) {
     static_assert((N == 1 || N == 2 || N == 4) && GS * (N - 1) <= 4095, "glds16_run: 1, 2 or 4 DMAs");

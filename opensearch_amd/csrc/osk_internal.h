@@ -363,6 +363,10 @@ constexpr int kAuxGroupF4 = 22;                 // float4 per 16-row group of th
 int sq8_wide_supported(int units8);
 int sq8_wide_ks(int units8);                    // its 64-dim slabs per row: 2, 4, 8 or 12
 hipError_t launch_sq8_wide(const Sq8Params& p, hipStream_t s, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
+// the wide kernel's main passes for ≤ 128-dim rows without a step barrier (osk_sq8w.hip sq8_wide_rows)
+bool sq8_wide_rows_supported(int u8);
+hipError_t launch_sq8_wide_rows(const Sq8Params& p, hipStream_t s, hipEvent_t ev_start = nullptr,
+                                hipEvent_t ev_stop = nullptr);
 #ifdef OSK_TESTING
 hipError_t launch_glds_probe(const int4* src, int4* out, hipStream_t s);   // (osk_testing_glds_probe)
 #endif
@@ -461,6 +465,8 @@ struct Tuning {
     std::atomic<int> sq6_rebound_retest{1};   // sq6_rebound: the final-floor 6-bit re-test (0: gather every candidate)
     std::atomic<int> sq6_rebound_stride{1};   // sq6_rebound: strided list assignment (0: contiguous)
     std::atomic<int> sq6_rebound_wgs{0};      // sq6_rebound: workgroups per CU (0: as many as fit)
+    std::atomic<int> sq8_wide_rows{1};    // wide kernel, ≤ 128 dims: the main passes on sq8_wide_rows (0: sq8_wide)
+    std::atomic<int> sq8_wide_rows_qcap{0};   // (tests) its deferred queue per owner wave, entries (0: kRowsQC)
     std::atomic<int> sq8_wide_defer{1};   // wide kernel: defer list insertions to each quarter's end (0: immediate)
     std::atomic<int> sq8_wide_quarter_rows{0};   // rows per wide quarter, read when a view builds its table (0 = auto)
     std::atomic<int> sq8_wide_force{0};   // (tests) the wide kernel for every eligible batch, whatever the model says

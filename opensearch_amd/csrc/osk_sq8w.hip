@@ -1188,6 +1188,477 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
 #endif
 }
 
+// ------------------------------------------------------------------------------------------------
+// sq8_wide_rows — the wide prefilter for rows of ≤ 128 dims (KS = 2) with no step barrier.
+//
+// sq8_wide shares each LDS ring slot between its 8 waves (each wave owns 32 queries and reads every row of
+// the step), so one barrier per 128-row step couples them: a step in which one wave takes the slow path holds
+// all eight, and at C4 most steps hold one (18 % of wave-steps are slow; DESIGN.md §3g: barrier waits 29 %
+// of wave 0's loop).  Here the roles are transposed: each wave owns ROWS — 16-row group g of a quarter goes
+// to wave g mod 8 — and multiplies them against ALL 256 queries, whose B fragments it keeps in VGPRs for the
+// launch (2 slabs × 16 query blocks × 4 = 128 VGPRs, which is why only KS = 2 takes this kernel).  A wave
+// loads its own groups straight into VGPRs (the tiled copy is lane-linear: a 1 KiB slab IS the A operand),
+// kRowsD groups ahead, and never waits for another wave inside a quarter.
+//   * the quick test per (group, query block) is sq8_wide's fast test (quick_consts: relaxed to the quarter's
+//     row maxima), its per-(query, quarter) constants in an LDS table computed once per quarter;
+//   * a passing (group, query block) runs the per-row test and appends each passing pair {int32 dot,
+//     row << 8 | query} to the queue of the wave that OWNS the query (wave w owns queries 32w … 32w + 31:
+//     their lists, floors and flush), one LDS atomic per block for the slots;
+//   * at the quarter's end (two barriers per quarter, ≈ 1,000 groups at C4) each wave drains its queue —
+//     precise bounds, floor, list appends or the ordered insertion, exactly sq8_wide's deferred drain — and
+//     flushes its queries' lists for the settle.  A queue that fills drops its further entries and marks
+//     their (quarter, query) lists for an exact re-scan by the settle (16th key above every threshold).
+// Same lists, floors and settle contract as sq8_wide, so results are bit-identical (tests/test_gpu_wide.py).
+// ------------------------------------------------------------------------------------------------
+constexpr int kRowsQC = 1024;   // deferred entries per owner wave and quarter
+constexpr int kRowsD = 2;       // groups in flight per wave (loads issued kRowsD groups ahead)
+constexpr int kRowsQB = 4;      // query blocks per accumulator pass (4 passes of 4 over the 16 blocks)
+
+// a pointer every lane of the wave holds alike (read from LDS), as SGPRs
+__device__ __forceinline__ const char* rfl_ptr_c(const void* ptr) {
+    const uint64_t v = (uint64_t)ptr;
+    return (const char*)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v));
+}
+
+// One group's loads: its two 1 KiB slabs (the A operand) and the bound terms its fast test reads — slot 17
+// {s_g, f_cos, zero-row flag, 0} (x); EUCLIDEAN also the lane's 4 rows' |x|² (w).
+template <int SIM>
+struct RowsItem {
+    int4 a0, a1;
+    float4 x;
+    float4 w;   // (EUCLIDEAN only)
+};
+
+template <int SIM>
+__global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
+    typedef int i32x4 __attribute__((ext_vector_type(4)));
+    constexpr int NQB = kWideQ / 16, QC = kRowsQC, D = kRowsD, PB = kRowsQB;
+    constexpr int sim = SIM;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int col = lane & 15, grp = lane >> 4;
+    const int u8 = p.units8, S = p.n_shards;
+#ifdef OSK_TESTING
+    const int ablate = p.ablate;   // A/B timing only (results wrong): 1 skip the quick tests, 2 skip the MFMAs
+#else
+    constexpr int ablate = 0;
+#endif
+    const int G = gridDim.x, n_quarters = 4 * p.n_tiles;
+    const int qbeg = p.quarter_begin, n_range = (p.quarter_end > 0 ? p.quarter_end : n_quarters) - qbeg;
+    const int n_mine = (int)blockIdx.x < n_range ? (n_range - 1 - (int)blockIdx.x) / G + 1 : 0;
+    const bool floor_lds = S <= kWideMaxFloorShards;
+
+    // (the fixed-size arrays are static LDS: their addresses are constants, so the hot loop's LDS accesses take
+    // immediate offsets instead of address registers)
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ WideCold s_cold;
+    __shared__ uint64_t s_lk[kWideQ * kKQ];                // [kWideQ][kKQ] upper-bound keys
+    __shared__ uint32_t s_lp[kWideQ * kKQ];                // their lower bounds
+    __shared__ __attribute__((aligned(16))) float4 s_qc[kWideQ];   // query bound terms
+    __shared__ uint2 s_q[kWideWaves * QC];                 // [8 owners][QC] deferred entries
+    __shared__ __attribute__((aligned(16))) float s_ca[kWideQ];    // [16 col][16 qb] quick-test constants
+    __shared__ __attribute__((aligned(16))) float s_cb[kWideQ];    // (EUCLIDEAN's second constant)
+    __shared__ float s_qnd[kWideQ];                        // |q|² device order (COSINE)
+    __shared__ int32_t s_cnt[kWideQ];                      // list fill
+    __shared__ int32_t s_ovf[kWideQ];                      // queue overflowed this quarter
+    __shared__ int32_t s_qn[16];                           // [8] queue fill per owner
+    WideQuarter* s_quart = reinterpret_cast<WideQuarter*>(smem);                // [n_mine]
+    uint32_t* s_floor = reinterpret_cast<uint32_t*>(s_quart + n_mine);         // [S][kWideQ] floors (S ≤ 16)
+    if (tid == 0) s_cold = WideCold{p.cand, p.cand_lb, p.list_lbmax, p.visited, p.qn_dev, p.pilot_keys, p.floors, p.q0,
+                                    p.n_lists, p.q_count, 4 * p.n_tiles, p.cos_slack, p.gam, p.g2};
+    for (int i = tid; i < kWideQ * kKQ; i += kWideThreads) {
+        s_lk[i] = 0ull;
+        s_lp[i] = 0u;
+    }
+    for (int i = tid; i < kWideQ; i += kWideThreads) {
+        s_cnt[i] = 0;
+        s_ovf[i] = 0;
+        s_qc[i] = i < p.q_count ? p.qc[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        s_qnd[i] = (SIM == SIM_COSINE && i < p.q_count) ? p.qn_dev[i] : 0.0f;
+    }
+    if (tid < 16) s_qn[tid] = 0;
+    if (floor_lds)
+        for (int i = tid; i < S * kWideQ; i += kWideThreads) {
+            const int qi = i % kWideQ;
+            s_floor[i] = (!p.floors || qi >= p.q_count) ? 0u : p.floors[(size_t)qi * S + i / kWideQ];
+        }
+    for (int i = tid; i < n_mine; i += kWideThreads) {
+        const int j = qbeg + (int)blockIdx.x + i * G;
+        const int tix = p.tile_order ? p.tile_order[j >> 2] : j >> 2, quarter = j & 3;
+        const TileDev tile = p.tiles[tix];
+        const int64_t trows = tile.row_end - tile.row_begin;
+        const int64_t spw = ((trows + 4 * kMfmaScanR - 1) / (4 * kMfmaScanR)) * kMfmaScanR;
+        const int64_t rb = min(tile.row_begin + quarter * spw, tile.row_end);
+        const int64_t re = min(rb + spw, tile.row_end);
+        WideQuarter d;
+        d.xt = p.rows8t[tile.seg] + (rb >> 4) * (2 * 64);
+        d.at = p.auxt[tile.seg] + (rb >> 4) * kAuxGroupF4;
+        d.vrow0 = (uint32_t)(p.seg_vrow[tile.seg] + rb);
+        d.nrows = (int32_t)(re - rb);
+        d.list = tix * 4 + quarter;
+        d.shard = tile.shard;
+        d.seg = tile.seg;
+        d.bm = p.quarter_bm[d.list];
+        s_quart[i] = d;
+    }
+    // the launch's query fragments: query block qb, slab s (lane: query qb·16 + col, 16-B unit 4s + grp)
+    i32x4 bfr[2][NQB];
+#pragma unroll
+    for (int qb = 0; qb < NQB; ++qb) {
+        const int qi = qb * 16 + col;
+        const bool qv = qi < p.q_count;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int f = s * 4 + grp;
+            const int4 v = (qv && f < u8) ? p.q8[(int64_t)qi * u8 + f] : make_int4(0, 0, 0, 0);
+            bfr[s][qb] = i32x4{v.x, v.y, v.z, v.w};
+        }
+    }
+    const int wq0 = wave * 32;   // this wave owns queries wq0 … wq0 + 31 (their lists, queue and flush)
+    const int qcap = p.wide_qcap > 0 ? min(p.wide_qcap, QC) : QC;   // (tests shrink the queues: their overflow path)
+    auto floor_of = [&](int qi, int sh) -> uint32_t {
+        const WideCold& c = s_cold;
+        return floor_lds ? s_floor[sh * kWideQ + qi] : ((!c.floors || qi >= c.q_count) ? 0u : c.floors[(size_t)qi * S + sh]);
+    };
+    __syncthreads();   // lists zeroed; s_qc, s_qnd, the floors and the quarter descriptors written
+#pragma unroll
+    for (int qb = 0; qb < NQB; ++qb)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) asm volatile("" ::"v"(bfr[s][qb]));
+
+    // ---- the quarter-end work: drain this wave's queue into its queries' lists, then flush them ----
+    auto drain_flush = [&](const WideQuarter& d) {
+        const WideCold& c = s_cold;
+        const int sh = d.shard;
+        const int n = min(s_qn[wave], qcap);
+        const uint2* q = s_q + (size_t)wave * QC;
+        for (int i0 = 0; i0 < n; i0 += 64) {
+            const bool ok = i0 + lane < n;
+            const uint2 en = ok ? q[i0 + lane] : make_uint2(0u, 0u);
+            const int qi = (int)(en.y & 255u), rowq = (int)(en.y >> 8);
+            const float* af = reinterpret_cast<const float*>(d.at + (rowq >> 4) * kAuxGroupF4);
+            const int rr = rowq & 15;
+            uint64_t key = 0ull;
+            uint32_t lbs = 0u;
+            bool ovf = false;
+            if (ok) {
+                const float a_r = SIM == SIM_COSINE ? af[68] : af[rr];   // (COSINE: the group's s_g, slot 17)
+                const float4 ax = make_float4(a_r, af[16 + rr], af[32 + rr], af[48 + rr]);
+                const float xnd = SIM == SIM_COSINE ? af[72 + rr] : 0.0f;
+                const float qndq = s_qnd[qi];
+                float lo, hi;
+                sq8_bounds(sim, (float)(int32_t)en.x, ax, s_qc[qi], c.gam, c.g2, lo, hi);
+                const float ub = SIM == SIM_EUCLIDEAN ? score_f32_l2(lo) : score_f32(sim, hi, qndq, xnd);
+                const float lb = SIM == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qndq, xnd);
+                const uint64_t kr = make_key(ub, d.vrow0 + (uint32_t)rowq);
+                const uint64_t tk = (uint64_t)floor_of(qi, sh) << 32;
+                if (kr > tk) {   // below the floor: cannot enter the top k
+                    const int pos = atomicAdd(&s_cnt[qi], 1);
+                    if (pos < kKQ - 1) {
+                        s_lk[qi * kKQ + pos] = kr;
+                        s_lp[qi * kKQ + pos] = float_to_sortable(lb);
+                    } else {
+                        key = kr;
+                        lbs = float_to_sortable(lb);
+                        ovf = true;
+                    }
+                }
+            }
+            uint64_t om = __ballot(ovf);
+            while (om) {   // the overflowed queries, one at a time: sq8_wide's ordered insertion
+                const int Q = __builtin_amdgcn_readlane(qi, (int)__builtin_ctzll(om));
+                const int o0 = Q * kKQ;
+                uint64_t lkb = lane < kKQ ? s_lk[o0 + lane] : 0ull;
+                uint32_t lpb = lane < kKQ ? s_lp[o0 + lane] : 0u;
+                if (s_cnt[Q] < kWideSorted) {   // first overflow: sort the appended rows (zeros last)
+                    int rank = 0;
+#pragma unroll 2
+                    for (int j = 0; j < kKQ; ++j) {
+                        const uint64_t kj = s_lk[o0 + j];
+                        rank += (kj > lkb) || (kj == lkb && j < lane);
+                    }
+                    if (lane < kKQ) {
+                        s_lk[o0 + rank] = lkb;
+                        s_lp[o0 + rank] = lpb;
+                    }
+                    lkb = lane < kKQ ? s_lk[o0 + lane] : 0ull;
+                    lpb = lane < kKQ ? s_lp[o0 + lane] : 0u;
+                }
+                uint64_t thrb = readlane64(lkb, kKQ - 1);
+                wave_offer2(key, lbs, ovf && qi == Q, lkb, lpb, thrb, lane, kKQ);
+                if (lane < kKQ) {
+                    s_lk[o0 + lane] = lkb;
+                    s_lp[o0 + lane] = lpb;
+                }
+                if (lane == 0) s_cnt[Q] = kWideSorted;
+                om = __ballot(ovf && qi != Q);
+                ovf = ovf && qi != Q;
+            }
+        }
+        // flush: this wave's queries, 4 per pass of 16 lanes → the settle's arrays, zeroed.  A query whose queue
+        // entries were dropped (s_ovf) gets a 16th key above every threshold: the settle re-scans the quarter
+        // exactly for it (its list maximum at least score 0, so the settle does not skip the list)
+        const int q_end = min(wq0 + 32, c.q_count);
+        for (int q0 = wq0; q0 < q_end; q0 += 4) {
+            const int qg = q0 + (lane >> 4), e = lane & 15;
+            uint64_t lkb = s_lk[qg * kKQ + e];
+            const uint32_t lpb = s_lp[qg * kKQ + e];
+            const bool dropped = s_ovf[qg] != 0;
+            if (dropped && e == kKQ - 1) lkb = 0xFFFFFFFF00000000ull;
+            uint32_t m = (lkb && lkb != 0xFFFFFFFF00000000ull) ? lpb : 0u;
+#pragma unroll
+            for (int o = 8; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+            if (dropped) m = max(m, 0x80000000u);   // (sortable score 0: a lower bound of any row)
+            if (qg < q_end) {
+                const size_t l = (size_t)(c.q0 + qg) * c.n_lists + d.list;
+                c.cand[l * kKQ + e] = lkb;
+                c.cand_lb[l * kKQ + e] = lpb;
+                if (e == 0) c.list_lbmax[l] = m;
+                s_lk[qg * kKQ + e] = 0ull;
+                s_lp[qg * kKQ + e] = 0u;
+                if (e == 0) {
+                    s_cnt[qg] = 0;
+                    s_ovf[qg] = 0;
+                }
+            }
+        }
+        if (lane == 0) s_qn[wave] = 0;
+        if (c.visited && c.q0 == 0 && tid == 0 && d.nrows > 0)
+            atomicAdd(&c.visited[d.seg], (unsigned long long)d.nrows);
+    };
+    // ---- a quarter starts: its quick-test constants for every query, each wave its own 32 (lanes 0..31) ----
+    auto begin_quarter = [&](const WideQuarter& d) {
+        if (lane < 32) {
+            const int oq = wq0 + lane;
+            float ca, cb = 0.0f;
+            if (oq < s_cold.q_count) {
+                const float4 qc = s_qc[oq];   // sq8_wide's per-query coefficients, exactly
+                const float sb = qc.x;
+                const float inv = qc.x > 0.0f ? (SIM == SIM_EUCLIDEAN ? 0.5f : 1.0f) / qc.x : 0.0f;
+                const float zq = qc.x > 0.0f ? qc.z / qc.x * (1.0f + 0x1p-20f) : 0.0f;
+                float QY, QZ, Q0;
+                if constexpr (SIM == SIM_EUCLIDEAN) {
+                    const double m = 0x1p-17;
+                    QY = __double2float_ru((2.0 + 2.0 * m) * (double)qc.y + 2.0 * m * (double)qc.z);
+                    QZ = __double2float_ru((2.0 + 2.0 * m) * (double)qc.z);
+                    Q0 = __double2float_rd((double)qc.w * (1.0 - m));
+                } else {
+                    const double r = 1.0 + 0x1p-18;
+                    QY = __double2float_ru(((double)qc.y + 0x1p-18 * (double)qc.z) * r);
+                    QZ = __double2float_ru((double)qc.z * r);
+                    Q0 = __double2float_ru((double)s_cold.gam * (double)qc.w * r);
+                }
+                const float QW = __double2float_ru((double)s_cold.gam * (1.0 + 0x1p-18));
+                const float ig2m = 1.0f / (1.0f - s_cold.g2);
+                const uint64_t tkey = (uint64_t)floor_of(oq, d.shard) << 32;
+                const float tq = sq8_quick(sim, tkey, SIM == SIM_COSINE ? sqrtf(s_qnd[oq]) : 0.0f, s_cold.cos_slack);
+                quick_consts<SIM>(tq, sb, inv, QY, QZ, Q0, QW, zq, ig2m, d.bm, ca, cb);
+            } else if (SIM == SIM_EUCLIDEAN) {   // (no query: no pair passes)
+                ca = 0.0f;
+                cb = __builtin_inff();
+            } else {
+                ca = __builtin_inff();
+            }
+            s_ca[(oq & 15) * 16 + (oq >> 4)] = ca;
+            if (SIM == SIM_EUCLIDEAN) s_cb[(oq & 15) * 16 + (oq >> 4)] = cb;
+        }
+    };
+    // empty quarters take no group, but the settle and the floors read every (query, quarter) slot
+    for (int q = 0; q < n_mine; ++q)
+        if (__builtin_amdgcn_readfirstlane(s_quart[q].nrows) <= 0) drain_flush(s_quart[q]);   // (all empty here)
+
+#ifdef OSK_TESTING
+    uint32_t n_events = 0, n_pairs = 0, n_slow = 0;
+#endif
+    // ---- the wave's items: per nonempty quarter, groups wave, wave + 8, … (a wave with none gets one phantom
+    // item there, so it still takes part in the quarter's barriers) ----
+    auto groups_of = [&](int q) { return __builtin_amdgcn_readfirstlane((s_quart[q].nrows + 15) >> 4); };
+    auto next_q = [&](int q) {   // the next nonempty quarter after q (n_mine: none)
+        do ++q; while (q < n_mine && groups_of(q) == 0);
+        return q;
+    };
+    int q_last = -1;
+    for (int q = 0; q < n_mine; ++q)
+        if (groups_of(q) > 0) q_last = q;
+    if (q_last < 0) return;   // (every wave alike: no nonempty quarter, no barrier follows)
+    int iq = next_q(-1), ig = wave;   // the next item to load
+    // one item's loads (unconditional: past the stream's end the last quarter's first group, so every item issues
+    // the same loads and the compiler's vmcnt waits stay exact)
+    auto load_item = [&](RowsItem<SIM>& it) {
+        const int q = iq < n_mine ? iq : q_last;
+        const int g = (iq < n_mine && ig < groups_of(q)) ? ig : 0;   // (a phantom item or past the end: group 0)
+        const int4* xg = reinterpret_cast<const int4*>(rfl_ptr_c(s_quart[q].xt)) + (size_t)g * 128;
+        const float4* ag = reinterpret_cast<const float4*>(rfl_ptr_c(s_quart[q].at)) + (size_t)g * kAuxGroupF4;
+        it.a0 = load_i4_g(xg + lane, true);
+        it.a1 = load_i4_g(xg + 64 + lane, true);
+        it.x = load_f4_g(ag + 17);                                 // {s_g, f_cos, zero-row flag, 0}
+        if constexpr (SIM == SIM_EUCLIDEAN) it.w = load_f4_g(ag + 12 + grp);   // w_r = |x|² of the lane's 4 rows
+        if (iq < n_mine) {   // advance the load cursor: groups wave, wave + 8, …, then the next quarter
+            ig += kWideWaves;
+            if (ig >= groups_of(iq)) {
+                iq = next_q(iq);
+                ig = wave;
+            }
+        }
+    };
+    // ... and one item's work
+    int pq = next_q(-1), pg = wave, cur = -1;
+    auto process = [&](const RowsItem<SIM>& it) {
+        if (pq != cur) {   // the quarter changes: the last one's drain + flush, the new one's constants
+            __syncthreads();
+            if (cur >= 0) drain_flush(s_quart[cur]);
+            begin_quarter(s_quart[pq]);
+            __syncthreads();
+            cur = pq;
+        }
+        const int ng = groups_of(pq);
+        const int g = pg;
+        if (g < ng && !(ablate & 1)) {
+            const int r0 = 16 * g, nr = min(16, __builtin_amdgcn_readfirstlane(s_quart[pq].nrows) - r0);
+            // the group's factor: DOT / MIP / EUCLIDEAN s_g (every valid row's a_r: one scale per group), COSINE f_cos
+            const float f = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(SIM == SIM_COSINE ? it.x.y : it.x.x)));
+            bool zg = false;
+            if constexpr (SIM == SIM_COSINE) zg = __builtin_amdgcn_readfirstlane(__float_as_int(it.x.z)) != 0;
+            // EUCLIDEAN: the smallest |x|² of the lane's rows (ca > 0: the per-row threshold w_r·ca + cb is smallest there)
+            const float wmin = SIM == SIM_EUCLIDEAN ? fminf(fminf(it.w.x, it.w.y), fminf(it.w.z, it.w.w)) : 0.0f;
+            const i32x4 A0 = i32x4{it.a0.x, it.a0.y, it.a0.z, it.a0.w}, A1 = i32x4{it.a1.x, it.a1.y, it.a1.z, it.a1.w};
+#pragma unroll
+            for (int h = 0; h < NQB / PB; ++h) {
+                i32x4 acc[PB];
+                if (!(ablate & 2)) {
+#pragma unroll
+                    for (int j = 0; j < PB; ++j)
+                        acc[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0, bfr[0][h * PB + j], i32x4{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+                    for (int j = 0; j < PB; ++j)
+                        acc[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1, bfr[1][h * PB + j], acc[j], 0, 0, 0);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < PB; ++j) acc[j] = (A0 ^ bfr[0][h * PB + j]) + (A1 ^ bfr[1][h * PB + j]);
+                }
+                const float4 cq = *reinterpret_cast<const float4*>(s_ca + col * 16 + h * PB);
+                const float cav[PB] = {cq.x, cq.y, cq.z, cq.w};
+                float cbv[PB] = {0.f, 0.f, 0.f, 0.f};
+                if constexpr (SIM == SIM_EUCLIDEAN) {
+                    const float4 bq = *reinterpret_cast<const float4*>(s_cb + col * 16 + h * PB);
+                    cbv[0] = bq.x, cbv[1] = bq.y, cbv[2] = bq.z, cbv[3] = bq.w;
+                }
+                // the fast test: per block the lane's largest dot against the group's common factor (DOT / MIP:
+                // s_g; COSINE: f_cos, a c ≤ 0 lets every pair through, as does a zero row) — sq8_wide's test.
+                // EUCLIDEAN: the per-row test I·s_g ≥ w_r·ca + cb (quick_consts) relaxed to the lane's smallest w_r
+                // (ca > 0), so t = fma(max I, s_g, −(wmin·ca + cb)) < 0 implies every row of the lane fails
+                float tf[PB];
+#pragma unroll
+                for (int j = 0; j < PB; ++j) {
+                    const i32x4& I = acc[j];
+                    const int M = max(max(I[0], I[1]), max(I[2], I[3]));
+                    float c = cav[j];
+                    if constexpr (SIM == SIM_COSINE) c = !(cav[j] > 0.0f) ? -__builtin_inff() : cav[j];
+                    if constexpr (SIM == SIM_EUCLIDEAN) c = fmaf(wmin, cav[j], cbv[j]);
+                    tf[j] = fmaf((float)M, f, -c);
+                }
+                float run = -__builtin_inff();
+#pragma unroll
+                for (int j = 0; j < PB; ++j) run = fmaxf(run, tf[j]);
+                if (!__ballot(!(run < 0.0f)) && !zg) continue;
+#ifdef OSK_TESTING
+                ++n_slow;
+#endif
+                // the slow path: per passing block the per-row test, then the passing pairs → the owner's queue
+                float4 arow = make_float4(f, f, f, f);   // the rows' factors (COSINE: per row, slot grp)
+                if constexpr (SIM == SIM_COSINE)
+                    arow = load_f4_g(reinterpret_cast<const float4*>(rfl_ptr_c(s_quart[pq].at)) + (size_t)g * kAuxGroupF4 + grp);
+#pragma unroll
+                for (int j = 0; j < PB; ++j) {
+                    const int qb = h * PB + j;
+                    if (!__ballot(!(tf[j] < 0.0f) || zg)) continue;   // (invalid queries never pass: their c)
+#ifdef OSK_TESTING
+                    ++n_events;
+#endif
+                    const int qi = qb * 16 + col;
+                    const bool qv = qi < s_cold.q_count;
+                    bool pass[4];
+                    if constexpr (SIM == SIM_EUCLIDEAN) {   // the per-row test: t_r = fma(I, s_g, −fma(w_r, ca, cb))
+                        const float wr[4] = {it.w.x, it.w.y, it.w.z, it.w.w};
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            pass[r] = !(fmaf((float)acc[j][r], f, -fmaf(wr[r], cav[j], cbv[j])) < 0.0f);
+                    } else {
+                        const float ar[4] = {arow.x, arow.y, arow.z, arow.w};
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) pass[r] = !(fmaf((float)acc[j][r], ar[r], -cav[j]) < 0.0f);
+                    }
+                    bool pr[4];
+                    uint64_t b[4];
+                    int tot = 0;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        pr[r] = pass[r] && 4 * grp + r < nr && qv;
+                        b[r] = __ballot(pr[r]);
+                        tot += __popcll(b[r]);
+                    }
+                    if (!tot) continue;
+                    const int owner = qb >> 1;   // (queries qb·16 … qb·16 + 15 belong to wave qb / 2)
+                    int base = 0;
+                    if (lane == 0) base = atomicAdd(&s_qn[owner], tot);
+                    base = __builtin_amdgcn_readfirstlane(base);
+                    uint2* oq_ = s_q + (size_t)owner * QC;
+                    bool dropped = false;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(b[r] >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)b[r], 0u));
+                        const int slot = base + below;
+                        if (pr[r]) {
+                            if (slot < qcap)
+                                oq_[slot] = make_uint2((uint32_t)acc[j][r], (uint32_t)(r0 + 4 * grp + r) << 8 | (uint32_t)qi);
+                            else
+                                dropped = true;
+                        }
+                        base += __popcll(b[r]);
+                    }
+                    if (dropped) s_ovf[qi] = 1;
+#ifdef OSK_TESTING
+                    n_pairs += tot;
+#endif
+                }
+            }
+        }
+        // advance the work cursor (the load cursor's rule)
+        pg += kWideWaves;
+        if (pg >= ng) {
+            pq = next_q(pq);
+            pg = wave;
+        }
+    };
+    RowsItem<SIM> slot[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) load_item(slot[d]);
+    while (pq < n_mine) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            if (pq < n_mine) {
+                process(slot[d]);
+                load_item(slot[d]);
+            }
+        }
+    }
+    // the last quarter's drain and flush
+    __syncthreads();
+    if (cur >= 0) drain_flush(s_quart[cur]);
+#ifdef OSK_TESTING
+    if (p.counters) {
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) n_pairs += __shfl_xor(n_pairs, o);
+        if (lane == 0) {
+            atomicAdd(&p.counters[4], (unsigned long long)n_events);
+            atomicAdd(&p.counters[5], (unsigned long long)n_pairs);
+            atomicAdd(&p.counters[7], (unsigned long long)n_slow);
+        }
+    }
+#endif
+}
+
 using WideFn = void (*)(Sq8Params);
 #define OSK_WIDE_SIMS(KS) {sq8_wide<KS, 0>, sq8_wide<KS, 1>, sq8_wide<KS, 2>, sq8_wide<KS, 3>}
 static const WideFn kWide[4][4] = {OSK_WIDE_SIMS(2), OSK_WIDE_SIMS(4), OSK_WIDE_SIMS(8), OSK_WIDE_SIMS(12)};
@@ -1204,6 +1675,34 @@ static size_t sq8_wide_lds(int ks, int sim, int n_shards, int n_mine) {
                       : ks == 8 ? wide_ring_bytes<8>(sim) : wide_ring_bytes<12>(sim);
     return ring + (size_t)kWideQ * kKQ * 12 + (size_t)kWideQ * 16 + (size_t)kWideQ * 4 +
            (n_shards <= kWideMaxFloorShards ? (size_t)n_shards * kWideQ * 4 : 0) + (size_t)n_mine * sizeof(WideQuarter);
+}
+
+using RowsFn = void (*)(Sq8Params);
+static const RowsFn kWideRows[4] = {sq8_wide_rows<0>, sq8_wide_rows<1>, sq8_wide_rows<2>, sq8_wide_rows<3>};
+// (dynamic LDS only: the quarter descriptors and the floors; the rest is static, kRowsStatic bytes)
+static size_t sq8_wide_rows_lds(int n_shards, int n_mine) {
+    return (size_t)n_mine * sizeof(WideQuarter) + (n_shards <= kWideMaxFloorShards ? (size_t)n_shards * kWideQ * 4 : 0);
+}
+static constexpr size_t kRowsStatic = (size_t)kWideQ * kKQ * 12 + (size_t)kWideQ * 16 +
+                                      (size_t)kWideWaves * kRowsQC * sizeof(uint2) + (size_t)kWideQ * 4 * 5 + 16 * 4 + 128;
+bool sq8_wide_rows_supported(int u8) { return sq8_wide_supported(u8) && sq8_wide_ks(u8) == 2; }
+
+hipError_t launch_sq8_wide_rows(const Sq8Params& p, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
+    if (!sq8_wide_rows_supported(p.units8) || p.q_count < 1 || p.q_count > kWideQ || p.accept || p.gtiles ||
+        p.sim < 0 || p.sim > 3 || !p.rows8t || !p.auxt || p.n_lists != 4 * p.n_tiles || p.k < 1 || p.k > kKQ ||
+        p.n_shards < 1 || p.wide_grid < 1 || p.pilot || !p.quarter_bm)
+        return hipErrorInvalidValue;
+    const int nq4 = (p.quarter_end > 0 ? p.quarter_end : 4 * p.n_tiles) - p.quarter_begin;
+    if (p.quarter_begin < 0 || nq4 < 1 || p.quarter_begin + nq4 > 4 * p.n_tiles) return hipErrorInvalidValue;
+    int grid = std::min(p.wide_grid, std::max(1, nq4));
+    while (sq8_wide_rows_lds(p.n_shards, (nq4 + grid - 1) / grid) + kRowsStatic > 160 * 1024) grid *= 2;
+    const size_t lds = sq8_wide_rows_lds(p.n_shards, (nq4 + grid - 1) / grid);
+    const auto fn = kWideRows[p.sim];
+    if (ev_start || ev_stop)
+        hipExtLaunchKernelGGL(fn, dim3(grid), dim3(kWideThreads), lds, s, ev_start, ev_stop, 0, p);
+    else
+        hipLaunchKernelGGL(fn, dim3(grid), dim3(kWideThreads), lds, s, p);
+    return hipGetLastError();
 }
 
 hipError_t launch_sq8_wide(const Sq8Params& p, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
@@ -1239,6 +1738,9 @@ hipError_t launch_sq8_wide(const Sq8Params& p, hipStream_t s, hipEvent_t ev_star
 // N = 1, 2, 4 DMAs at both strides the kernel uses (1 KiB slabs, kAuxGroupF4 bound-term groups), each DMA k
 // reads gbase + lane·16 + k·GS and must land at ldsk[k] + lane·16 — the destinations here are out of order and
 // not GS apart — with every other LDS byte untouched.  One 64-lane workgroup; out: 6 images of the 16 KiB LDS.
+// (Every destination is ≥ k·GS above the LDS base: glds16_run's precondition.  The first version of this probe
+// put them in reverse order from offset 512, so M0 = ldsk[k] − k·GS went below 0 for three of its DMAs, and
+// exactly those three (192 words) did not land: M0 does not wrap.)
 template <int N, int GS>
 __device__ void glds_probe_case(const int4* src, int4* lds, int4* out) {
     for (int i = threadIdx.x; i < 1024; i += 64) lds[i] = make_int4(-1, -1, -1, -1);
@@ -1246,7 +1748,7 @@ __device__ void glds_probe_case(const int4* src, int4* lds, int4* out) {
     const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(__attribute__((address_space(3))) char*)lds);
     uint32_t ldsk[N];
 #pragma unroll
-    for (int k = 0; k < N; ++k) ldsk[k] = base + (uint32_t)((N - 1 - k) * 2048 + 512);
+    for (int k = 0; k < N; ++k) ldsk[k] = base + (uint32_t)(3072 + (N - 1 - k) * 2048 + 512);
     glds16_run<N, GS>(src, (uint32_t)threadIdx.x * 16u, ldsk);
     vm_wait<0>();
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");

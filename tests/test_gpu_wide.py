@@ -314,3 +314,32 @@ def test_wide_copy_is_built_only_when_a_batch_takes_the_wide_kernel():
         assert_same(wide, narrow)
     finally:
         close_all(ds, readers)
+
+
+@pytest.mark.parametrize("qcap", [0, 1, 8])
+@pytest.mark.parametrize("sim", SIMS, ids=lambda s: s.name)
+def test_wide_rows_kernel_equals_the_ring_kernel(sim, qcap):
+    """≤ 128 dims run the main passes on sq8_wide_rows (rows owned by waves, no step barrier, insertions queued
+    to the query's owner wave).  Its results equal sq8_wide's (tune sq8_wide_rows 0), the fp32 scan and
+    sq8_mfma; with the queues shrunk to 1 or 8 entries (sq8_wide_rows_qcap) most entries are dropped and their
+    (quarter, query) lists marked for the settle's exact re-scan — results still equal, bit for bit."""
+    rows_list = [corpus(n, 96, sim, 80 + i) for i, n in enumerate([23001, 1, 7000, 16])]
+    shard_of, shard_index = [0, 0, 1, 2], [1, 2, 0]
+    queries = corpus(300, 96, sim, 90)
+    queries[7] = 0.0
+    ds, readers = view_of(rows_list, sim, shard_of, shard_index)
+    try:
+        _lib.tune("sq8_wide_rows_qcap", qcap)
+        try:
+            rows = three_ways(ds, queries, 10)
+        finally:
+            _lib.tune("sq8_wide_rows_qcap", 0)
+        ring = tuned("sq8_wide_rows", 0, 1, lambda: ds.search(queries, 10, 0, 10))
+        assert_same(rows, ring)
+        for i in (0, 7, 299):
+            es, ed, esh, _, _ = oracle_merge(rows_list, shard_of, shard_index, queries[i], 10, sim)
+            s, d, sh, c, _, _ = rows
+            assert np.array_equal(d[i, :c[i]], ed) and np.array_equal(sh[i, :c[i]], esh)
+            assert np.array_equal(bits(s[i, :c[i]]), bits(es))
+    finally:
+        close_all(ds, readers)
