@@ -38,7 +38,12 @@ OSK_HD float sortable_to_float(uint32_t u) {
     __builtin_memcpy(&s, &b, 4);
     return s;
 }
+// A NaN score is never a hit: [L] exactSearch collects a doc only when `score > topDoc.score` (the HitQueue
+// starts full of −∞ sentinels), false for NaN — a COSINE zero vector (query or row) scores NaN and is visited but
+// never collected.  Its key is the empty slot; the same holds for a NaN bound (COSINE: NaN exactly when the exact
+// score is), so such a row is never a candidate either.
 OSK_HD uint64_t make_key(float score, uint32_t doc) {
+    if (score != score) return 0ull;
     return ((uint64_t)float_to_sortable(score) << 32) | (uint64_t)(0xFFFFFFFFu - doc);
 }
 OSK_HD float key_score(uint64_t key) { return sortable_to_float((uint32_t)(key >> 32)); }
