@@ -261,9 +261,12 @@ __global__ __launch_bounds__(kSelThreads) void sel_bounds(SelParams p) {
                 lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qnd, xnd);
             }
             nvis += __popcll(__ballot(t == 0 && valid[u]));
-            // every real score is ≥ 0, whose sortable form is ≥ 2^31: 0 = no row
-            lbv[u] = valid[u] ? float_to_sortable(lb) : 0u;
-            ubv[u] = valid[u] ? float_to_sortable(ub) : 0u;
+            // every real score is ≥ 0, whose sortable form is ≥ 2^31: 0 = no row.  A NaN bound (COSINE with a zero
+            // query or row: its exact score is NaN too) is no row either — a NaN is never a hit (make_key), and
+            // the select must not count it among the k it keeps
+            const bool cand = valid[u] && lb == lb && ub == ub;
+            lbv[u] = cand ? float_to_sortable(lb) : 0u;
+            ubv[u] = cand ? float_to_sortable(ub) : 0u;
         }
         // the iteration's U·R rows are contiguous (r0 + u·R + g): lane j < U·R gathers row r0 + j's values
         // from the lane holding them (t = 0 of group g = j mod R) and the wave stores them as one
@@ -520,6 +523,14 @@ __device__ __forceinline__ void bitonic_desc(uint64_t* sk, int np, int tid) {
     __syncthreads();
 }
 
+// The hits of a sorted (descending, zeros last) list of kk keys: its non-zero prefix.  (Candidate keys are
+// distinct and non-zero — a NaN score is no candidate, make_key — so this is kk; counted, never assumed.)
+__device__ __forceinline__ void sel_count_hits(const uint64_t* sk, int kk, int tid, int32_t* out) {
+    if (tid == 0 && (kk == 0 || sk[0] == 0ull)) *out = 0;
+    for (int i = tid; i < kk; i += 1024)
+        if (sk[i] != 0ull && (i + 1 == kk || sk[i + 1] == 0ull)) *out = i + 1;
+}
+
 // per shard: the top k of its n candidate keys (distinct), sorted best first.  Few candidates
 // (n ≤ 2k + 256, in LDS): one bitonic sort.  Otherwise: a radix select (8-bit digits, LDS histogram)
 // of the kk-th largest key over the candidates (in LDS when n ≤ kSelCap, else in global memory), the
@@ -589,7 +600,7 @@ __global__ __launch_bounds__(1024) void sel_sort(SelParams p) {
         for (int i = n + tid; i < np; i += 1024) sk[i] = 0ull;
         bitonic_desc(sk, np, tid);
         for (int i = tid; i < p.k; i += 1024) ok[i] = i < kk ? sk[i] : 0ull;
-        if (tid == 0) p.out_counts[s] = kk;
+        sel_count_hits(sk, kk, tid, p.out_counts + s);
         return;
     }
     const uint64_t* src = dst;
@@ -636,15 +647,19 @@ __global__ __launch_bounds__(1024) void sel_sort(SelParams p) {
     const uint64_t kth = s_prefix;   // the kk-th largest key: exactly kk keys are ≥ it
     for (int i = tid; i < n; i += 1024) {
         const uint64_t key = src[i];
-        if (key >= kth) ok[atomicAdd(&s_ctr, 1)] = key;
+        if (key >= kth && key != 0ull) {   // (keys are distinct but for empty ones: never more than kk survive)
+            const int pos = atomicAdd(&s_ctr, 1);
+            if (pos < kk) ok[pos] = key;
+        }
     }
     __syncthreads();
+    const int ns = min(s_ctr, kk);
     int np = 2;
     while (np < kk) np <<= 1;
-    for (int i = tid; i < np; i += 1024) sk[i] = i < kk ? ok[i] : 0ull;
+    for (int i = tid; i < np; i += 1024) sk[i] = i < ns ? ok[i] : 0ull;
     bitonic_desc(sk, np, tid);
     for (int i = tid; i < p.k; i += 1024) ok[i] = i < kk ? sk[i] : 0ull;
-    if (tid == 0) p.out_counts[s] = kk;
+    sel_count_hits(sk, kk, tid, p.out_counts + s);
 }
 
 // ---- coordinator merge of large lists ----------------------------------------------------------
