@@ -1197,8 +1197,10 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
 // of wave 0's loop).  Here the roles are transposed: each wave owns ROWS — 16-row group g of a quarter goes
 // to wave g mod 8 — and multiplies them against ALL 256 queries, whose B fragments it keeps in VGPRs for the
 // launch (2 slabs × 16 query blocks × 4 = 128 VGPRs, which is why only KS = 2 takes this kernel).  A wave
-// loads its own groups straight into VGPRs (the tiled copy is lane-linear: a 1 KiB slab IS the A operand),
-// kRowsD groups ahead, and never waits for another wave inside a quarter.
+// streams its own groups through its own LDS-DMA ring (kRowsNR groups deep: ≈ 68 KB in flight per CU, what
+// HBM needs under load — a first version loaded 2 groups ahead into VGPRs, 34 KB per CU, and streamed at
+// 3 TB/s) and reads them back as the A operand (the tiled copy is lane-linear: a 1 KiB slab IS the operand);
+// it waits only on its own DMAs, never for another wave inside a quarter.
 //   * the quick test per (group, query block) is sq8_wide's fast test (quick_consts: relaxed to the quarter's
 //     row maxima), its per-(query, quarter) constants in an LDS table computed once per quarter;
 //   * a passing (group, query block) runs the per-row test and appends each passing pair {int32 dot,
@@ -1210,9 +1212,10 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
 //     their (quarter, query) lists for an exact re-scan by the settle (16th key above every threshold).
 // Same lists, floors and settle contract as sq8_wide, so results are bit-identical (tests/test_gpu_wide.py).
 // ------------------------------------------------------------------------------------------------
-constexpr int kRowsQC = 1024;   // deferred entries per owner wave and quarter
-constexpr int kRowsD = 2;       // groups in flight per wave (loads issued kRowsD groups ahead)
+constexpr int kRowsNR = 4;      // groups in flight per wave: its LDS-DMA ring's slots
 constexpr int kRowsQB = 4;      // query blocks per accumulator pass (4 passes of 4 over the 16 blocks)
+constexpr int kRowsSlot = 2048 + 5 * 16;   // a ring slot: the group's 2 slabs, then 5 bound-term float4 (rows_issue)
+constexpr int kRowsMaxFloorShards = 8;     // (per-(shard, query) floors in LDS up to this many shards)
 
 // a pointer every lane of the wave holds alike (read from LDS), as SGPRs
 __device__ __forceinline__ const char* rfl_ptr_c(const void* ptr) {
@@ -1221,19 +1224,10 @@ __device__ __forceinline__ const char* rfl_ptr_c(const void* ptr) {
                          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v));
 }
 
-// One group's loads: its two 1 KiB slabs (the A operand) and the bound terms its fast test reads — slot 17
-// {s_g, f_cos, zero-row flag, 0} (x); EUCLIDEAN also the lane's 4 rows' |x|² (w).
-template <int SIM>
-struct RowsItem {
-    int4 a0, a1;
-    float4 x;
-    float4 w;   // (EUCLIDEAN only)
-};
-
 template <int SIM>
 __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     typedef int i32x4 __attribute__((ext_vector_type(4)));
-    constexpr int NQB = kWideQ / 16, QC = kRowsQC, D = kRowsD, PB = kRowsQB;
+    constexpr int NQB = kWideQ / 16, NR = kRowsNR, PB = kRowsQB;
     constexpr int sim = SIM;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int col = lane & 15, grp = lane >> 4;
@@ -1246,24 +1240,27 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     const int G = gridDim.x, n_quarters = 4 * p.n_tiles;
     const int qbeg = p.quarter_begin, n_range = (p.quarter_end > 0 ? p.quarter_end : n_quarters) - qbeg;
     const int n_mine = (int)blockIdx.x < n_range ? (n_range - 1 - (int)blockIdx.x) / G + 1 : 0;
-    const bool floor_lds = S <= kWideMaxFloorShards;
+    const bool floor_lds = S <= kRowsMaxFloorShards;
+    const int qcap = p.wide_qcap;   // deferred entries per owner wave (launch_sq8_wide_rows: what LDS leaves; tests less)
 
     // (the fixed-size arrays are static LDS: their addresses are constants, so the hot loop's LDS accesses take
-    // immediate offsets instead of address registers)
+    // immediate offsets instead of address registers; the rings, queues, quarter descriptors and floors are the
+    // dynamic part)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ WideCold s_cold;
     __shared__ uint64_t s_lk[kWideQ * kKQ];                // [kWideQ][kKQ] upper-bound keys
     __shared__ uint32_t s_lp[kWideQ * kKQ];                // their lower bounds
     __shared__ __attribute__((aligned(16))) float4 s_qc[kWideQ];   // query bound terms
-    __shared__ uint2 s_q[kWideWaves * QC];                 // [8 owners][QC] deferred entries
     __shared__ __attribute__((aligned(16))) float s_ca[kWideQ];    // [16 col][16 qb] quick-test constants
     __shared__ __attribute__((aligned(16))) float s_cb[kWideQ];    // (EUCLIDEAN's second constant)
     __shared__ float s_qnd[kWideQ];                        // |q|² device order (COSINE)
     __shared__ int32_t s_cnt[kWideQ];                      // list fill
     __shared__ int32_t s_ovf[kWideQ];                      // queue overflowed this quarter
     __shared__ int32_t s_qn[16];                           // [8] queue fill per owner
-    WideQuarter* s_quart = reinterpret_cast<WideQuarter*>(smem);                // [n_mine]
-    uint32_t* s_floor = reinterpret_cast<uint32_t*>(s_quart + n_mine);         // [S][kWideQ] floors (S ≤ 16)
+    char* s_ring = smem;                                                                   // [8 waves][NR] slots
+    WideQuarter* s_quart = reinterpret_cast<WideQuarter*>(smem + kWideWaves * NR * kRowsSlot);   // [n_mine]
+    uint2* s_q = reinterpret_cast<uint2*>(s_quart + n_mine);                             // [8 owners][qcap]
+    uint32_t* s_floor = reinterpret_cast<uint32_t*>(s_q + kWideWaves * qcap);           // [S][kWideQ] (S ≤ 8)
     if (tid == 0) s_cold = WideCold{p.cand, p.cand_lb, p.list_lbmax, p.visited, p.qn_dev, p.pilot_keys, p.floors, p.q0,
                                     p.n_lists, p.q_count, 4 * p.n_tiles, p.cos_slack, p.gam, p.g2};
     for (int i = tid; i < kWideQ * kKQ; i += kWideThreads) {
@@ -1315,7 +1312,6 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
         }
     }
     const int wq0 = wave * 32;   // this wave owns queries wq0 … wq0 + 31 (their lists, queue and flush)
-    const int qcap = p.wide_qcap > 0 ? min(p.wide_qcap, QC) : QC;   // (tests shrink the queues: their overflow path)
     auto floor_of = [&](int qi, int sh) -> uint32_t {
         const WideCold& c = s_cold;
         return floor_lds ? s_floor[sh * kWideQ + qi] : ((!c.floors || qi >= c.q_count) ? 0u : c.floors[(size_t)qi * S + sh]);
@@ -1331,7 +1327,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
         const WideCold& c = s_cold;
         const int sh = d.shard;
         const int n = min(s_qn[wave], qcap);
-        const uint2* q = s_q + (size_t)wave * QC;
+        const uint2* q = s_q + (size_t)wave * qcap;
         for (int i0 = 0; i0 < n; i0 += 64) {
             const bool ok = i0 + lane < n;
             const uint2 en = ok ? q[i0 + lane] : make_uint2(0u, 0u);
@@ -1481,19 +1477,25 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     for (int q = 0; q < n_mine; ++q)
         if (groups_of(q) > 0) q_last = q;
     if (q_last < 0) return;   // (every wave alike: no nonempty quarter, no barrier follows)
-    int iq = next_q(-1), ig = wave;   // the next item to load
-    // one item's loads (unconditional: past the stream's end the last quarter's first group, so every item issues
-    // the same loads and the compiler's vmcnt waits stay exact)
-    auto load_item = [&](RowsItem<SIM>& it) {
+    int iq = next_q(-1), ig = wave;   // the next item to issue
+    // this wave's ring: slot d at ring_base + d·kRowsSlot (LDS byte address for the DMAs, pointer for the reads)
+    const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem + (uint32_t)(wave * NR * kRowsSlot));
+    const char* ring = s_ring + wave * NR * kRowsSlot;
+    // one item's DMAs into slot d — the two 1 KiB slabs (lane-linear: the A operand), and 5 bound-term float4:
+    // lanes 0–3 the rows' |x|² (EUCLIDEAN, slots 12–15) or per-row factors (COSINE, slots 0–3), lane 4 slot 17
+    // {s_g, f_cos, zero-row flag, 0}.  Three DMA instructions whatever the item (past the stream's end the last
+    // quarter's first group: the ring's vmcnt waits count exactly three per item).
+    auto issue = [&](int d) {
         const int q = iq < n_mine ? iq : q_last;
         const int g = (iq < n_mine && ig < groups_of(q)) ? ig : 0;   // (a phantom item or past the end: group 0)
         const int4* xg = reinterpret_cast<const int4*>(rfl_ptr_c(s_quart[q].xt)) + (size_t)g * 128;
         const float4* ag = reinterpret_cast<const float4*>(rfl_ptr_c(s_quart[q].at)) + (size_t)g * kAuxGroupF4;
-        it.a0 = load_i4_g(xg + lane, true);
-        it.a1 = load_i4_g(xg + 64 + lane, true);
-        it.x = load_f4_g(ag + 17);                                 // {s_g, f_cos, zero-row flag, 0}
-        if constexpr (SIM == SIM_EUCLIDEAN) it.w = load_f4_g(ag + 12 + grp);   // w_r = |x|² of the lane's 4 rows
-        if (iq < n_mine) {   // advance the load cursor: groups wave, wave + 8, …, then the next quarter
+        const uint32_t base = ring_lds + (uint32_t)(d * kRowsSlot);
+        glds16(xg + lane, base);
+        glds16(xg + 64 + lane, base + 1024u);
+        if (lane < 5) glds16(ag + (lane == 4 ? 17 : (SIM == SIM_EUCLIDEAN ? 12 : 0) + lane), base + 2048u);
+        if (iq < n_mine) {   // advance the issue cursor: groups wave, wave + 8, …, then the next quarter
             ig += kWideWaves;
             if (ig >= groups_of(iq)) {
                 iq = next_q(iq);
@@ -1503,7 +1505,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     };
     // ... and one item's work
     int pq = next_q(-1), pg = wave, cur = -1;
-    auto process = [&](const RowsItem<SIM>& it) {
+    auto process = [&](int d) {
         if (pq != cur) {   // the quarter changes: the last one's drain + flush, the new one's constants
             __syncthreads();
             if (cur >= 0) drain_flush(s_quart[cur]);
@@ -1515,13 +1517,17 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
         const int g = pg;
         if (g < ng && !(ablate & 1)) {
             const int r0 = 16 * g, nr = min(16, __builtin_amdgcn_readfirstlane(s_quart[pq].nrows) - r0);
+            const char* sl = ring + d * kRowsSlot;
+            const float4 g17 = *reinterpret_cast<const float4*>(sl + 2048 + 64);   // {s_g, f_cos, zero-row flag, 0}
+            const float4 xr4 = *reinterpret_cast<const float4*>(sl + 2048 + grp * 16);   // EUCLIDEAN |x|², COSINE factors
             // the group's factor: DOT / MIP / EUCLIDEAN s_g (every valid row's a_r: one scale per group), COSINE f_cos
-            const float f = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(SIM == SIM_COSINE ? it.x.y : it.x.x)));
+            const float f = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(SIM == SIM_COSINE ? g17.y : g17.x)));
             bool zg = false;
-            if constexpr (SIM == SIM_COSINE) zg = __builtin_amdgcn_readfirstlane(__float_as_int(it.x.z)) != 0;
+            if constexpr (SIM == SIM_COSINE) zg = __builtin_amdgcn_readfirstlane(__float_as_int(g17.z)) != 0;
             // EUCLIDEAN: the smallest |x|² of the lane's rows (ca > 0: the per-row threshold w_r·ca + cb is smallest there)
-            const float wmin = SIM == SIM_EUCLIDEAN ? fminf(fminf(it.w.x, it.w.y), fminf(it.w.z, it.w.w)) : 0.0f;
-            const i32x4 A0 = i32x4{it.a0.x, it.a0.y, it.a0.z, it.a0.w}, A1 = i32x4{it.a1.x, it.a1.y, it.a1.z, it.a1.w};
+            const float wmin = SIM == SIM_EUCLIDEAN ? fminf(fminf(xr4.x, xr4.y), fminf(xr4.z, xr4.w)) : 0.0f;
+            const i32x4 A0 = *reinterpret_cast<const i32x4*>(sl + lane * 16);
+            const i32x4 A1 = *reinterpret_cast<const i32x4*>(sl + 1024 + lane * 16);
 #pragma unroll
             for (int h = 0; h < NQB / PB; ++h) {
                 i32x4 acc[PB];
@@ -1565,9 +1571,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
                 ++n_slow;
 #endif
                 // the slow path: per passing block the per-row test, then the passing pairs → the owner's queue
-                float4 arow = make_float4(f, f, f, f);   // the rows' factors (COSINE: per row, slot grp)
-                if constexpr (SIM == SIM_COSINE)
-                    arow = load_f4_g(reinterpret_cast<const float4*>(rfl_ptr_c(s_quart[pq].at)) + (size_t)g * kAuxGroupF4 + grp);
+                const float4 arow = SIM == SIM_COSINE ? xr4 : make_float4(f, f, f, f);   // the rows' factors
 #pragma unroll
                 for (int j = 0; j < PB; ++j) {
                     const int qb = h * PB + j;
@@ -1579,7 +1583,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
                     const bool qv = qi < s_cold.q_count;
                     bool pass[4];
                     if constexpr (SIM == SIM_EUCLIDEAN) {   // the per-row test: t_r = fma(I, s_g, −fma(w_r, ca, cb))
-                        const float wr[4] = {it.w.x, it.w.y, it.w.z, it.w.w};
+                        const float wr[4] = {xr4.x, xr4.y, xr4.z, xr4.w};
 #pragma unroll
                         for (int r = 0; r < 4; ++r)
                             pass[r] = !(fmaf((float)acc[j][r], f, -fmaf(wr[r], cav[j], cbv[j])) < 0.0f);
@@ -1602,7 +1606,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
                     int base = 0;
                     if (lane == 0) base = atomicAdd(&s_qn[owner], tot);
                     base = __builtin_amdgcn_readfirstlane(base);
-                    uint2* oq_ = s_q + (size_t)owner * QC;
+                    uint2* oq_ = s_q + (size_t)owner * qcap;
                     bool dropped = false;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
@@ -1631,18 +1635,19 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
             pg = wave;
         }
     };
-    RowsItem<SIM> slot[D];
 #pragma unroll
-    for (int d = 0; d < D; ++d) load_item(slot[d]);
+    for (int d = 0; d < NR; ++d) issue(d);
     while (pq < n_mine) {
 #pragma unroll
-        for (int d = 0; d < D; ++d) {
+        for (int d = 0; d < NR; ++d) {
             if (pq < n_mine) {
-                process(slot[d]);
-                load_item(slot[d]);
+                vm_wait<(NR - 1) * 3>();   // slot d's three DMAs have landed (the NR − 1 younger items' may not)
+                process(d);
+                issue(d);
             }
         }
     }
+    vm_wait<0>();   // no DMA may still be landing in this workgroup's LDS when it retires
     // the last quarter's drain and flush
     __syncthreads();
     if (cur >= 0) drain_flush(s_quart[cur]);
@@ -1679,12 +1684,14 @@ static size_t sq8_wide_lds(int ks, int sim, int n_shards, int n_mine) {
 
 using RowsFn = void (*)(Sq8Params);
 static const RowsFn kWideRows[4] = {sq8_wide_rows<0>, sq8_wide_rows<1>, sq8_wide_rows<2>, sq8_wide_rows<3>};
-// (dynamic LDS only: the quarter descriptors and the floors; the rest is static, kRowsStatic bytes)
+// dynamic LDS: the rings, the quarter descriptors and the floors (+ the queues, sized from what is left); the rest
+// is static, kRowsStatic bytes
 static size_t sq8_wide_rows_lds(int n_shards, int n_mine) {
-    return (size_t)n_mine * sizeof(WideQuarter) + (n_shards <= kWideMaxFloorShards ? (size_t)n_shards * kWideQ * 4 : 0);
+    return (size_t)kWideWaves * kRowsNR * kRowsSlot + (size_t)n_mine * sizeof(WideQuarter) +
+           (n_shards <= kRowsMaxFloorShards ? (size_t)n_shards * kWideQ * 4 : 0);
 }
-static constexpr size_t kRowsStatic = (size_t)kWideQ * kKQ * 12 + (size_t)kWideQ * 16 +
-                                      (size_t)kWideWaves * kRowsQC * sizeof(uint2) + (size_t)kWideQ * 4 * 5 + 16 * 4 + 128;
+static constexpr size_t kRowsStatic = (size_t)kWideQ * kKQ * 12 + (size_t)kWideQ * 16 + (size_t)kWideQ * 4 * 5 + 16 * 4 + 128;
+static constexpr int kRowsMinQcap = 128;   // deferred entries per owner wave at least (else more workgroups)
 bool sq8_wide_rows_supported(int u8) { return sq8_wide_supported(u8) && sq8_wide_ks(u8) == 2; }
 
 hipError_t launch_sq8_wide_rows(const Sq8Params& p, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
@@ -1695,13 +1702,21 @@ hipError_t launch_sq8_wide_rows(const Sq8Params& p, hipStream_t s, hipEvent_t ev
     const int nq4 = (p.quarter_end > 0 ? p.quarter_end : 4 * p.n_tiles) - p.quarter_begin;
     if (p.quarter_begin < 0 || nq4 < 1 || p.quarter_begin + nq4 > 4 * p.n_tiles) return hipErrorInvalidValue;
     int grid = std::min(p.wide_grid, std::max(1, nq4));
-    while (sq8_wide_rows_lds(p.n_shards, (nq4 + grid - 1) / grid) + kRowsStatic > 160 * 1024) grid *= 2;
-    const size_t lds = sq8_wide_rows_lds(p.n_shards, (nq4 + grid - 1) / grid);
+    constexpr size_t cap = 160 * 1024;
+    while (sq8_wide_rows_lds(p.n_shards, (nq4 + grid - 1) / grid) + kRowsStatic +
+               (size_t)kWideWaves * kRowsMinQcap * sizeof(uint2) > cap)
+        grid *= 2;
+    size_t lds = sq8_wide_rows_lds(p.n_shards, (nq4 + grid - 1) / grid);
+    // the queues: what LDS leaves, ≤ 1024 entries per owner wave (multiples of 64); tests ask for fewer
+    Sq8Params q = p;
+    const int room = (int)std::min<size_t>(1024, (cap - lds - kRowsStatic) / (kWideWaves * sizeof(uint2)) / 64 * 64);
+    q.wide_qcap = p.wide_qcap > 0 ? std::min(p.wide_qcap, room) : room;
+    lds += (size_t)kWideWaves * q.wide_qcap * sizeof(uint2);
     const auto fn = kWideRows[p.sim];
     if (ev_start || ev_stop)
-        hipExtLaunchKernelGGL(fn, dim3(grid), dim3(kWideThreads), lds, s, ev_start, ev_stop, 0, p);
+        hipExtLaunchKernelGGL(fn, dim3(grid), dim3(kWideThreads), lds, s, ev_start, ev_stop, 0, q);
     else
-        hipLaunchKernelGGL(fn, dim3(grid), dim3(kWideThreads), lds, s, p);
+        hipLaunchKernelGGL(fn, dim3(grid), dim3(kWideThreads), lds, s, q);
     return hipGetLastError();
 }
 
