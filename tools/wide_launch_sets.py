@@ -18,7 +18,7 @@ import sys
 def dispatches(path, value=None):
     out = []
     for r in csv.DictReader(open(path)):
-        if "sq8_wide<" not in r["Kernel_Name"]:
+        if "sq8_wide<" not in r["Kernel_Name"] and "sq8_wide_rows<" not in r["Kernel_Name"]:
             continue
         if value:
             if r["Counter_Name"] != value:
