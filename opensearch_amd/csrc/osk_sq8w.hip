@@ -1505,6 +1505,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     };
     // ... and one item's work
     int pq = next_q(-1), pg = wave, cur = -1;
+    int c_ng = 0, c_nrows = 0;   // (the work quarter's groups and rows, in SGPRs: not re-read from LDS per item)
     auto process = [&](int d) {
         if (pq != cur) {   // the quarter changes: the last one's drain + flush, the new one's constants
             __syncthreads();
@@ -1512,25 +1513,37 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
             begin_quarter(s_quart[pq]);
             __syncthreads();
             cur = pq;
+            c_nrows = __builtin_amdgcn_readfirstlane(s_quart[pq].nrows);
+            c_ng = (c_nrows + 15) >> 4;
         }
-        const int ng = groups_of(pq);
         const int g = pg;
-        if (g < ng && !(ablate & 1)) {
-            const int r0 = 16 * g, nr = min(16, __builtin_amdgcn_readfirstlane(s_quart[pq].nrows) - r0);
+        if (g < c_ng && !(ablate & 1)) {
+            const int r0 = 16 * g, nr = min(16, c_nrows - r0);
+            // every LDS read of the item at once (one wait): the A operand, the group's terms, the query constants
             const char* sl = ring + d * kRowsSlot;
+            const i32x4 A0 = *reinterpret_cast<const i32x4*>(sl + lane * 16);
+            const i32x4 A1 = *reinterpret_cast<const i32x4*>(sl + 1024 + lane * 16);
             const float4 g17 = *reinterpret_cast<const float4*>(sl + 2048 + 64);   // {s_g, f_cos, zero-row flag, 0}
             const float4 xr4 = *reinterpret_cast<const float4*>(sl + 2048 + grp * 16);   // EUCLIDEAN |x|², COSINE factors
+            // the pass's query constants (PB = 4 blocks: one ds_read_b128 each)
+            auto consts = [&](int h, float (&cav)[PB], float (&cbv)[PB]) __attribute__((always_inline)) {
+                const float4 cq = *reinterpret_cast<const float4*>(s_ca + col * 16 + h * PB);
+                cav[0] = cq.x, cav[1] = cq.y, cav[2] = cq.z, cav[3] = cq.w;
+                if constexpr (SIM == SIM_EUCLIDEAN) {
+                    const float4 bq = *reinterpret_cast<const float4*>(s_cb + col * 16 + h * PB);
+                    cbv[0] = bq.x, cbv[1] = bq.y, cbv[2] = bq.z, cbv[3] = bq.w;
+                } else {
+                    cbv[0] = cbv[1] = cbv[2] = cbv[3] = 0.0f;
+                }
+            };
             // the group's factor: DOT / MIP / EUCLIDEAN s_g (every valid row's a_r: one scale per group), COSINE f_cos
             const float f = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(SIM == SIM_COSINE ? g17.y : g17.x)));
             bool zg = false;
             if constexpr (SIM == SIM_COSINE) zg = __builtin_amdgcn_readfirstlane(__float_as_int(g17.z)) != 0;
             // EUCLIDEAN: the smallest |x|² of the lane's rows (ca > 0: the per-row threshold w_r·ca + cb is smallest there)
             const float wmin = SIM == SIM_EUCLIDEAN ? fminf(fminf(xr4.x, xr4.y), fminf(xr4.z, xr4.w)) : 0.0f;
-            const i32x4 A0 = *reinterpret_cast<const i32x4*>(sl + lane * 16);
-            const i32x4 A1 = *reinterpret_cast<const i32x4*>(sl + 1024 + lane * 16);
-#pragma unroll
-            for (int h = 0; h < NQB / PB; ++h) {
-                i32x4 acc[PB];
+            // a pass of PB query blocks: their dots (2 chained MFMAs each)
+            auto dots = [&](int h, i32x4 (&acc)[PB]) __attribute__((always_inline)) {
                 if (!(ablate & 2)) {
 #pragma unroll
                     for (int j = 0; j < PB; ++j)
@@ -1542,18 +1555,15 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
 #pragma unroll
                     for (int j = 0; j < PB; ++j) acc[j] = (A0 ^ bfr[0][h * PB + j]) + (A1 ^ bfr[1][h * PB + j]);
                 }
-                const float4 cq = *reinterpret_cast<const float4*>(s_ca + col * 16 + h * PB);
-                const float cav[PB] = {cq.x, cq.y, cq.z, cq.w};
-                float cbv[PB] = {0.f, 0.f, 0.f, 0.f};
-                if constexpr (SIM == SIM_EUCLIDEAN) {
-                    const float4 bq = *reinterpret_cast<const float4*>(s_cb + col * 16 + h * PB);
-                    cbv[0] = bq.x, cbv[1] = bq.y, cbv[2] = bq.z, cbv[3] = bq.w;
-                }
-                // the fast test: per block the lane's largest dot against the group's common factor (DOT / MIP:
-                // s_g; COSINE: f_cos, a c ≤ 0 lets every pair through, as does a zero row) — sq8_wide's test.
-                // EUCLIDEAN: the per-row test I·s_g ≥ w_r·ca + cb (quick_consts) relaxed to the lane's smallest w_r
-                // (ca > 0), so t = fma(max I, s_g, −(wmin·ca + cb)) < 0 implies every row of the lane fails
-                float tf[PB];
+            };
+            // the fast test: per block the lane's largest dot against the group's common factor (DOT / MIP:
+            // s_g; COSINE: f_cos, a c ≤ 0 lets every pair through, as does a zero row) — sq8_wide's test.
+            // EUCLIDEAN: the per-row test I·s_g ≥ w_r·ca + cb (quick_consts) relaxed to the lane's smallest w_r
+            // (ca > 0), so t = fma(max I, s_g, −(wmin·ca + cb)) < 0 implies every row of the lane fails.
+            // All 16 blocks first, ONE vote per group (no branch between the passes: the next pass's MFMAs overlap
+            // this pass's tests); a passing pass recomputes its dots and tests in the slow path.
+            auto tests = [&](const i32x4 (&acc)[PB], const float (&cav)[PB], const float (&cbv)[PB], float (&tf)[PB])
+                __attribute__((always_inline)) {
 #pragma unroll
                 for (int j = 0; j < PB; ++j) {
                     const i32x4& I = acc[j];
@@ -1563,74 +1573,92 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
                     if constexpr (SIM == SIM_EUCLIDEAN) c = fmaf(wmin, cav[j], cbv[j]);
                     tf[j] = fmaf((float)M, f, -c);
                 }
-                float run = -__builtin_inff();
+            };
+            float hm[NQB / PB];   // per pass, the lane's largest test value
 #pragma unroll
-                for (int j = 0; j < PB; ++j) run = fmaxf(run, tf[j]);
-                if (!__ballot(!(run < 0.0f)) && !zg) continue;
-#ifdef OSK_TESTING
-                ++n_slow;
-#endif
+            for (int h = 0; h < NQB / PB; ++h) {
+                i32x4 acc[PB];
+                float cav[PB], cbv[PB], tf[PB];
+                consts(h, cav, cbv);
+                dots(h, acc);
+                tests(acc, cav, cbv, tf);
+                hm[h] = fmaxf(fmaxf(tf[0], tf[1]), fmaxf(tf[2], tf[3]));
+            }
+            const float run = fmaxf(fmaxf(hm[0], hm[1]), fmaxf(hm[2], hm[3]));
+            if (__ballot(!(run < 0.0f)) || zg) {
                 // the slow path: per passing block the per-row test, then the passing pairs → the owner's queue
                 const float4 arow = SIM == SIM_COSINE ? xr4 : make_float4(f, f, f, f);   // the rows' factors
 #pragma unroll
-                for (int j = 0; j < PB; ++j) {
-                    const int qb = h * PB + j;
-                    if (!__ballot(!(tf[j] < 0.0f) || zg)) continue;   // (invalid queries never pass: their c)
+                for (int h = 0; h < NQB / PB; ++h) {
+                    if (!__ballot(!(hm[h] < 0.0f)) && !zg) continue;
 #ifdef OSK_TESTING
-                    ++n_events;
+                    ++n_slow;
 #endif
-                    const int qi = qb * 16 + col;
-                    const bool qv = qi < s_cold.q_count;
-                    bool pass[4];
-                    if constexpr (SIM == SIM_EUCLIDEAN) {   // the per-row test: t_r = fma(I, s_g, −fma(w_r, ca, cb))
-                        const float wr[4] = {xr4.x, xr4.y, xr4.z, xr4.w};
+                    i32x4 acc[PB];
+                    float cav[PB], cbv[PB], tf[PB];
+                    consts(h, cav, cbv);
+                    dots(h, acc);
+                    tests(acc, cav, cbv, tf);
 #pragma unroll
-                        for (int r = 0; r < 4; ++r)
-                            pass[r] = !(fmaf((float)acc[j][r], f, -fmaf(wr[r], cav[j], cbv[j])) < 0.0f);
-                    } else {
-                        const float ar[4] = {arow.x, arow.y, arow.z, arow.w};
+                    for (int j = 0; j < PB; ++j) {
+                        const int qb = h * PB + j;
+                        if (!__ballot(!(tf[j] < 0.0f) || zg)) continue;   // (invalid queries never pass: their c)
+#ifdef OSK_TESTING
+                        ++n_events;
+#endif
+                        const int qi = qb * 16 + col;
+                        const bool qv = qi < s_cold.q_count;
+                        bool pass[4];
+                        if constexpr (SIM == SIM_EUCLIDEAN) {   // the per-row test: t_r = fma(I, s_g, −fma(w_r, ca, cb))
+                            const float wr[4] = {xr4.x, xr4.y, xr4.z, xr4.w};
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) pass[r] = !(fmaf((float)acc[j][r], ar[r], -cav[j]) < 0.0f);
-                    }
-                    bool pr[4];
-                    uint64_t b[4];
-                    int tot = 0;
+                            for (int r = 0; r < 4; ++r)
+                                pass[r] = !(fmaf((float)acc[j][r], f, -fmaf(wr[r], cav[j], cbv[j])) < 0.0f);
+                        } else {
+                            const float ar[4] = {arow.x, arow.y, arow.z, arow.w};
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        pr[r] = pass[r] && 4 * grp + r < nr && qv;
-                        b[r] = __ballot(pr[r]);
-                        tot += __popcll(b[r]);
-                    }
-                    if (!tot) continue;
-                    const int owner = qb >> 1;   // (queries qb·16 … qb·16 + 15 belong to wave qb / 2)
-                    int base = 0;
-                    if (lane == 0) base = atomicAdd(&s_qn[owner], tot);
-                    base = __builtin_amdgcn_readfirstlane(base);
-                    uint2* oq_ = s_q + (size_t)owner * qcap;
-                    bool dropped = false;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(b[r] >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)b[r], 0u));
-                        const int slot = base + below;
-                        if (pr[r]) {
-                            if (slot < qcap)
-                                oq_[slot] = make_uint2((uint32_t)acc[j][r], (uint32_t)(r0 + 4 * grp + r) << 8 | (uint32_t)qi);
-                            else
-                                dropped = true;
+                            for (int r = 0; r < 4; ++r) pass[r] = !(fmaf((float)acc[j][r], ar[r], -cav[j]) < 0.0f);
                         }
-                        base += __popcll(b[r]);
-                    }
-                    if (dropped) s_ovf[qi] = 1;
+                        bool pr[4];
+                        uint64_t b[4];
+                        int tot = 0;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            pr[r] = pass[r] && 4 * grp + r < nr && qv;
+                            b[r] = __ballot(pr[r]);
+                            tot += __popcll(b[r]);
+                        }
+                        if (!tot) continue;
+                        const int owner = qb >> 1;   // (queries qb·16 … qb·16 + 15 belong to wave qb / 2)
+                        int base = 0;
+                        if (lane == 0) base = atomicAdd(&s_qn[owner], tot);
+                        base = __builtin_amdgcn_readfirstlane(base);
+                        uint2* oq_ = s_q + (size_t)owner * qcap;
+                        bool dropped = false;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(b[r] >> 32),
+                                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)b[r], 0u));
+                            const int slot = base + below;
+                            if (pr[r]) {
+                                if (slot < qcap)
+                                    oq_[slot] = make_uint2((uint32_t)acc[j][r], (uint32_t)(r0 + 4 * grp + r) << 8 | (uint32_t)qi);
+                                else
+                                    dropped = true;
+                            }
+                            base += __popcll(b[r]);
+                        }
+                        if (dropped) s_ovf[qi] = 1;
 #ifdef OSK_TESTING
-                    n_pairs += tot;
+                        if (lane == 0) n_pairs += tot;
 #endif
+                    }
                 }
             }
         }
         // advance the work cursor (the load cursor's rule)
         pg += kWideWaves;
-        if (pg >= ng) {
+        if (pg >= c_ng) {
             pq = next_q(pq);
             pg = wave;
         }
