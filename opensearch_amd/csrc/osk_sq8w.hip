@@ -1233,7 +1233,9 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     const int col = lane & 15, grp = lane >> 4;
     const int u8 = p.units8, S = p.n_shards;
 #ifdef OSK_TESTING
-    const int ablate = p.ablate;   // A/B timing only (results wrong): 1 skip the quick tests, 2 skip the MFMAs
+    // A/B timing only (results wrong): 1 skip each group's work (streaming alone), 2 the MFMAs replaced by XORs,
+    // 4 skip the slow path, 8 MFMAs without the fast test (their results consumed by one max)
+    const int ablate = p.ablate;
 #else
     constexpr int ablate = 0;
 #endif
@@ -1579,13 +1581,19 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
             for (int h = 0; h < NQB / PB; ++h) {
                 i32x4 acc[PB];
                 float cav[PB], cbv[PB], tf[PB];
-                consts(h, cav, cbv);
                 dots(h, acc);
+                if (ablate & 8) {   // (A/B: the MFMAs alone)
+                    hm[h] = (float)max(max(acc[0][0], acc[1][1]), max(acc[2][2], acc[3][3]));
+                    continue;
+                }
+                consts(h, cav, cbv);
                 tests(acc, cav, cbv, tf);
                 hm[h] = fmaxf(fmaxf(tf[0], tf[1]), fmaxf(tf[2], tf[3]));
             }
             const float run = fmaxf(fmaxf(hm[0], hm[1]), fmaxf(hm[2], hm[3]));
-            if (__ballot(!(run < 0.0f)) || zg) {
+            if (ablate & 12) {
+                if (run == 1.2345f) s_ovf[0] = 1;   // (keeps the work)
+            } else if (__ballot(!(run < 0.0f)) || zg) {
                 // the slow path: per passing block the per-row test, then the passing pairs → the owner's queue
                 const float4 arow = SIM == SIM_COSINE ? xr4 : make_float4(f, f, f, f);   // the rows' factors
 #pragma unroll
