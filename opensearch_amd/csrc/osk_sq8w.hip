@@ -1212,7 +1212,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
 //     their (quarter, query) lists for an exact re-scan by the settle (16th key above every threshold).
 // Same lists, floors and settle contract as sq8_wide, so results are bit-identical (tests/test_gpu_wide.py).
 // ------------------------------------------------------------------------------------------------
-constexpr int kRowsNR = 4;      // groups in flight per wave: its LDS-DMA ring's slots
+constexpr int kRowsNR = 6;      // groups in flight per wave: its LDS-DMA ring's slots
 constexpr int kRowsQB = 4;      // query blocks per accumulator pass (4 passes of 4 over the 16 blocks)
 constexpr int kRowsSlot = 2048 + 5 * 16;   // a ring slot: the group's 2 slabs, then 5 bound-term float4 (rows_issue)
 constexpr int kRowsMaxFloorShards = 8;     // (per-(shard, query) floors in LDS up to this many shards)
@@ -1250,8 +1250,6 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     // dynamic part)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ WideCold s_cold;
-    __shared__ uint64_t s_lk[kWideQ * kKQ];                // [kWideQ][kKQ] upper-bound keys
-    __shared__ uint32_t s_lp[kWideQ * kKQ];                // their lower bounds
     __shared__ __attribute__((aligned(16))) float4 s_qc[kWideQ];   // query bound terms
     __shared__ __attribute__((aligned(16))) float s_ca[kWideQ];    // [16 col][16 qb] quick-test constants
     __shared__ __attribute__((aligned(16))) float s_cb[kWideQ];    // (EUCLIDEAN's second constant)
@@ -1260,15 +1258,15 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     __shared__ int32_t s_ovf[kWideQ];                      // queue overflowed this quarter
     __shared__ int32_t s_qn[16];                           // [8] queue fill per owner
     char* s_ring = smem;                                                                   // [8 waves][NR] slots
+    // the lists [kWideQ][kKQ] keys + lower bounds (48 KB) overlay the rings: they live only in the quarter-end
+    // drain and flush, when no DMA is in flight (a quarter's items are issued inside the quarter only)
+    uint64_t* s_lk = reinterpret_cast<uint64_t*>(smem);
+    uint32_t* s_lp = reinterpret_cast<uint32_t*>(s_lk + kWideQ * kKQ);
     WideQuarter* s_quart = reinterpret_cast<WideQuarter*>(smem + kWideWaves * NR * kRowsSlot);   // [n_mine]
     uint2* s_q = reinterpret_cast<uint2*>(s_quart + n_mine);                             // [8 owners][qcap]
     uint32_t* s_floor = reinterpret_cast<uint32_t*>(s_q + kWideWaves * qcap);           // [S][kWideQ] (S ≤ 8)
     if (tid == 0) s_cold = WideCold{p.cand, p.cand_lb, p.list_lbmax, p.visited, p.qn_dev, p.pilot_keys, p.floors, p.q0,
                                     p.n_lists, p.q_count, 4 * p.n_tiles, p.cos_slack, p.gam, p.g2};
-    for (int i = tid; i < kWideQ * kKQ; i += kWideThreads) {
-        s_lk[i] = 0ull;
-        s_lp[i] = 0u;
-    }
     for (int i = tid; i < kWideQ; i += kWideThreads) {
         s_cnt[i] = 0;
         s_ovf[i] = 0;
@@ -1328,6 +1326,10 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     auto drain_flush = [&](const WideQuarter& d) {
         const WideCold& c = s_cold;
         const int sh = d.shard;
+        for (int i = lane; i < 32 * kKQ; i += 64) {   // this wave's queries' lists (ring memory: zero them first)
+            s_lk[wq0 * kKQ + i] = 0ull;
+            s_lp[wq0 * kKQ + i] = 0u;
+        }
         const int n = min(s_qn[wave], qcap);
         const uint2* q = s_q + (size_t)wave * qcap;
         for (int i0 = 0; i0 < n; i0 += 64) {
@@ -1412,8 +1414,6 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
                 c.cand[l * kKQ + e] = lkb;
                 c.cand_lb[l * kKQ + e] = lpb;
                 if (e == 0) c.list_lbmax[l] = m;
-                s_lk[qg * kKQ + e] = 0ull;
-                s_lp[qg * kKQ + e] = 0u;
                 if (e == 0) {
                     s_cnt[qg] = 0;
                     s_ovf[qg] = 0;
@@ -1468,58 +1468,30 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
 #ifdef OSK_TESTING
     uint32_t n_events = 0, n_pairs = 0, n_slow = 0;
 #endif
-    // ---- the wave's items: per nonempty quarter, groups wave, wave + 8, … (a wave with none gets one phantom
-    // item there, so it still takes part in the quarter's barriers) ----
+    // ---- the wave's items: per nonempty quarter, its groups wave, wave + 8, … — issued kRowsNR ahead through the
+    // wave's ring, never past the quarter's end (the lists overlay the rings in the quarter-end drain) ----
     auto groups_of = [&](int q) { return __builtin_amdgcn_readfirstlane((s_quart[q].nrows + 15) >> 4); };
-    auto next_q = [&](int q) {   // the next nonempty quarter after q (n_mine: none)
-        do ++q; while (q < n_mine && groups_of(q) == 0);
-        return q;
-    };
-    int q_last = -1;
-    for (int q = 0; q < n_mine; ++q)
-        if (groups_of(q) > 0) q_last = q;
-    if (q_last < 0) return;   // (every wave alike: no nonempty quarter, no barrier follows)
-    int iq = next_q(-1), ig = wave;   // the next item to issue
     // this wave's ring: slot d at ring_base + d·kRowsSlot (LDS byte address for the DMAs, pointer for the reads)
     const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(
         (uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem + (uint32_t)(wave * NR * kRowsSlot));
     const char* ring = s_ring + wave * NR * kRowsSlot;
-    // one item's DMAs into slot d — the two 1 KiB slabs (lane-linear: the A operand), and 5 bound-term float4:
+    const int4* c_xt = nullptr;
+    const float4* c_at = nullptr;
+    int c_ng = 0, c_nrows = 0;   // (the quarter's groups and rows, in SGPRs)
+    // group g's DMAs into slot d — the two 1 KiB slabs (lane-linear: the A operand), and 5 bound-term float4:
     // lanes 0–3 the rows' |x|² (EUCLIDEAN, slots 12–15) or per-row factors (COSINE, slots 0–3), lane 4 slot 17
-    // {s_g, f_cos, zero-row flag, 0}.  Three DMA instructions whatever the item (past the stream's end the last
-    // quarter's first group: the ring's vmcnt waits count exactly three per item).
-    auto issue = [&](int d) {
-        const int q = iq < n_mine ? iq : q_last;
-        const int g = (iq < n_mine && ig < groups_of(q)) ? ig : 0;   // (a phantom item or past the end: group 0)
-        const int4* xg = reinterpret_cast<const int4*>(rfl_ptr_c(s_quart[q].xt)) + (size_t)g * 128;
-        const float4* ag = reinterpret_cast<const float4*>(rfl_ptr_c(s_quart[q].at)) + (size_t)g * kAuxGroupF4;
+    // {s_g, f_cos, zero-row flag, 0}: three DMA instructions
+    auto issue = [&](int d, int g) {
+        const int4* xg = c_xt + (size_t)g * 128;
+        const float4* ag = c_at + (size_t)g * kAuxGroupF4;
         const uint32_t base = ring_lds + (uint32_t)(d * kRowsSlot);
         glds16(xg + lane, base);
         glds16(xg + 64 + lane, base + 1024u);
         if (lane < 5) glds16(ag + (lane == 4 ? 17 : (SIM == SIM_EUCLIDEAN ? 12 : 0) + lane), base + 2048u);
-        if (iq < n_mine) {   // advance the issue cursor: groups wave, wave + 8, …, then the next quarter
-            ig += kWideWaves;
-            if (ig >= groups_of(iq)) {
-                iq = next_q(iq);
-                ig = wave;
-            }
-        }
     };
-    // ... and one item's work
-    int pq = next_q(-1), pg = wave, cur = -1;
-    int c_ng = 0, c_nrows = 0;   // (the work quarter's groups and rows, in SGPRs: not re-read from LDS per item)
-    auto process = [&](int d) {
-        if (pq != cur) {   // the quarter changes: the last one's drain + flush, the new one's constants
-            __syncthreads();
-            if (cur >= 0) drain_flush(s_quart[cur]);
-            begin_quarter(s_quart[pq]);
-            __syncthreads();
-            cur = pq;
-            c_nrows = __builtin_amdgcn_readfirstlane(s_quart[pq].nrows);
-            c_ng = (c_nrows + 15) >> 4;
-        }
-        const int g = pg;
-        if (g < c_ng && !(ablate & 1)) {
+    // ... and group g's work, its data in slot d
+    auto process = [&](int d, int g) {
+        if (!(ablate & 1)) {
             const int r0 = 16 * g, nr = min(16, c_nrows - r0);
             // every LDS read of the item at once (one wait): the A operand, the group's terms, the query constants
             const char* sl = ring + d * kRowsSlot;
@@ -1664,26 +1636,44 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
                 }
             }
         }
-        // advance the work cursor (the load cursor's rule)
-        pg += kWideWaves;
-        if (pg >= c_ng) {
-            pq = next_q(pq);
-            pg = wave;
-        }
     };
+    int cur = -1;
+    for (int q = 0; q < n_mine; ++q) {
+        if (groups_of(q) == 0) continue;   // (flushed above)
+        // the quarter changes: the last one's drain + flush, this one's constants (two barriers; between them no
+        // wave has a DMA in flight, so the lists may overlay the rings)
+        if (cur >= 0) {
+            __syncthreads();
+            drain_flush(s_quart[cur]);
+        }
+        begin_quarter(s_quart[q]);
+        __syncthreads();
+        cur = q;
+        c_nrows = __builtin_amdgcn_readfirstlane(s_quart[q].nrows);
+        c_ng = (c_nrows + 15) >> 4;
+        c_xt = reinterpret_cast<const int4*>(rfl_ptr_c(s_quart[q].xt));
+        c_at = reinterpret_cast<const float4*>(rfl_ptr_c(s_quart[q].at));
+        // this wave's groups: wave + 8i, i < n_it
+        const int n_it = c_ng > wave ? (c_ng - 1 - wave) / kWideWaves + 1 : 0;
 #pragma unroll
-    for (int d = 0; d < NR; ++d) issue(d);
-    while (pq < n_mine) {
+        for (int d = 0; d < NR; ++d)
+            if (d < n_it) issue(d, wave + d * kWideWaves);
+        for (int i0 = 0; i0 < n_it; i0 += NR) {
 #pragma unroll
-        for (int d = 0; d < NR; ++d) {
-            if (pq < n_mine) {
-                vm_wait<(NR - 1) * 3>();   // slot d's three DMAs have landed (the NR − 1 younger items' may not)
-                process(d);
-                issue(d);
+            for (int d = 0; d < NR; ++d) {
+                const int i = i0 + d;
+                if (i < n_it) {
+                    // slot d's three DMAs have landed (the NR − 1 younger items' may not; at the quarter's tail
+                    // fewer are younger: wait for all)
+                    if (i + NR - 1 < n_it) vm_wait<(NR - 1) * 3>();
+                    else vm_wait<0>();
+                    process(d, wave + i * kWideWaves);
+                    if (i + NR < n_it) issue(d, wave + (i + NR) * kWideWaves);
+                }
             }
         }
     }
-    vm_wait<0>();   // no DMA may still be landing in this workgroup's LDS when it retires
+    vm_wait<0>();   // (no DMA is in flight past a quarter; kept: nothing may land after the workgroup retires)
     // the last quarter's drain and flush
     __syncthreads();
     if (cur >= 0) drain_flush(s_quart[cur]);
@@ -1726,7 +1716,8 @@ static size_t sq8_wide_rows_lds(int n_shards, int n_mine) {
     return (size_t)kWideWaves * kRowsNR * kRowsSlot + (size_t)n_mine * sizeof(WideQuarter) +
            (n_shards <= kRowsMaxFloorShards ? (size_t)n_shards * kWideQ * 4 : 0);
 }
-static constexpr size_t kRowsStatic = (size_t)kWideQ * kKQ * 12 + (size_t)kWideQ * 16 + (size_t)kWideQ * 4 * 5 + 16 * 4 + 128;
+static constexpr size_t kRowsStatic = (size_t)kWideQ * 16 + (size_t)kWideQ * 4 * 5 + 16 * 4 + 128;
+static_assert(kWideWaves * kRowsNR * kRowsSlot >= kWideQ * kKQ * 12, "the lists overlay the rings");
 static constexpr int kRowsMinQcap = 128;   // deferred entries per owner wave at least (else more workgroups)
 bool sq8_wide_rows_supported(int u8) { return sq8_wide_supported(u8) && sq8_wide_ks(u8) == 2; }
 
