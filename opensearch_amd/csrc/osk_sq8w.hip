@@ -1243,7 +1243,9 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     const int qbeg = p.quarter_begin, n_range = (p.quarter_end > 0 ? p.quarter_end : n_quarters) - qbeg;
     const int n_mine = (int)blockIdx.x < n_range ? (n_range - 1 - (int)blockIdx.x) / G + 1 : 0;
     const bool floor_lds = S <= kRowsMaxFloorShards;
-    const int qcap = p.wide_qcap;   // deferred entries per owner wave (launch_sq8_wide_rows: what LDS leaves; tests less)
+    // the deferred queues: one per (owner, producer) wave pair, sub = qcap / 8 entries each (qcap per owner:
+    // launch_sq8_wide_rows, what LDS leaves; tests less) — a producer appends with its own counter, no atomics
+    const int qcap = p.wide_qcap, sub = p.wide_qcap / kWideWaves;
 
     // (the fixed-size arrays are static LDS: their addresses are constants, so the hot loop's LDS accesses take
     // immediate offsets instead of address registers; the rings, queues, quarter descriptors and floors are the
@@ -1256,14 +1258,14 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     __shared__ float s_qnd[kWideQ];                        // |q|² device order (COSINE)
     __shared__ int32_t s_cnt[kWideQ];                      // list fill
     __shared__ int32_t s_ovf[kWideQ];                      // queue overflowed this quarter
-    __shared__ int32_t s_qn[16];                           // [8] queue fill per owner
+    __shared__ int32_t s_qn[kWideWaves * kWideWaves];      // [owner][producer] queue fill (published at quarter end)
     char* s_ring = smem;                                                                   // [8 waves][NR] slots
     // the lists [kWideQ][kKQ] keys + lower bounds (48 KB) overlay the rings: they live only in the quarter-end
     // drain and flush, when no DMA is in flight (a quarter's items are issued inside the quarter only)
     uint64_t* s_lk = reinterpret_cast<uint64_t*>(smem);
     uint32_t* s_lp = reinterpret_cast<uint32_t*>(s_lk + kWideQ * kKQ);
     WideQuarter* s_quart = reinterpret_cast<WideQuarter*>(smem + kWideWaves * NR * kRowsSlot);   // [n_mine]
-    uint2* s_q = reinterpret_cast<uint2*>(s_quart + n_mine);                             // [8 owners][qcap]
+    uint2* s_q = reinterpret_cast<uint2*>(s_quart + n_mine);                             // [8 owners][8][sub]
     uint32_t* s_floor = reinterpret_cast<uint32_t*>(s_q + kWideWaves * qcap);           // [S][kWideQ] (S ≤ 8)
     if (tid == 0) s_cold = WideCold{p.cand, p.cand_lb, p.list_lbmax, p.visited, p.qn_dev, p.pilot_keys, p.floors, p.q0,
                                     p.n_lists, p.q_count, 4 * p.n_tiles, p.cos_slack, p.gam, p.g2};
@@ -1273,7 +1275,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
         s_qc[i] = i < p.q_count ? p.qc[i] : make_float4(0.f, 0.f, 0.f, 0.f);
         s_qnd[i] = (SIM == SIM_COSINE && i < p.q_count) ? p.qn_dev[i] : 0.0f;
     }
-    if (tid < 16) s_qn[tid] = 0;
+    if (tid < kWideWaves * kWideWaves) s_qn[tid] = 0;
     if (floor_lds)
         for (int i = tid; i < S * kWideQ; i += kWideThreads) {
             const int qi = i % kWideQ;
@@ -1330,11 +1332,22 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
             s_lk[wq0 * kKQ + i] = 0ull;
             s_lp[wq0 * kKQ + i] = 0u;
         }
-        const int n = min(s_qn[wave], qcap);
+        // this owner's entries: producer p's sub-queue holds cnt[p] of them; entry e of the concatenation is found
+        // by the producers' running offsets (8 scalar compares per lane)
+        int off[kWideWaves + 1];
+        off[0] = 0;
+#pragma unroll
+        for (int pw = 0; pw < kWideWaves; ++pw)
+            off[pw + 1] = off[pw] + min(__builtin_amdgcn_readfirstlane(s_qn[wave * kWideWaves + pw]), sub);
+        const int n = off[kWideWaves];
         const uint2* q = s_q + (size_t)wave * qcap;
         for (int i0 = 0; i0 < n; i0 += 64) {
-            const bool ok = i0 + lane < n;
-            const uint2 en = ok ? q[i0 + lane] : make_uint2(0u, 0u);
+            const int e = i0 + lane;
+            const bool ok = e < n;
+            int pw = 0;
+#pragma unroll
+            for (int w = 1; w < kWideWaves; ++w) pw += e >= off[w];
+            const uint2 en = ok ? q[pw * sub + (e - off[pw])] : make_uint2(0u, 0u);
             const int qi = (int)(en.y & 255u), rowq = (int)(en.y >> 8);
             const float* af = reinterpret_cast<const float*>(d.at + (rowq >> 4) * kAuxGroupF4);
             const int rr = rowq & 15;
@@ -1420,7 +1433,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
                 }
             }
         }
-        if (lane == 0) s_qn[wave] = 0;
+        if (lane < kWideWaves) s_qn[wave * kWideWaves + lane] = 0;
         if (c.visited && c.q0 == 0 && tid == 0 && d.nrows > 0)
             atomicAdd(&c.visited[d.seg], (unsigned long long)d.nrows);
     };
@@ -1488,6 +1501,16 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
         glds16(xg + lane, base);
         glds16(xg + 64 + lane, base + 1024u);
         if (lane < 5) glds16(ag + (lane == 4 ? 17 : (SIM == SIM_EUCLIDEAN ? 12 : 0) + lane), base + 2048u);
+    };
+    int q_cnt[kWideWaves];   // this wave's entries per owner in the current quarter (wave-uniform)
+#pragma unroll
+    for (int o = 0; o < kWideWaves; ++o) q_cnt[o] = 0;
+    auto publish = [&]() {   // the counts → s_qn (before the quarter-end barrier), reset
+#pragma unroll
+        for (int o = 0; o < kWideWaves; ++o) {
+            if (lane == 0) s_qn[o * kWideWaves + wave] = q_cnt[o];
+            q_cnt[o] = 0;
+        }
     };
     // ... and group g's work, its data in slot d
     auto process = [&](int d, int g) {
@@ -1610,10 +1633,9 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
                         }
                         if (!tot) continue;
                         const int owner = qb >> 1;   // (queries qb·16 … qb·16 + 15 belong to wave qb / 2)
-                        int base = 0;
-                        if (lane == 0) base = atomicAdd(&s_qn[owner], tot);
-                        base = __builtin_amdgcn_readfirstlane(base);
-                        uint2* oq_ = s_q + (size_t)owner * qcap;
+                        int base = q_cnt[owner];     // (this wave's sub-queue of the owner: no other writer)
+                        q_cnt[owner] += tot;
+                        uint2* oq_ = s_q + (size_t)owner * qcap + (size_t)wave * sub;
                         bool dropped = false;
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
@@ -1621,7 +1643,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)b[r], 0u));
                             const int slot = base + below;
                             if (pr[r]) {
-                                if (slot < qcap)
+                                if (slot < sub)
                                     oq_[slot] = make_uint2((uint32_t)acc[j][r], (uint32_t)(r0 + 4 * grp + r) << 8 | (uint32_t)qi);
                                 else
                                     dropped = true;
@@ -1643,6 +1665,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
         // the quarter changes: the last one's drain + flush, this one's constants (two barriers; between them no
         // wave has a DMA in flight, so the lists may overlay the rings)
         if (cur >= 0) {
+            publish();
             __syncthreads();
             drain_flush(s_quart[cur]);
         }
@@ -1675,6 +1698,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     }
     vm_wait<0>();   // (no DMA is in flight past a quarter; kept: nothing may land after the workgroup retires)
     // the last quarter's drain and flush
+    publish();
     __syncthreads();
     if (cur >= 0) drain_flush(s_quart[cur]);
 #ifdef OSK_TESTING
