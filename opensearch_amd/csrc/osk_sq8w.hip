@@ -1537,8 +1537,6 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
             const float f = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(SIM == SIM_COSINE ? g17.y : g17.x)));
             bool zg = false;
             if constexpr (SIM == SIM_COSINE) zg = __builtin_amdgcn_readfirstlane(__float_as_int(g17.z)) != 0;
-            // EUCLIDEAN: the smallest |x|² of the lane's rows (ca > 0: the per-row threshold w_r·ca + cb is smallest there)
-            const float wmin = SIM == SIM_EUCLIDEAN ? fminf(fminf(xr4.x, xr4.y), fminf(xr4.z, xr4.w)) : 0.0f;
             // a pass of PB query blocks: their dots (2 chained MFMAs each)
             auto dots = [&](int h, i32x4 (&acc)[PB]) __attribute__((always_inline)) {
                 if (!(ablate & 2)) {
@@ -1555,8 +1553,9 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
             };
             // the fast test: per block the lane's largest dot against the group's common factor (DOT / MIP:
             // s_g; COSINE: f_cos, a c ≤ 0 lets every pair through, as does a zero row) — sq8_wide's test.
-            // EUCLIDEAN: the per-row test I·s_g ≥ w_r·ca + cb (quick_consts) relaxed to the lane's smallest w_r
-            // (ca > 0), so t = fma(max I, s_g, −(wmin·ca + cb)) < 0 implies every row of the lane fails.
+            // EUCLIDEAN: the per-row test I_r·s_g ≥ w_r·ca + cb itself, t = max_r fma(I_r, s_g, −fma(w_r, ca, cb)) —
+            // the score 2·x·q − |x|² is a small difference of large terms, and relaxing the lane's four rows to
+            // (max I, min w) let every group through at C2 (uniform [0,1) coordinates: rows 4.000 slow passes of 4).
             // All 16 blocks first, ONE vote per group (no branch between the passes: the next pass's MFMAs overlap
             // this pass's tests); a passing pass recomputes its dots and tests in the slow path.
             auto tests = [&](const i32x4 (&acc)[PB], const float (&cav)[PB], const float (&cbv)[PB], float (&tf)[PB])
@@ -1564,11 +1563,17 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
 #pragma unroll
                 for (int j = 0; j < PB; ++j) {
                     const i32x4& I = acc[j];
-                    const int M = max(max(I[0], I[1]), max(I[2], I[3]));
-                    float c = cav[j];
-                    if constexpr (SIM == SIM_COSINE) c = !(cav[j] > 0.0f) ? -__builtin_inff() : cav[j];
-                    if constexpr (SIM == SIM_EUCLIDEAN) c = fmaf(wmin, cav[j], cbv[j]);
-                    tf[j] = fmaf((float)M, f, -c);
+                    if constexpr (SIM == SIM_EUCLIDEAN) {
+                        tf[j] = fmaxf(fmaxf(fmaf((float)I[0], f, -fmaf(xr4.x, cav[j], cbv[j])),
+                                            fmaf((float)I[1], f, -fmaf(xr4.y, cav[j], cbv[j]))),
+                                      fmaxf(fmaf((float)I[2], f, -fmaf(xr4.z, cav[j], cbv[j])),
+                                            fmaf((float)I[3], f, -fmaf(xr4.w, cav[j], cbv[j]))));
+                    } else {
+                        const int M = max(max(I[0], I[1]), max(I[2], I[3]));
+                        float c = cav[j];
+                        if constexpr (SIM == SIM_COSINE) c = !(cav[j] > 0.0f) ? -__builtin_inff() : cav[j];
+                        tf[j] = fmaf((float)M, f, -c);
+                    }
                 }
             };
             float hm[NQB / PB];   // per pass, the lane's largest test value
