@@ -323,6 +323,7 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         {"sq8_wide_defer", &g_tuning.sq8_wide_defer, 0, 1, false},
         {"sq8_wide_rows", &g_tuning.sq8_wide_rows, 0, 1, false},
         {"sq8_wide_rows_qcap", &g_tuning.sq8_wide_rows_qcap, 0, 1 << 20, false},
+        {"sq8_scan_deep", &g_tuning.sq8_scan_deep, 0, 1, false},
         {"sq6_rebound_stride", &g_tuning.sq6_rebound_stride, 0, 1, false},
         {"sq6_rebound_retest", &g_tuning.sq6_rebound_retest, 0, 1, false},
         {"sq6_rebound_wgs", &g_tuning.sq6_rebound_wgs, 0, 16, false},

@@ -466,6 +466,7 @@ struct Tuning {
     std::atomic<int> sq6_rebound_stride{1};   // sq6_rebound: strided list assignment (0: contiguous)
     std::atomic<int> sq6_rebound_wgs{0};      // sq6_rebound: workgroups per CU (0: as many as fit)
     std::atomic<int> sq8_wide_rows{1};    // wide kernel, ≤ 128 dims: the main passes on sq8_wide_rows (0: sq8_wide)
+    std::atomic<int> sq8_scan_deep{0};    // single-query sq8_scan ≤ 256 dims: U = 8 row groups in flight per wave
     std::atomic<int> sq8_wide_rows_qcap{0};   // (tests) its deferred queue per owner wave, entries (0: kRowsQC)
     std::atomic<int> sq8_wide_defer{1};   // wide kernel: defer list insertions to each quarter's end (0: immediate)
     std::atomic<int> sq8_wide_quarter_rows{0};   // rows per wide quarter, read when a view builds its table (0 = auto)

@@ -321,7 +321,7 @@ __device__ __forceinline__ void gather_wave_range(int64_t cnt, int j, int nj, in
 }
 
 template <int L, int V, int NQ, int U, int MODE = kScanRows>
-__global__ __launch_bounds__(kBlock, NQ == 1 && V <= 3 ? 4 : 1) void sq8_scan(Sq8Params p) {   // ≤ 128 VGPRs: 4 waves/SIMD
+__global__ __launch_bounds__(kBlock, NQ == 1 && V <= 3 ? (U > 4 ? 3 : 4) : 1) void sq8_scan(Sq8Params p) {   // ≤ 128 VGPRs: 4 waves/SIMD (U = 8: 3)
     constexpr int R = 64 / L;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform: scalar loop control
     const int t = lane & (L - 1), g = lane / L;
@@ -614,12 +614,18 @@ static const Sq8Fn kSq8Gather[8][4] = {OSK_SQ8_GROW(4, 1),  OSK_SQ8_GROW(8, 1), 
                                        OSK_SQ8_GROW(16, 2), OSK_SQ8_GROW(16, 3), OSK_SQ8_GROW(16, 4),
                                        OSK_SQ8_GROW(32, 4), OSK_SQ8_GROW(64, 4)};
 
+// single queries over ≤ 256-dim rows (V = 1) with twice the row groups in flight per wave (U = 8: 8 KiB per wave
+// of rows; the U = 4 scan's waves each wait out ≈ 8 dependent round trips over a 1M-row view)
+static const Sq8Fn kSq8Deep[3] = {sq8_scan<4, 1, 1, 8>, sq8_scan<8, 1, 1, 8>, sq8_scan<16, 1, 1, 8>};
+
 hipError_t launch_sq8_scan(int nq, const Sq8Params& p, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
     const int slot = nq <= 1 ? 0 : nq <= 2 ? 1 : nq <= 4 ? 2 : 3;
     // NQ > 1: the queries and the 4 waves' per-query lists in LDS
     const size_t lds = slot == 0 ? 0 : (size_t)(1 << slot) * (p.units8 * 16 + 4 * kKQ * 12);
     const int c = sq8_cfg(p.units8);
-    const auto fn = p.gtiles ? kSq8Gather[c][slot] : kSq8[c][slot];
+    const auto fn = p.gtiles ? kSq8Gather[c][slot]
+                    : (slot == 0 && c <= 2 && g_tuning.sq8_scan_deep) ? kSq8Deep[c]
+                                                                      : kSq8[c][slot];
     if (ev_start || ev_stop)
         hipExtLaunchKernelGGL(fn, dim3(p.n_tiles), dim3(kBlock), lds, s, ev_start, ev_stop, 0, p);
     else

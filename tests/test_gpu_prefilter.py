@@ -10,7 +10,8 @@ Every test runs five times: batches scanned by the wide int8 MFMA kernel (sq8_wi
 by the int8 MFMA kernel (sq8_mfma, tune "sq8_mfma_min"
 2, the default) with 32 and with 16 queries per launch (rows ≤ 256 dims streamed by the LDS-DMA ring,
 the default), with 32 queries and register row loads ("sq8_mfma_ring" 0), and by the VALU kernel
-(sq8_scan, "sq8_mfma_min" 0).
+(sq8_scan, "sq8_mfma_min" 0), the last also with its single-query launches at 8 row groups in flight per wave
+("sq8_scan_deep" 1).
 """
 import numpy as np
 import pytest
@@ -24,18 +25,23 @@ SIMS = [LU.VectorSimilarityFunction(s) for s in range(4)]
 COS = LU.VectorSimilarityFunction.COSINE
 
 
-@pytest.fixture(autouse=True, params=["mfma32", "mfma16", "mfma32reg", "valu", "wide"])
+SCAN_DEEP_DEFAULT = 0
+
+
+@pytest.fixture(autouse=True, params=["mfma32", "mfma16", "mfma32reg", "valu", "valudeep", "wide"])
 def scan_kernel(request):
     """The int8 scan kernel of batched prefilter searches (single queries always take sq8_scan):
     sq8_mfma with 32 or 16 queries per launch (LDS-DMA ring), with register row loads, sq8_scan, or the
     wide kernel (osk_sq8w.hip, 256 queries per launch; unfiltered batches of rows ≤ 256 dims, the others
     fall back to sq8_mfma)."""
-    _lib.tune("sq8_mfma_min", 0 if request.param == "valu" else 2)
+    _lib.tune("sq8_mfma_min", 0 if request.param in ("valu", "valudeep") else 2)
+    _lib.tune("sq8_scan_deep", 1 if request.param == "valudeep" else 0)
     _lib.tune("sq8_mfma_queries", 16 if request.param == "mfma16" else 32)
     _lib.tune("sq8_mfma_ring", 0 if request.param == "mfma32reg" else -1)
     _lib.tune("sq8_wide_min", 2 if request.param == "wide" else 0)
     _lib.tune("sq8_wide_force", 1 if request.param == "wide" else 0)
     yield request.param
+    _lib.tune("sq8_scan_deep", SCAN_DEEP_DEFAULT)
     _lib.tune("sq8_mfma_min", 2)
     _lib.tune("sq8_mfma_queries", 32)
     _lib.tune("sq8_mfma_ring", -1)
