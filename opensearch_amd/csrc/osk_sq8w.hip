@@ -1228,6 +1228,7 @@ template <int SIM>
 __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     typedef int i32x4 __attribute__((ext_vector_type(4)));
     constexpr int NQB = kWideQ / 16, NR = kRowsNR, PB = kRowsQB;
+    static_assert(PB == 2 || PB == 4, "passes of 2 or 4 query blocks");
     constexpr int sim = SIM;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int col = lane & 15, grp = lane >> 4;
@@ -1522,15 +1523,25 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
             const i32x4 A1 = *reinterpret_cast<const i32x4*>(sl + 1024 + lane * 16);
             const float4 g17 = *reinterpret_cast<const float4*>(sl + 2048 + 64);   // {s_g, f_cos, zero-row flag, 0}
             const float4 xr4 = *reinterpret_cast<const float4*>(sl + 2048 + grp * 16);   // EUCLIDEAN |x|², COSINE factors
-            // the pass's query constants (PB = 4 blocks: one ds_read_b128 each)
+            // the pass's query constants (PB blocks: one ds_read_b128 / b64 each)
             auto consts = [&](int h, float (&cav)[PB], float (&cbv)[PB]) __attribute__((always_inline)) {
-                const float4 cq = *reinterpret_cast<const float4*>(s_ca + col * 16 + h * PB);
-                cav[0] = cq.x, cav[1] = cq.y, cav[2] = cq.z, cav[3] = cq.w;
-                if constexpr (SIM == SIM_EUCLIDEAN) {
-                    const float4 bq = *reinterpret_cast<const float4*>(s_cb + col * 16 + h * PB);
-                    cbv[0] = bq.x, cbv[1] = bq.y, cbv[2] = bq.z, cbv[3] = bq.w;
-                } else {
+                if constexpr (PB == 4) {
+                    const float4 cq = *reinterpret_cast<const float4*>(s_ca + col * 16 + h * PB);
+                    cav[0] = cq.x, cav[1] = cq.y, cav[2] = cq.z, cav[3] = cq.w;
                     cbv[0] = cbv[1] = cbv[2] = cbv[3] = 0.0f;
+                } else {
+                    const float2 cq = *reinterpret_cast<const float2*>(s_ca + col * 16 + h * PB);
+                    cav[0] = cq.x, cav[1] = cq.y;
+                    cbv[0] = cbv[1] = 0.0f;
+                }
+                if constexpr (SIM == SIM_EUCLIDEAN) {
+                    if constexpr (PB == 4) {
+                        const float4 bq = *reinterpret_cast<const float4*>(s_cb + col * 16 + h * PB);
+                        cbv[0] = bq.x, cbv[1] = bq.y, cbv[2] = bq.z, cbv[3] = bq.w;
+                    } else {
+                        const float2 bq = *reinterpret_cast<const float2*>(s_cb + col * 16 + h * PB);
+                        cbv[0] = bq.x, cbv[1] = bq.y;
+                    }
                 }
             };
             // the group's factor: DOT / MIP / EUCLIDEAN s_g (every valid row's a_r: one scale per group), COSINE f_cos
@@ -1583,14 +1594,22 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
                 float cav[PB], cbv[PB], tf[PB];
                 dots(h, acc);
                 if (ablate & 8) {   // (A/B: the MFMAs alone)
-                    hm[h] = (float)max(max(acc[0][0], acc[1][1]), max(acc[2][2], acc[3][3]));
+                    int m = acc[0][0];
+#pragma unroll
+                    for (int j = 1; j < PB; ++j) m = max(m, acc[j][j & 3]);
+                    hm[h] = (float)m;
                     continue;
                 }
                 consts(h, cav, cbv);
                 tests(acc, cav, cbv, tf);
-                hm[h] = fmaxf(fmaxf(tf[0], tf[1]), fmaxf(tf[2], tf[3]));
+                float m = tf[0];
+#pragma unroll
+                for (int j = 1; j < PB; ++j) m = fmaxf(m, tf[j]);
+                hm[h] = m;
             }
-            const float run = fmaxf(fmaxf(hm[0], hm[1]), fmaxf(hm[2], hm[3]));
+            float run = hm[0];
+#pragma unroll
+            for (int h = 1; h < NQB / PB; ++h) run = fmaxf(run, hm[h]);
             if (ablate & 12) {
                 if (run == 1.2345f) s_ovf[0] = 1;   // (keeps the work)
             } else if (__ballot(!(run < 0.0f)) || zg) {
@@ -1614,7 +1633,13 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
 #ifdef OSK_TESTING
                         ++n_events;
 #endif
-                        const int qi = qb * 16 + col;
+                        // the lane's column and row group, opaque here: else the compiler hoists the (block, row)
+                        // combinations of the enqueue's words and tests out of the loop as 64 per-lane constants,
+                        // and at EUCLIDEAN (whose tests hold one more constant per query) spilled them to scratch —
+                        // each reload a vmcnt(0), which drains the wave's DMA ring
+                        int ocol = col, ogrp = grp;
+                        __asm__ volatile("" : "+v"(ocol), "+v"(ogrp));
+                        const int qi = qb * 16 + ocol;
                         const bool qv = qi < s_cold.q_count;
                         bool pass[4];
                         if constexpr (SIM == SIM_EUCLIDEAN) {   // the per-row test: t_r = fma(I, s_g, −fma(w_r, ca, cb))
@@ -1632,7 +1657,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
                         int tot = 0;
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
-                            pr[r] = pass[r] && 4 * grp + r < nr && qv;
+                            pr[r] = pass[r] && 4 * ogrp + r < nr && qv;
                             b[r] = __ballot(pr[r]);
                             tot += __popcll(b[r]);
                         }
@@ -1649,7 +1674,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
                             const int slot = base + below;
                             if (pr[r]) {
                                 if (slot < sub)
-                                    oq_[slot] = make_uint2((uint32_t)acc[j][r], (uint32_t)(r0 + 4 * grp + r) << 8 | (uint32_t)qi);
+                                    oq_[slot] = make_uint2((uint32_t)acc[j][r], (uint32_t)(r0 + 4 * ogrp + r) << 8 | (uint32_t)qi);
                                 else
                                     dropped = true;
                             }
