@@ -37,6 +37,9 @@
 // Results are bit-identical to sq8_mfma's, the fp32 streaming scan's and the oracle's (tests/test_gpu_wide.py).
 #include <hip/hip_ext.h>
 
+#include <map>
+#include <mutex>
+
 #include "osk_device.h"
 #include "osk_internal.h"
 #include "osk_wave.h"
@@ -1747,7 +1750,6 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
 using WideFn = void (*)(Sq8Params);
 #define OSK_WIDE_SIMS(KS) {sq8_wide<KS, 0>, sq8_wide<KS, 1>, sq8_wide<KS, 2>, sq8_wide<KS, 3>}
 static const WideFn kWide[4][4] = {OSK_WIDE_SIMS(2), OSK_WIDE_SIMS(4), OSK_WIDE_SIMS(8), OSK_WIDE_SIMS(12)};
-static constexpr size_t kLdsCap = 160 * 1024 - 128;   // (the kernel's static LDS: WideCold)
 static_assert(sizeof(WideCold) <= 128, "WideCold: 128 B of static LDS reserved");
 
 template <int KS>
@@ -1770,7 +1772,20 @@ static size_t sq8_wide_rows_lds(int n_shards, int n_mine) {
     return (size_t)kWideWaves * kRowsNR * kRowsSlot + (size_t)n_mine * sizeof(WideQuarter) +
            (n_shards <= kRowsMaxFloorShards ? (size_t)n_shards * kWideQ * 4 : 0);
 }
-static constexpr size_t kRowsStatic = (size_t)kWideQ * 16 + (size_t)kWideQ * 4 * 5 + 16 * 4 + 128;
+// the kernel's static LDS as compiled (hipFuncGetAttributes, once per kernel): a hand-kept estimate fell 160 B
+// short when the queue counts grew to [8][8], so EUCLIDEAN's dynamic LDS (sized to fill the 160 KB) took the
+// launch past the CU's LDS and the GPU faulted (round 6; found by tests/test_gpu_wide.py)
+static size_t kernel_static_lds(const void* fn) {
+    static std::mutex mu;
+    static std::map<const void*, size_t> cache;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(fn);
+    if (it != cache.end()) return it->second;
+    hipFuncAttributes a{};
+    const size_t v = hipFuncGetAttributes(&a, fn) == hipSuccess ? a.sharedSizeBytes : (size_t)16 * 1024;   // (else: generous)
+    cache[fn] = v;
+    return v;
+}
 static_assert(kWideWaves * kRowsNR * kRowsSlot >= kWideQ * kKQ * 12, "the lists overlay the rings");
 static constexpr int kRowsMinQcap = 128;   // deferred entries per owner wave at least (else more workgroups)
 bool sq8_wide_rows_supported(int u8) { return sq8_wide_supported(u8) && sq8_wide_ks(u8) == 2; }
@@ -1783,17 +1798,18 @@ hipError_t launch_sq8_wide_rows(const Sq8Params& p, hipStream_t s, hipEvent_t ev
     const int nq4 = (p.quarter_end > 0 ? p.quarter_end : 4 * p.n_tiles) - p.quarter_begin;
     if (p.quarter_begin < 0 || nq4 < 1 || p.quarter_begin + nq4 > 4 * p.n_tiles) return hipErrorInvalidValue;
     int grid = std::min(p.wide_grid, std::max(1, nq4));
-    constexpr size_t cap = 160 * 1024;
-    while (sq8_wide_rows_lds(p.n_shards, (nq4 + grid - 1) / grid) + kRowsStatic +
-               (size_t)kWideWaves * kRowsMinQcap * sizeof(uint2) > cap)
+    const auto fn = kWideRows[p.sim];
+    const size_t cap = 160 * 1024 - kernel_static_lds(reinterpret_cast<const void*>(fn));
+    while (sq8_wide_rows_lds(p.n_shards, (nq4 + grid - 1) / grid) + (size_t)kWideWaves * kRowsMinQcap * sizeof(uint2) >
+           cap)
         grid *= 2;
     size_t lds = sq8_wide_rows_lds(p.n_shards, (nq4 + grid - 1) / grid);
     // the queues: what LDS leaves, ≤ 1024 entries per owner wave (multiples of 64); tests ask for fewer
     Sq8Params q = p;
-    const int room = (int)std::min<size_t>(1024, (cap - lds - kRowsStatic) / (kWideWaves * sizeof(uint2)) / 64 * 64);
+    const int room = (int)std::min<size_t>(1024, (cap - lds) / (kWideWaves * sizeof(uint2)) / 64 * 64);
     q.wide_qcap = p.wide_qcap > 0 ? std::min(p.wide_qcap, room) : room;
     lds += (size_t)kWideWaves * q.wide_qcap * sizeof(uint2);
-    const auto fn = kWideRows[p.sim];
+    if (lds > cap) return hipErrorInvalidValue;   // (never: the grid doubling above)
     if (ev_start || ev_stop)
         hipExtLaunchKernelGGL(fn, dim3(grid), dim3(kWideThreads), lds, s, ev_start, ev_stop, 0, q);
     else
@@ -1813,12 +1829,13 @@ hipError_t launch_sq8_wide(const Sq8Params& p, hipStream_t s, hipEvent_t ev_star
         return hipErrorInvalidValue;
     int grid = std::min(p.wide_grid, std::max(1, nq4));
     // more workgroups (rounds of the chip) when one CU's share of quarter descriptors does not fit
-    while (sq8_wide_lds(ks, p.sim, p.n_shards, (nq4 + grid - 1) / grid) > kLdsCap) grid *= 2;
+    const size_t lcap = 160 * 1024 - kernel_static_lds(reinterpret_cast<const void*>(fn));
+    while (sq8_wide_lds(ks, p.sim, p.n_shards, (nq4 + grid - 1) / grid) > lcap) grid *= 2;
     size_t lds = sq8_wide_lds(ks, p.sim, p.n_shards, (nq4 + grid - 1) / grid);
     // the deferred-insertion queues in what LDS is left: ≥ 256 entries per wave (one (group, query block) adds at
     // most 64 lanes × 4 rows), else the immediate insertions (and always for the pilot)
     Sq8Params q = p;
-    const int room = (int)((kLdsCap - lds) / (kWideWaves * sizeof(uint2))) / 64 * 64;
+    const int room = (int)((lcap - lds) / (kWideWaves * sizeof(uint2))) / 64 * 64;
     q.wide_qcap = (!p.pilot && p.wide_defer && room >= 256) ? std::min(room, 512) : 0;
     lds += (size_t)kWideWaves * q.wide_qcap * sizeof(uint2);
     if (ev_start || ev_stop)
