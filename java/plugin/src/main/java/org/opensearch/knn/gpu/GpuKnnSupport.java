@@ -36,11 +36,22 @@ import static java.lang.foreign.ValueLayout.JAVA_LONG;
 final class GpuKnnSupport {
     private GpuKnnSupport() {}
 
-    /** The shard's rewritten query, or null when some leaf is not GPU-resident (take Lucene's route). */
+    /** The shard's rewritten query, or null when some leaf is not GPU-resident or k is above the library's
+     *  OSK_MAX_K (take Lucene's route). */
     static Query rewrite(IndexSearcher searcher, String field, Object target, int k, Query filter) throws IOException {
+        if (k < 1 || k > KnnQueryBuilder.MAX_K) return null;   // (osk_view_search refuses it: Lucene's per-leaf route)
         IndexReader reader = searcher.getIndexReader();
-        MemorySegment view = GpuShardViews.forReader(reader, field);
-        if (view == null) return null;
+        GpuShardViews.Lease lease = GpuShardViews.forReader(reader, field);
+        if (lease == null) return null;
+        try {
+            return search(searcher, reader, lease.view(), field, target, k, filter);
+        } finally {
+            GpuShardViews.done(lease);
+        }
+    }
+
+    private static Query search(IndexSearcher searcher, IndexReader reader, MemorySegment view, String field,
+                                Object target, int k, Query filter) throws IOException {
         List<LeafReaderContext> leaves = reader.leaves();
         Weight filterWeight = filter == null ? null : searcher.createWeight(searcher.rewrite(
             new BooleanQuery.Builder().add(filter, BooleanClause.Occur.FILTER).build()), ScoreMode.COMPLETE_NO_SCORES, 1f);

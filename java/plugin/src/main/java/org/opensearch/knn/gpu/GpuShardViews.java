@@ -41,21 +41,40 @@ final class GpuShardViews {
         return vr instanceof GpuFlatVectorsReader g ? g : null;
     }
 
-    /** The shard's view over the field (created on first use, cached until the reader closes); null when some leaf
+    /** A view handed to one search: {@code owned} when the reader has no cache helper (no closed listener to
+     *  release a cached view), so the caller releases it after its call through {@link #done}. */
+    record Lease(MemorySegment view, boolean owned) {}
+
+    /** The shard's view over the field (created on first use, cached until the reader closes; a reader without a
+     *  cache helper gets a view for this one call, never cached: nothing would release it); null when some leaf
      *  with the field is not GPU-resident (the caller then takes Lucene's per-leaf route). */
-    static MemorySegment forReader(IndexReader reader, String field) throws IOException {
+    static Lease forReader(IndexReader reader, String field) throws IOException {
         IndexReader.CacheHelper ch = reader.getReaderCacheHelper();
-        Key key = new Key(ch == null ? reader : ch.getKey(), field);
+        if (ch == null) {
+            MemorySegment v = create(reader.leaves(), field);
+            return v == null ? null : new Lease(v, true);
+        }
+        Key key = new Key(ch.getKey(), field);
         MemorySegment v = VIEWS.get(key);
-        if (v != null) return v;
+        if (v != null) return new Lease(v, false);
         synchronized (GpuShardViews.class) {
             v = VIEWS.get(key);
-            if (v != null) return v;
+            if (v != null) return new Lease(v, false);
             v = create(reader.leaves(), field);
             if (v == null) return null;
             VIEWS.put(key, v);
-            if (ch != null) ch.addClosedListener(k -> release(new Key(k, field)));
-            return v;
+            ch.addClosedListener(k -> release(new Key(k, field)));
+            return new Lease(v, false);
+        }
+    }
+
+    /** After the call: releases a view that was created for it alone. */
+    static void done(Lease lease) {
+        if (lease == null || !lease.owned()) return;
+        try {
+            OsKnn.check((int) OsKnn.VIEW_RELEASE.invokeExact(lease.view()));
+        } catch (Throwable t) {
+            throw OsKnn.wrap(t);
         }
     }
 

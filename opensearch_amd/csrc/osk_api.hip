@@ -138,6 +138,10 @@ std::vector<SegDev> seg_devs(const osk_view* v) {
 
 }  // namespace osk
 
+namespace {
+void sq6_forget_segment(const osk_seg* sg);   // (below, with the 6-bit tier's in-flight records)
+}
+
 osk_seg::~osk_seg() {
     if (self_view) delete self_view;   // holds no reference on this segment
     if (d_rows) (void)hipFree(d_rows);
@@ -161,6 +165,7 @@ osk_seg::~osk_seg() {
         (void)hipStreamSynchronize(nullptr);
         if (cur >= 0) (void)hipSetDevice(cur);
     }
+    sq6_forget_segment(this);   // (a later segment at this address must not wait on this one's launches)
 }
 
 int64_t osk_seg::hbm_bytes() const {
@@ -1478,6 +1483,14 @@ void sq6_prune_locked() {
             g_sq6_inflight[j++] = std::move(g_sq6_inflight[i]);
     }
     g_sq6_inflight.resize(j);
+}
+
+// A segment being destroyed leaves the in-flight records (its launches have completed: the destructor's hipFree
+// calls synchronise the device), so a segment later allocated at the same address never waits on them.
+void sq6_forget_segment(const osk_seg* sg) {
+    std::lock_guard<std::mutex> lk(g_sq6_inflight_mu);
+    for (Sq6Inflight& f : g_sq6_inflight) f.segs.erase(std::remove(f.segs.begin(), f.segs.end(), sg), f.segs.end());
+    sq6_prune_locked();
 }
 
 // A 6-bit launch over a view with a probing segment: record its completion (caller holds the shared side
