@@ -1095,17 +1095,36 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
                     for (int qb = 0; qb < QB; ++qb) {
                         const int qi = wq0 + qb * 16 + col;
                         const float4 qc = s_qc[qi];
-                        uint64_t best = 0ull;
+                        // one precise bound per lane: of its 4 rows the one whose approximate score is best
+                        // (any row's lower bound is a valid pilot key; the bound is ≈ 40 VALU, the pick 3 per row:
+                        // DOT / MIP / COSINE I·a_r, EUCLIDEAN 2·I·a_r·s_q − |x|²)
+                        // (the chosen row's operands carried along as selects: an index into ax[] put it in scratch)
+                        int rb = 0, ib = pacc[qb][0];
+                        float4 axb = ax[0];
+                        float vb = -__builtin_inff();
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
-                            const int rr = 4 * grp + r;
+                            const float ia = (float)pacc[qb][r] * ax[r].x;
+                            float v = SIM == SIM_EUCLIDEAN ? fmaf(2.0f * ia, qc.x, -ax[r].w) : ia;
+                            if (!(4 * grp + r < nr)) v = -__builtin_inff();
+                            const bool take = v > vb;
+                            vb = take ? v : vb;
+                            rb = take ? r : rb;
+                            ib = take ? pacc[qb][r] : ib;
+                            axb.x = take ? ax[r].x : axb.x;
+                            axb.y = take ? ax[r].y : axb.y;
+                            axb.z = take ? ax[r].z : axb.z;
+                            axb.w = take ? ax[r].w : axb.w;
+                        }
+                        uint64_t best = 0ull;
+                        {
+                            const int rr = 4 * grp + rb;
                             float xnd = 0.0f;
                             if constexpr (SIM == SIM_COSINE) xnd = *reinterpret_cast<const float*>(ga + 288 + rr * 4);
                             float lo, hi;
-                            sq8_bounds(sim, (float)pacc[qb][r], ax[r], qc, s_cold.gam, s_cold.g2, lo, hi);
+                            sq8_bounds(sim, (float)ib, axb, qc, s_cold.gam, s_cold.g2, lo, hi);
                             const float lb = SIM == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qnd[qb], xnd);
-                            const uint64_t key = rr < nr ? make_key(lb, hd.vrow0 + (uint32_t)(r0 + rr)) : 0ull;
-                            best = key > best ? key : best;
+                            best = vb > -__builtin_inff() ? make_key(lb, hd.vrow0 + (uint32_t)(r0 + rr)) : 0ull;
                         }
 #pragma unroll
                         for (int o = 16; o <= 32; o <<= 1) {
