@@ -1730,8 +1730,18 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             p.pilot = 1;
             // (0: 128 rows per quarter, 256 at ≥ 512 dims, where the pilot's steps are 32 rows and the better
             // floors pay: C3 b256 3.76 → 3.71 ms, C4's 96 dims 22.98 → 23.27 ms, profiles/r05p/tune50_*)
+            // At least ≈ 64k pilot rows per shard: the floor is the k-th best of the shard's quarter maxima, so a
+            // shard of few quarters (6.5M rows over 8 shards: 64 quarters of 12.7k rows) sampled at 128 rows a
+            // quarter floored the first pass at ≈ its 1,000th best row, and the rows kernel's queues overflowed for
+            // every query (exact re-scans of the overflowed quarters); up to 1,024 rows a quarter.
             const int prows = g_tuning.sq8_wide_pilot_rows.load();
-            p.pilot_rows = prows > 0 ? prows : (sq8_wide_ks(u8) >= 8 ? 256 : 0);
+            int pr = prows > 0 ? prows : (sq8_wide_ks(u8) >= 8 ? 256 : kWidePilotRowsDefault);
+            if (prows <= 0) {
+                const int qps = std::max(1, 4 * v->n_wtiles / std::max(1, S));   // quarters per shard
+                const int want = (kWidePilotSample + qps - 1) / qps;
+                pr = std::max(pr, std::min(1024, (want + 127) / 128 * 128));
+            }
+            p.pilot_rows = pr;
             p.wide_defer = g_tuning.sq8_wide_defer;
             p.pilot_keys = v->ws_pilot.as<uint64_t>();
             p.quarter_begin = 0;

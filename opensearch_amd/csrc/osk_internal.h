@@ -359,6 +359,8 @@ hipError_t launch_sq8_mfma(const Sq8Params& p, hipStream_t s, hipEvent_t ev_star
 constexpr int kWideQB = 2;                      // 16-query MFMA blocks per wave
 constexpr int kWideWaves = 8;                   // two per SIMD
 constexpr int kWideQ = kWideWaves * 16 * kWideQB;   // queries per launch
+constexpr int kWidePilotRowsDefault = 128;   // the wide pilot's rows per quarter (≥ 512 dims: 256)...
+constexpr int kWidePilotSample = 65536;      // ...raised to sample at least this many rows per shard (≤ 1,024 a quarter)
 constexpr int kAuxGroupF4 = 22;                 // float4 per 16-row group of the tiled bound terms
 int sq8_wide_supported(int units8);
 int sq8_wide_ks(int units8);                    // its 64-dim slabs per row: 2, 4, 8 or 12
