@@ -781,8 +781,8 @@ int32_t osk_view_create(osk_seg* const* segs, int32_t n_segs, const int32_t* seg
     OSK_HIP(v->d_tile_coff.reserve(sizeof(int32_t) * tile_coff.size()));
     OSK_HIP(v->d_tile_order.reserve(sizeof(int32_t) * tile_order.size()));
     OSK_HIP(v->d_seg_vrow.reserve(sizeof(int64_t) * n_segs));
-    OSK_HIP(v->d_counters.reserve(sizeof(unsigned long long) * 16));
-    OSK_HIP(hipMemsetAsync(v->d_counters.p, 0, sizeof(unsigned long long) * 16, st));
+    OSK_HIP(v->d_counters.reserve(sizeof(unsigned long long) * 24));
+    OSK_HIP(hipMemsetAsync(v->d_counters.p, 0, sizeof(unsigned long long) * 24, st));
     OSK_HIP(hipMemcpyAsync(v->d_seg_vrow.p, vrow.data(), sizeof(int64_t) * n_segs, hipMemcpyHostToDevice, st));
     OSK_HIP(hipMemcpyAsync(v->d_segs.p, sd.data(), sizeof(SegDev) * n_segs, hipMemcpyHostToDevice, st));
     if (!tiles.empty())
@@ -2303,7 +2303,8 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
                      n == "sq8_wide_wait_cycles" || n == "sq8_wide_slow_steps" || n == "sq8_wide_loop_cycles" ||
                      n == "sq8_wide_slow_cycles" || n == "sq8_wide_drain_cycles" ||
                      n == "sq6_rebound_gathered_rows" || n == "sq6_rebound_passes" ||
-                     n == "sq6_rebound_max_wg_cycles";
+                     n == "sq6_rebound_max_wg_cycles" || n == "sq8_rows_total_cycles" || n == "sq8_rows_setup_cycles" ||
+                     n == "sq8_rows_quarter_end_cycles" || n == "sq8_rows_first_wait_cycles";
     OSK_REQUIRE(dev || n == "mfma_calls" || n == "mfma_fallback_queries" || n == "sq8_calls" || n == "sq6_calls" ||
                     n == "select_calls" || n == "sq8_wide_calls",
                 "unknown counter: " + n);
@@ -2313,7 +2314,7 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
         std::lock_guard<std::mutex> lk(s->mu);
         if (dev) {
             if (!s->d_counters.p) continue;
-            unsigned long long c[16];
+            unsigned long long c[24];
             OSK_HIP(hipDeviceSynchronize());   // the last search may be on any stream
             OSK_HIP(hipMemcpy(c, s->d_counters.p, sizeof(c), hipMemcpyDeviceToHost));
             // [4] … [8]: the wide kernel's insertion events, quick-test passes, wave 0's shader clocks in the
@@ -2324,7 +2325,12 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
                              : n == "sq8_wide_wait_cycles" ? c[6] : n == "sq8_wide_slow_steps" ? c[7]
                              : n == "sq8_wide_loop_cycles" ? c[8] : n == "sq8_wide_slow_cycles" ? c[9]
                              : n == "sq8_wide_drain_cycles" ? c[10] : n == "sq6_rebound_gathered_rows" ? c[11]
-                             : n == "sq6_rebound_passes" ? c[12] : c[13]);
+                             : n == "sq6_rebound_passes" ? c[12] : n == "sq6_rebound_max_wg_cycles" ? c[13]
+                             // [16] … [19]: sq8_wide_rows, wave 0's shader clocks per workgroup summed: the whole
+                             // kernel, its setup (to the first quarter), the quarter ends (publish, barriers, drain,
+                             // flush, next constants), the waits for each quarter's first group (testing build)
+                             : n == "sq8_rows_total_cycles" ? c[16] : n == "sq8_rows_setup_cycles" ? c[17]
+                             : n == "sq8_rows_quarter_end_cycles" ? c[18] : c[19]);
         } else {
             sum += n == "mfma_calls" ? s->mfma_calls : n == "mfma_fallback_queries" ? s->mfma_fallback_queries
                  : n == "sq8_calls" ? s->sq8_calls : n == "sq6_calls" ? s->sq6_calls

@@ -1269,6 +1269,10 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     // the deferred queues: one per (owner, producer) wave pair, sub = qcap / 8 entries each (qcap per owner:
     // launch_sq8_wide_rows, what LDS leaves; tests less) — a producer appends with its own counter, no atomics
     const int qcap = p.wide_qcap, sub = p.wide_qcap / kWideWaves;
+#ifdef OSK_TESTING
+    const uint64_t t_start = clock64();
+    uint64_t cyc_setup = 0, cyc_qend = 0, cyc_first = 0;
+#endif
 
     // (the fixed-size arrays are static LDS: their addresses are constants, so the hot loop's LDS accesses take
     // immediate offsets instead of address registers; the rings, queues, quarter descriptors and floors are the
@@ -1712,8 +1716,14 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
         }
     };
     int cur = -1;
+#ifdef OSK_TESTING
+    cyc_setup = clock64() - t_start;
+#endif
     for (int q = 0; q < n_mine; ++q) {
         if (groups_of(q) == 0) continue;   // (flushed above)
+#ifdef OSK_TESTING
+        const uint64_t t_q0 = clock64();
+#endif
         // the quarter changes: the last one's drain + flush, this one's constants (two barriers; between them no
         // wave has a DMA in flight, so the lists may overlay the rings)
         if (cur >= 0) {
@@ -1723,6 +1733,9 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
         }
         begin_quarter(s_quart[q]);
         __syncthreads();
+#ifdef OSK_TESTING
+        cyc_qend += clock64() - t_q0;
+#endif
         cur = q;
         c_nrows = __builtin_amdgcn_readfirstlane(s_quart[q].nrows);
         c_ng = (c_nrows + 15) >> 4;
@@ -1740,8 +1753,14 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
                 if (i < n_it) {
                     // slot d's three DMAs have landed (the NR − 1 younger items' may not; at the quarter's tail
                     // fewer are younger: wait for all)
+#ifdef OSK_TESTING
+                    const uint64_t t_w0 = clock64();
+#endif
                     if (i + NR - 1 < n_it) vm_wait<(NR - 1) * 3>();
                     else vm_wait<0>();
+#ifdef OSK_TESTING
+                    if (i == 0) cyc_first += clock64() - t_w0;
+#endif
                     process(d, wave + i * kWideWaves);
                     if (i + NR < n_it) issue(d, wave + (i + NR) * kWideWaves);
                 }
@@ -1750,10 +1769,20 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     }
     vm_wait<0>();   // (no DMA is in flight past a quarter; kept: nothing may land after the workgroup retires)
     // the last quarter's drain and flush
+#ifdef OSK_TESTING
+    const uint64_t t_e0 = clock64();
+#endif
     publish();
     __syncthreads();
     if (cur >= 0) drain_flush(s_quart[cur]);
 #ifdef OSK_TESTING
+    cyc_qend += clock64() - t_e0;
+    if (p.counters && tid == 0) {
+        atomicAdd(&p.counters[16], (unsigned long long)(clock64() - t_start));
+        atomicAdd(&p.counters[17], (unsigned long long)cyc_setup);
+        atomicAdd(&p.counters[18], (unsigned long long)cyc_qend);
+        atomicAdd(&p.counters[19], (unsigned long long)cyc_first);
+    }
     if (p.counters) {
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) n_pairs += __shfl_xor(n_pairs, o);
