@@ -1270,10 +1270,15 @@ int32_t ensure_sq8w(osk_view* v, hipStream_t st) {
         // (≥ 512 dims: quarters of R / (8·CUs), so the first pass — one round of the persistent grid — covers
         // 1/8 of the rows, not 1/2, and the second pass's floors come early; list traffic is small beside
         // rows of ≥ 512 B)
-        const int qdiv = sq8_wide_ks(v->segs.empty() ? 1 : v->segs[0]->units8) >= 8 ? 8 : 2;
+        const int u8w = v->segs.empty() ? 1 : v->segs[0]->units8;
+        const int qdiv = sq8_wide_ks(u8w) >= 8 ? 8 : 2;
+        // (≤ 32,768 rows when the rows kernel takes the main passes: its quarter ends are two barriers and a
+        // flush, so longer quarters pay — C4 b1024 16.42 → 16.05 ms, 8,192 17.67 ms, profiles/r06/tune14.jsonl;
+        // the ring kernel keeps 16,384, round 5's best)
+        const int64_t qmax = (g_tuning.sq8_wide_rows && sq8_wide_rows_supported(u8w)) ? 32768 : 16384;
         const int64_t qr = g_tuning.sq8_wide_quarter_rows > 0
                                ? std::max<int64_t>(16, (int64_t)g_tuning.sq8_wide_quarter_rows & ~15ll)
-                               : std::min<int64_t>(16384, std::max<int64_t>(256, (int64_t)(R / ((double)qdiv * v->n_cus)) + 15 & ~15ll));
+                               : std::min<int64_t>(qmax, std::max<int64_t>(256, (int64_t)(R / ((double)qdiv * v->n_cus)) + 15 & ~15ll));
         const int64_t trows = 4 * qr;
         std::vector<TileDev> wt;
         v->wshard_tile_begin.assign(v->n_shards + 1, 0);
@@ -1748,7 +1753,13 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             p.quarter_end = 0;
             p.floors = nullptr;
             p.quarter_bm = v->d_quarter_bm.as<const float4>();
-            OSK_HIP(launch_sq8_wide(p, st, e0, nullptr));
+            // ≤ 128 dims: the pilot and the main passes without a step barrier (sq8_wide_rows, osk_sq8w.hip)
+            const bool rows = g_tuning.sq8_wide_rows && sq8_wide_rows_supported(u8);
+            p.wide_qcap = rows ? (int)g_tuning.sq8_wide_rows_qcap : 0;
+            if (rows)
+                OSK_HIP(launch_sq8_wide_rows(p, st, e0, nullptr));
+            else
+                OSK_HIP(launch_sq8_wide(p, st, e0, nullptr));
             const int nql = 4 * v->n_wtiles;
             const int32_t* sqb = v->d_shard_quarter_begin.as<int32_t>();
             uint32_t* floor_a = v->ws_wfloor.as<uint32_t>();
@@ -1765,9 +1776,6 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             // would idle the chip, and a partial round leaves a tail)
             const int rounds = std::max(1, (int)std::lround((double)nql / ((double)phase * wgrid)));
             const int n_a = phase > 1 ? std::min(nql / 2, rounds * wgrid) : 0;
-            // ≤ 128 dims: the main passes without a step barrier (sq8_wide_rows, osk_sq8w.hip)
-            const bool rows = g_tuning.sq8_wide_rows && sq8_wide_rows_supported(u8);
-            p.wide_qcap = rows ? (int)g_tuning.sq8_wide_rows_qcap : 0;
             auto main_pass = [&](hipEvent_t ev) {
                 return rows ? launch_sq8_wide_rows(p, st, nullptr, ev) : launch_sq8_wide(p, st, nullptr, ev);
             };
@@ -2304,7 +2312,8 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
                      n == "sq8_wide_slow_cycles" || n == "sq8_wide_drain_cycles" ||
                      n == "sq6_rebound_gathered_rows" || n == "sq6_rebound_passes" ||
                      n == "sq6_rebound_max_wg_cycles" || n == "sq8_rows_total_cycles" || n == "sq8_rows_setup_cycles" ||
-                     n == "sq8_rows_quarter_end_cycles" || n == "sq8_rows_first_wait_cycles";
+                     n == "sq8_rows_quarter_end_cycles" || n == "sq8_rows_first_wait_cycles" ||
+                     n == "sq8_rows_setup_barrier_cycles" || n == "sq8_rows_setup_fragment_cycles";
     OSK_REQUIRE(dev || n == "mfma_calls" || n == "mfma_fallback_queries" || n == "sq8_calls" || n == "sq6_calls" ||
                     n == "select_calls" || n == "sq8_wide_calls",
                 "unknown counter: " + n);
@@ -2330,7 +2339,8 @@ int32_t osk_view_counter(osk_view* v, const char* name, int64_t* value) {
                              // kernel, its setup (to the first quarter), the quarter ends (publish, barriers, drain,
                              // flush, next constants), the waits for each quarter's first group (testing build)
                              : n == "sq8_rows_total_cycles" ? c[16] : n == "sq8_rows_setup_cycles" ? c[17]
-                             : n == "sq8_rows_quarter_end_cycles" ? c[18] : c[19]);
+                             : n == "sq8_rows_quarter_end_cycles" ? c[18] : n == "sq8_rows_first_wait_cycles" ? c[19]
+                             : n == "sq8_rows_setup_barrier_cycles" ? c[20] : c[21]);
         } else {
             sum += n == "mfma_calls" ? s->mfma_calls : n == "mfma_fallback_queries" ? s->mfma_fallback_queries
                  : n == "sq8_calls" ? s->sq8_calls : n == "sq6_calls" ? s->sq6_calls

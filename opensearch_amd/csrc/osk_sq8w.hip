@@ -1246,7 +1246,7 @@ __device__ __forceinline__ const char* rfl_ptr_c(const void* ptr) {
                          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v));
 }
 
-template <int SIM>
+template <int SIM, bool PILOT>
 __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     typedef int i32x4 __attribute__((ext_vector_type(4)));
     constexpr int NQB = kWideQ / 16, NR = kRowsNR, PB = kRowsQB;
@@ -1320,13 +1320,18 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
         d.xt = p.rows8t[tile.seg] + (rb >> 4) * (2 * 64);
         d.at = p.auxt[tile.seg] + (rb >> 4) * kAuxGroupF4;
         d.vrow0 = (uint32_t)(p.seg_vrow[tile.seg] + rb);
-        d.nrows = (int32_t)(re - rb);
+        // (the pilot: the quarter's first rows only)
+        d.nrows = (int32_t)(PILOT ? min<int64_t>(p.pilot_rows > 0 ? p.pilot_rows : kWidePilotRows, re - rb) : re - rb);
         d.list = tix * 4 + quarter;
         d.shard = tile.shard;
         d.seg = tile.seg;
-        d.bm = p.quarter_bm[d.list];
+        d.bm = PILOT ? make_float4(0.f, 0.f, 0.f, 0.f) : p.quarter_bm[d.list];
         s_quart[i] = d;
     }
+    // the pilot's per-query best key of the current quarter (the queues' LDS: the pilot has none)
+    uint64_t* s_pk = reinterpret_cast<uint64_t*>(s_q);
+    if (PILOT)
+        for (int i = tid; i < kWideQ; i += kWideThreads) s_pk[i] = 0ull;
     // the launch's query fragments: query block qb, slab s (lane: query qb·16 + col, 16-B unit 4s + grp)
     i32x4 bfr[2][NQB];
 #pragma unroll
@@ -1346,14 +1351,32 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
         return floor_lds ? s_floor[sh * kWideQ + qi] : ((!c.floors || qi >= c.q_count) ? 0u : c.floors[(size_t)qi * S + sh]);
     };
     __syncthreads();   // lists zeroed; s_qc, s_qnd, the floors and the quarter descriptors written
+#ifdef OSK_TESTING
+    const uint64_t t_bar = clock64();
+#endif
 #pragma unroll
     for (int qb = 0; qb < NQB; ++qb)
 #pragma unroll
         for (int s = 0; s < 2; ++s) asm volatile("" ::"v"(bfr[s][qb]));
+#ifdef OSK_TESTING
+    const uint64_t t_frag = clock64();
+#endif
 
     // ---- the quarter-end work: drain this wave's queue into its queries' lists, then flush them ----
     auto drain_flush = [&](const WideQuarter& d) {
         const WideCold& c = s_cold;
+        if constexpr (PILOT) {   // the quarter's best key per query → pilot_keys; its list maximum zeroed (the
+                                 // two-pass main pass reads the second pass's lists as empty until it writes them)
+            if (lane < 32) {
+                const int qi = wq0 + lane;
+                if (qi < c.q_count) {
+                    c.pilot_keys[(size_t)qi * c.n_quarters + d.list] = s_pk[qi];
+                    c.list_lbmax[(size_t)(c.q0 + qi) * c.n_lists + d.list] = 0u;
+                }
+                s_pk[qi] = 0ull;
+            }
+            return;
+        }
         const int sh = d.shard;
         for (int i = lane; i < 32 * kKQ; i += 64) {   // this wave's queries' lists (ring memory: zero them first)
             s_lk[wq0 * kKQ + i] = 0ull;
@@ -1466,7 +1489,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     };
     // ---- a quarter starts: its quick-test constants for every query, each wave its own 32 (lanes 0..31) ----
     auto begin_quarter = [&](const WideQuarter& d) {
-        if (lane < 32) {
+        if (!PILOT && lane < 32) {
             const int oq = wq0 + lane;
             float ca, cb = 0.0f;
             if (oq < s_cold.q_count) {
@@ -1518,6 +1541,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     const int4* c_xt = nullptr;
     const float4* c_at = nullptr;
     int c_ng = 0, c_nrows = 0;   // (the quarter's groups and rows, in SGPRs)
+    uint32_t c_vrow0 = 0;        // (the pilot: the quarter's first view row)
     // group g's DMAs into slot d — the two 1 KiB slabs (lane-linear: the A operand), and 5 bound-term float4:
     // lanes 0–3 the rows' |x|² (EUCLIDEAN, slots 12–15) or per-row factors (COSINE, slots 0–3), lane 4 slot 17
     // {s_g, f_cos, zero-row flag, 0}: three DMA instructions
@@ -1541,6 +1565,69 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     };
     // ... and group g's work, its data in slot d
     auto process = [&](int d, int g) {
+        if constexpr (PILOT) {
+            // per query block: the lane's 4 rows' dots, its row with the best approximate score bounded
+            // precisely (sq8_bounds, as the drain does), the best of the group's 16 rows per query (grp lanes)
+            // → an LDS max per query over the quarter's groups
+            const int r0 = 16 * g, nr = min(16, c_nrows - r0);
+            const char* sl = ring + d * kRowsSlot;
+            const i32x4 A0 = *reinterpret_cast<const i32x4*>(sl + lane * 16);
+            const i32x4 A1 = *reinterpret_cast<const i32x4*>(sl + 1024 + lane * 16);
+            const float4* ag = c_at + (size_t)g * kAuxGroupF4;   // (the group's full terms, from L2 / HBM)
+            const float sg = *reinterpret_cast<const float*>(sl + 2048 + 64);
+            const float4 ta = SIM == SIM_COSINE ? make_float4(sg, sg, sg, sg) : ag[grp];
+            const float4 ty = ag[4 + grp], tz = ag[8 + grp], tw = ag[12 + grp];
+            const float4 tx = SIM == SIM_COSINE ? ag[18 + grp] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float fa[4] = {ta.x, ta.y, ta.z, ta.w}, fy[4] = {ty.x, ty.y, ty.z, ty.w};
+            const float fz[4] = {tz.x, tz.y, tz.z, tz.w}, fw[4] = {tw.x, tw.y, tw.z, tw.w};
+            const float fx[4] = {tx.x, tx.y, tx.z, tx.w};
+#pragma unroll
+            for (int h = 0; h < NQB / PB; ++h) {
+                i32x4 acc[PB];
+#pragma unroll
+                for (int j = 0; j < PB; ++j)
+                    acc[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0, bfr[0][h * PB + j], i32x4{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+                for (int j = 0; j < PB; ++j)
+                    acc[j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1, bfr[1][h * PB + j], acc[j], 0, 0, 0);
+#pragma unroll
+                for (int j = 0; j < PB; ++j) {
+                    const int qi = (h * PB + j) * 16 + col;
+                    const float4 qc = s_qc[qi];
+                    int rb = 0, ib = acc[j][0];
+                    float vb = -__builtin_inff(), ab = fa[0], yb = fy[0], zb = fz[0], wb = fw[0], xb = fx[0];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float ia = (float)acc[j][r] * fa[r];
+                        float v = SIM == SIM_EUCLIDEAN ? fmaf(2.0f * ia, qc.x, -fw[r]) : ia;
+                        if (!(4 * grp + r < nr)) v = -__builtin_inff();
+                        const bool take = v > vb;
+                        vb = take ? v : vb;
+                        rb = take ? r : rb;
+                        ib = take ? acc[j][r] : ib;
+                        ab = take ? fa[r] : ab;
+                        yb = take ? fy[r] : yb;
+                        zb = take ? fz[r] : zb;
+                        wb = take ? fw[r] : wb;
+                        xb = take ? fx[r] : xb;
+                    }
+                    float lo, hi;
+                    sq8_bounds(sim, (float)ib, make_float4(ab, yb, zb, wb), qc, s_cold.gam, s_cold.g2, lo, hi);
+                    const float lb = SIM == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, s_qnd[qi], xb);
+                    uint64_t key = (vb > -__builtin_inff() && qi < s_cold.q_count)
+                                       ? make_key(lb, c_vrow0 + (uint32_t)(r0 + 4 * grp + rb)) : 0ull;
+#pragma unroll
+                    for (int o = 16; o <= 32; o <<= 1) {
+                        const uint64_t other = ((uint64_t)(uint32_t)__shfl_xor((int)(key >> 32), o) << 32) |
+                                               (uint32_t)__shfl_xor((int)(uint32_t)key, o);
+                        key = other > key ? other : key;
+                    }
+                    if (grp == 0 && key) atomicMax(reinterpret_cast<unsigned long long*>(&s_pk[qi]),
+                                                   (unsigned long long)key);
+                }
+            }
+            return;
+        }
         if (!(ablate & 1)) {
             const int r0 = 16 * g, nr = min(16, c_nrows - r0);
             // every LDS read of the item at once (one wait): the A operand, the group's terms, the query constants
@@ -1738,6 +1825,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
 #endif
         cur = q;
         c_nrows = __builtin_amdgcn_readfirstlane(s_quart[q].nrows);
+        if (PILOT) c_vrow0 = __builtin_amdgcn_readfirstlane(s_quart[q].vrow0);
         c_ng = (c_nrows + 15) >> 4;
         c_xt = reinterpret_cast<const int4*>(rfl_ptr_c(s_quart[q].xt));
         c_at = reinterpret_cast<const float4*>(rfl_ptr_c(s_quart[q].at));
@@ -1777,11 +1865,13 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     if (cur >= 0) drain_flush(s_quart[cur]);
 #ifdef OSK_TESTING
     cyc_qend += clock64() - t_e0;
-    if (p.counters && tid == 0) {
+    if (!PILOT && p.counters && tid == 0) {
         atomicAdd(&p.counters[16], (unsigned long long)(clock64() - t_start));
         atomicAdd(&p.counters[17], (unsigned long long)cyc_setup);
         atomicAdd(&p.counters[18], (unsigned long long)cyc_qend);
         atomicAdd(&p.counters[19], (unsigned long long)cyc_first);
+        atomicAdd(&p.counters[20], (unsigned long long)(t_bar - t_start));   // setup: to the first barrier
+        atomicAdd(&p.counters[21], (unsigned long long)(t_frag - t_bar));    // then the fragments' arrival
     }
     if (p.counters) {
 #pragma unroll
@@ -1813,7 +1903,10 @@ static size_t sq8_wide_lds(int ks, int sim, int n_shards, int n_mine) {
 }
 
 using RowsFn = void (*)(Sq8Params);
-static const RowsFn kWideRows[4] = {sq8_wide_rows<0>, sq8_wide_rows<1>, sq8_wide_rows<2>, sq8_wide_rows<3>};
+static const RowsFn kWideRows[2][4] = {{sq8_wide_rows<0, false>, sq8_wide_rows<1, false>, sq8_wide_rows<2, false>,
+                                        sq8_wide_rows<3, false>},
+                                       {sq8_wide_rows<0, true>, sq8_wide_rows<1, true>, sq8_wide_rows<2, true>,
+                                        sq8_wide_rows<3, true>}};
 // dynamic LDS: the rings, the quarter descriptors and the floors (+ the queues, sized from what is left); the rest
 // is static, kRowsStatic bytes
 static size_t sq8_wide_rows_lds(int n_shards, int n_mine) {
@@ -1841,12 +1934,13 @@ bool sq8_wide_rows_supported(int u8) { return sq8_wide_supported(u8) && sq8_wide
 hipError_t launch_sq8_wide_rows(const Sq8Params& p, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
     if (!sq8_wide_rows_supported(p.units8) || p.q_count < 1 || p.q_count > kWideQ || p.accept || p.gtiles ||
         p.sim < 0 || p.sim > 3 || !p.rows8t || !p.auxt || p.n_lists != 4 * p.n_tiles || p.k < 1 || p.k > kKQ ||
-        p.n_shards < 1 || p.wide_grid < 1 || p.pilot || !p.quarter_bm)
+        p.n_shards < 1 || p.wide_grid < 1 || (p.pilot && !p.pilot_keys) || (!p.pilot && !p.quarter_bm))
         return hipErrorInvalidValue;
     const int nq4 = (p.quarter_end > 0 ? p.quarter_end : 4 * p.n_tiles) - p.quarter_begin;
-    if (p.quarter_begin < 0 || nq4 < 1 || p.quarter_begin + nq4 > 4 * p.n_tiles) return hipErrorInvalidValue;
+    if (p.quarter_begin < 0 || nq4 < 1 || p.quarter_begin + nq4 > 4 * p.n_tiles || (p.quarter_begin && p.pilot))
+        return hipErrorInvalidValue;
     int grid = std::min(p.wide_grid, std::max(1, nq4));
-    const auto fn = kWideRows[p.sim];
+    const auto fn = kWideRows[p.pilot ? 1 : 0][p.sim];
     const size_t cap = 160 * 1024 - kernel_static_lds(reinterpret_cast<const void*>(fn));
     while (sq8_wide_rows_lds(p.n_shards, (nq4 + grid - 1) / grid) + (size_t)kWideWaves * kRowsMinQcap * sizeof(uint2) >
            cap)

@@ -64,7 +64,8 @@ for ab in [int(x) for x in os.environ.get("ABLATE", "0,1,2,3").split(",")]:
     x0 = [counter(c) for c in ("sq8_fallback_queries", "sq8_exact_tiles", "sq8_rescored_rows")]
     cyc0 = [counter("sq8_wide_" + c + "_cycles") for c in ("wait", "loop", "slow", "drain")]
     slow0 = counter("sq8_wide_slow_steps")
-    rows0 = [counter("sq8_rows_" + c + "_cycles") for c in ("total", "setup", "quarter_end", "first_wait")]
+    RC = ("total", "setup", "quarter_end", "first_wait", "setup_barrier", "setup_fragment")
+    rows0 = [counter("sq8_rows_" + c + "_cycles") for c in RC]
     check(lib().osk_view_profile(shards.view, 1))
     n = 5
     for _ in range(n):
@@ -91,11 +92,12 @@ for ab in [int(x) for x in os.environ.get("ABLATE", "0,1,2,3").split(",")]:
     print(f"   clocks per wg-launch (wave 0): loop {cyc[1] / wgs:.0f}, wait+barrier {cyc[0] / wgs:.0f} "
           f"({cyc[0] / max(1, cyc[1]):.2f}), slow-path enqueues {cyc[2] / wgs:.0f} ({cyc[2] / max(1, cyc[1]):.2f}), "
           f"quarter-end drains + flushes {cyc[3] / wgs:.0f} ({cyc[3] / max(1, cyc[1]):.2f})", flush=True)
-    rows = [counter("sq8_rows_" + c + "_cycles") - c0 for c0, c in zip(rows0, ("total", "setup", "quarter_end", "first_wait"))]
+    rows = [counter("sq8_rows_" + c + "_cycles") - c0 for c0, c in zip(rows0, RC)]
     if rows[0]:   # sq8_wide_rows (main passes): wave 0 per workgroup-launch, 2 launches per search
         rw = 256 * 2 * n
         print(f"   sq8_wide_rows clocks per wg-launch (wave 0): total {rows[0] / rw:.0f}, setup {rows[1] / rw:.0f}, "
-              f"quarter ends {rows[2] / rw:.0f}, first-group waits {rows[3] / rw:.0f}", flush=True)
+              f"quarter ends {rows[2] / rw:.0f}, first-group waits {rows[3] / rw:.0f} (setup: to the barrier "
+              f"{rows[4] / rw:.0f}, then the fragments {rows[5] / rw:.0f})", flush=True)
 if not SHIPPED:
     _lib.tune("sq8_mfma_ablate", 0)
 shards.close()
