@@ -1272,10 +1272,10 @@ int32_t ensure_sq8w(osk_view* v, hipStream_t st) {
         // rows of ≥ 512 B)
         const int u8w = v->segs.empty() ? 1 : v->segs[0]->units8;
         const int qdiv = sq8_wide_ks(u8w) >= 8 ? 8 : 2;
-        // (≤ 32,768 rows when the rows kernel takes the main passes: its quarter ends are two barriers and a
-        // flush, so longer quarters pay — C4 b1024 16.42 → 16.05 ms, 8,192 17.67 ms, profiles/r06/tune14.jsonl;
-        // the ring kernel keeps 16,384, round 5's best)
-        const int64_t qmax = (g_tuning.sq8_wide_rows && sq8_wide_rows_supported(u8w)) ? 32768 : 16384;
+        // (≤ 16,384 rows, round 5's best for the ring kernel; the rows kernel ran C4 b1024 in 16.05 ms at 32,768
+        // against 16.42 (profiles/r06/tune14.jsonl) but a first-pass quarter that long can fill a queue: one C4
+        // query in 256 took an exact re-scan, profiles/r06/rows_clocks_c4_b256_q32768.log)
+        const int64_t qmax = 16384;
         const int64_t qr = g_tuning.sq8_wide_quarter_rows > 0
                                ? std::max<int64_t>(16, (int64_t)g_tuning.sq8_wide_quarter_rows & ~15ll)
                                : std::min<int64_t>(qmax, std::max<int64_t>(256, (int64_t)(R / ((double)qdiv * v->n_cus)) + 15 & ~15ll));

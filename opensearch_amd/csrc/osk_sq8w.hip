@@ -1266,9 +1266,12 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     const int qbeg = p.quarter_begin, n_range = (p.quarter_end > 0 ? p.quarter_end : n_quarters) - qbeg;
     const int n_mine = (int)blockIdx.x < n_range ? (n_range - 1 - (int)blockIdx.x) / G + 1 : 0;
     const bool floor_lds = S <= kRowsMaxFloorShards;
-    // the deferred queues: one per (owner, producer) wave pair, sub = qcap / 8 entries each (qcap per owner:
-    // launch_sq8_wide_rows, what LDS leaves; tests less) — a producer appends with its own counter, no atomics
-    const int qcap = p.wide_qcap, sub = p.wide_qcap / kWideWaves;
+    // the deferred queues, qcap entries per owner wave (launch_sq8_wide_rows: what LDS leaves; tests less): one
+    // sub-queue per (owner, producer) wave pair, sub = qcap / 16 entries each, which a producer appends to at
+    // its own count (no atomics), and the other half a pool per owner for what a producer's sub-queue cannot
+    // hold (one LDS atomic per overflowing event) — a heavy quarter for one producer no longer drops entries
+    // while the owner's other sub-queues stand empty
+    const int qcap = p.wide_qcap, sub = p.wide_qcap / (2 * kWideWaves), pool = p.wide_qcap - kWideWaves * sub;
 #ifdef OSK_TESTING
     const uint64_t t_start = clock64();
     uint64_t cyc_setup = 0, cyc_qend = 0, cyc_first = 0;
@@ -1286,13 +1289,14 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     __shared__ int32_t s_cnt[kWideQ];                      // list fill
     __shared__ int32_t s_ovf[kWideQ];                      // queue overflowed this quarter
     __shared__ int32_t s_qn[kWideWaves * kWideWaves];      // [owner][producer] queue fill (published at quarter end)
+    __shared__ int32_t s_qo[kWideWaves];                   // [owner] pool fill
     char* s_ring = smem;                                                                   // [8 waves][NR] slots
     // the lists [kWideQ][kKQ] keys + lower bounds (48 KB) overlay the rings: they live only in the quarter-end
     // drain and flush, when no DMA is in flight (a quarter's items are issued inside the quarter only)
     uint64_t* s_lk = reinterpret_cast<uint64_t*>(smem);
     uint32_t* s_lp = reinterpret_cast<uint32_t*>(s_lk + kWideQ * kKQ);
     WideQuarter* s_quart = reinterpret_cast<WideQuarter*>(smem + kWideWaves * NR * kRowsSlot);   // [n_mine]
-    uint2* s_q = reinterpret_cast<uint2*>(s_quart + n_mine);                             // [8 owners][8][sub]
+    uint2* s_q = reinterpret_cast<uint2*>(s_quart + n_mine);                             // [8 owners][8 × sub + pool]
     uint32_t* s_floor = reinterpret_cast<uint32_t*>(s_q + kWideWaves * qcap);           // [S][kWideQ] (S ≤ 8)
     if (tid == 0) s_cold = WideCold{p.cand, p.cand_lb, p.list_lbmax, p.visited, p.qn_dev, p.pilot_keys, p.floors, p.q0,
                                     p.n_lists, p.q_count, 4 * p.n_tiles, p.cos_slack, p.gam, p.g2};
@@ -1303,6 +1307,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
         s_qnd[i] = (SIM == SIM_COSINE && i < p.q_count) ? p.qn_dev[i] : 0.0f;
     }
     if (tid < kWideWaves * kWideWaves) s_qn[tid] = 0;
+    if (tid < kWideWaves) s_qo[tid] = 0;
     if (floor_lds)
         for (int i = tid; i < S * kWideQ; i += kWideThreads) {
             const int qi = i % kWideQ;
@@ -1389,7 +1394,8 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
 #pragma unroll
         for (int pw = 0; pw < kWideWaves; ++pw)
             off[pw + 1] = off[pw] + min(__builtin_amdgcn_readfirstlane(s_qn[wave * kWideWaves + pw]), sub);
-        const int n = off[kWideWaves];
+        const int n_sub = off[kWideWaves];
+        const int n = n_sub + min(__builtin_amdgcn_readfirstlane(s_qo[wave]), pool);   // (then the pool's)
         const uint2* q = s_q + (size_t)wave * qcap;
         for (int i0 = 0; i0 < n; i0 += 64) {
             const int e = i0 + lane;
@@ -1397,7 +1403,8 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
             int pw = 0;
 #pragma unroll
             for (int w = 1; w < kWideWaves; ++w) pw += e >= off[w];
-            const uint2 en = ok ? q[pw * sub + (e - off[pw])] : make_uint2(0u, 0u);
+            const int qx = e < n_sub ? pw * sub + (e - off[pw]) : kWideWaves * sub + (e - n_sub);
+            const uint2 en = ok ? q[qx] : make_uint2(0u, 0u);
             const int qi = (int)(en.y & 255u), rowq = (int)(en.y >> 8);
             const float* af = reinterpret_cast<const float*>(d.at + (rowq >> 4) * kAuxGroupF4);
             const int rr = rowq & 15;
@@ -1484,6 +1491,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
             }
         }
         if (lane < kWideWaves) s_qn[wave * kWideWaves + lane] = 0;
+        if (lane == 0) s_qo[wave] = 0;
         if (c.visited && c.q0 == 0 && tid == 0 && d.nrows > 0)
             atomicAdd(&c.visited[d.seg], (unsigned long long)d.nrows);
     };
@@ -1776,9 +1784,19 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
                         }
                         if (!tot) continue;
                         const int owner = qb >> 1;   // (queries qb·16 … qb·16 + 15 belong to wave qb / 2)
-                        int base = q_cnt[owner];     // (this wave's sub-queue of the owner: no other writer)
+                        const int own0 = q_cnt[owner];   // (this wave's sub-queue of the owner: no other writer)
+                        int base = own0;
                         q_cnt[owner] += tot;
                         uint2* oq_ = s_q + (size_t)owner * qcap + (size_t)wave * sub;
+                        // what the sub-queue cannot hold goes to the owner's pool, in the event's order
+                        const int n_over = tot - min(tot, max(0, sub - own0));
+                        int pbase = 0;
+                        if (n_over) {
+                            if (lane == 0) pbase = atomicAdd(&s_qo[owner], n_over);
+                            pbase = __builtin_amdgcn_readfirstlane(pbase);
+                        }
+                        const int ovf0 = max(own0, sub);   // (the slot of the event's first pool entry)
+                        uint2* pq_ = s_q + (size_t)owner * qcap + (size_t)kWideWaves * sub;
                         bool dropped = false;
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
@@ -1786,8 +1804,12 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)b[r], 0u));
                             const int slot = base + below;
                             if (pr[r]) {
+                                const uint2 en = make_uint2((uint32_t)acc[j][r], (uint32_t)(r0 + 4 * ogrp + r) << 8 | (uint32_t)qi);
+                                const int ps = pbase + (slot - ovf0);
                                 if (slot < sub)
-                                    oq_[slot] = make_uint2((uint32_t)acc[j][r], (uint32_t)(r0 + 4 * ogrp + r) << 8 | (uint32_t)qi);
+                                    oq_[slot] = en;
+                                else if (ps < pool)
+                                    pq_[ps] = en;
                                 else
                                     dropped = true;
                             }
