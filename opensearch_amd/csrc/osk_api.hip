@@ -1321,6 +1321,12 @@ int32_t ensure_sq8w(osk_view* v, hipStream_t st) {
         OSK_HIP(v->d_quarter_bm.reserve(sizeof(float4) * 4 * std::max<size_t>(1, wt.size())));
         OSK_HIP(launch_wide_quarter_max(v->d_wtiles.as<TileDev>(), v->n_wtiles, v->d_sq8_auxt.as<const float4*>(),
                                         v->d_quarter_bm.as<float4>(), st));
+        // the quarters' descriptors, read by every workgroup's setup instead of recomputed (64 B each)
+        OSK_HIP(v->d_wqtable.reserve((size_t)64 * 4 * std::max<size_t>(1, wt.size())));
+        OSK_HIP(launch_wide_quarter_table(v->d_wtiles.as<TileDev>(), v->d_wtile_order.as<int32_t>(), 4 * v->n_wtiles,
+                                          sq8_wide_ks(u8w), v->d_sq8_rows_w.p, v->d_sq8_auxt.p,
+                                          v->d_seg_vrow.as<int64_t>(), v->d_quarter_bm.as<const float4>(),
+                                          v->d_wqtable.p, st));
     }
     OSK_HIP(hipStreamSynchronize(st));
     v->sq8w_ready = true;
@@ -1753,6 +1759,7 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             p.quarter_end = 0;
             p.floors = nullptr;
             p.quarter_bm = v->d_quarter_bm.as<const float4>();
+            p.wide_qtable = v->d_wqtable.p;
             // ≤ 128 dims: the pilot and the main passes without a step barrier (sq8_wide_rows, osk_sq8w.hip)
             const bool rows = g_tuning.sq8_wide_rows && sq8_wide_rows_supported(u8);
             p.wide_qcap = rows ? (int)g_tuning.sq8_wide_rows_qcap : 0;

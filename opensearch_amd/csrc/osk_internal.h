@@ -192,6 +192,7 @@ struct Sq8Params {
     int wide_qcap;                   // (set by launch_sq8_wide: entries per wave's deferred queue, 0 = immediate)
     const uint32_t* floors;          // sq8_wide: [q_count][n_shards] floor score (sortable bits; 0 = none)
     const float4* quarter_bm;        // sq8_wide: [4·n_tiles] the quarters' row maxima (launch_wide_quarter_max)
+    const void* wide_qtable;         // sq8_wide: [4·n_tiles] the quarters' descriptors in tile order (null: computed)
 };
 
 struct SettleParams {
@@ -390,6 +391,9 @@ hipError_t launch_wide_quarter_max(const TileDev* tiles, int n_tiles, const floa
 // shard's pilot keys (pilot_keys [nq][n_lists], one per quarter) or of its lists' maximum lower bounds
 // (list_lbmax [nq][n_lists]; 0 = not written); the shard's quarters / lists are [shard_list_begin[s], [s + 1]).
 // Sortable score bits; a floor at or below score 0 is dropped (ties at the clamp).
+hipError_t launch_wide_quarter_table(const TileDev* tiles, const int32_t* tile_order, int n_q, int ks,
+                                     const void* rows8t, const void* auxt, const int64_t* seg_vrow,
+                                     const float4* quarter_bm, void* out, hipStream_t s);
 hipError_t launch_wide_floor(const uint32_t* list_lbmax, const uint64_t* pilot_keys, int n_lists,
                              const int32_t* shard_list_begin, int n_shards, int nq, int k, const uint32_t* base,
                              uint32_t* floors, hipStream_t s);

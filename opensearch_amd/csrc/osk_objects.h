@@ -190,6 +190,7 @@ struct osk_view {
     osk::DevBuf d_sq8_rows_w;                         // per segment: the wide kernel's group-scaled copy
     osk::DevBuf d_sq8_auxt, d_shard_quarter_begin;    // per segment: its tiled bound terms (sq8_wide); 4·shard_tile_begin
     osk::DevBuf d_quarter_bm;                         // per (wide tile, quarter): its rows' bound-term maxima
+    osk::DevBuf d_wqtable;                            // per quarter in tile order: the wide kernels' descriptor
     // sq8_wide's own tiles (ensure_sq8w: quarters of ≈ R / (2·CUs) rows), their shard ranges and dispatch order
     osk::DevBuf d_wtiles, d_wtile_order, d_wshard_tile_begin;
     std::vector<int32_t> wshard_tile_begin;

@@ -308,6 +308,54 @@ struct WideQuarter {
     int32_t pad[3];
     float4 bm;            // the quarter's row maxima {max s|q|, max |δ|, max |x|², min |x|²} (launch_wide_quarter_max)
 };
+static_assert(sizeof(WideQuarter) == 64, "one 64-B descriptor per quarter");
+
+// Quarter j of the tile order (4 per wide tile): its rows, copy pointers and maxima.  The wide kernels read it
+// from the view's table (launch_wide_quarter_table, built once with the tile table): computing it at launch
+// took three dependent global loads (tile order → tile → the segment's pointers) in every workgroup's setup.
+__device__ __forceinline__ WideQuarter wide_quarter_of(const TileDev* __restrict__ tiles,
+                                                       const int32_t* __restrict__ tile_order, int j, int ks,
+                                                       const int4* const* __restrict__ rows8t,
+                                                       const float4* const* __restrict__ auxt,
+                                                       const int64_t* __restrict__ seg_vrow,
+                                                       const float4* __restrict__ quarter_bm) {
+    const int tix = tile_order ? tile_order[j >> 2] : j >> 2, quarter = j & 3;
+    const TileDev tile = tiles[tix];
+    const int64_t trows = tile.row_end - tile.row_begin;
+    const int64_t spw = ((trows + 4 * kMfmaScanR - 1) / (4 * kMfmaScanR)) * kMfmaScanR;
+    const int64_t rb = min(tile.row_begin + quarter * spw, tile.row_end);
+    const int64_t re = min(rb + spw, tile.row_end);
+    WideQuarter d;
+    d.xt = rows8t[tile.seg] + (rb >> 4) * (ks * 64);
+    d.at = auxt[tile.seg] + (rb >> 4) * kAuxGroupF4;
+    d.vrow0 = (uint32_t)(seg_vrow[tile.seg] + rb);
+    d.nrows = (int32_t)(re - rb);
+    d.list = tix * 4 + quarter;
+    d.shard = tile.shard;
+    d.seg = tile.seg;
+    d.pad[0] = d.pad[1] = d.pad[2] = 0;
+    d.bm = quarter_bm ? quarter_bm[d.list] : make_float4(0.f, 0.f, 0.f, 0.f);
+    return d;
+}
+__global__ __launch_bounds__(kBlock) void wide_quarter_table(const TileDev* __restrict__ tiles,
+                                                             const int32_t* __restrict__ tile_order, int n_q, int ks,
+                                                             const int4* const* __restrict__ rows8t,
+                                                             const float4* const* __restrict__ auxt,
+                                                             const int64_t* __restrict__ seg_vrow,
+                                                             const float4* __restrict__ quarter_bm,
+                                                             WideQuarter* __restrict__ out) {
+    const int j = blockIdx.x * kBlock + threadIdx.x;
+    if (j < n_q) out[j] = wide_quarter_of(tiles, tile_order, j, ks, rows8t, auxt, seg_vrow, quarter_bm);
+}
+hipError_t launch_wide_quarter_table(const TileDev* tiles, const int32_t* tile_order, int n_q, int ks,
+                                     const void* rows8t, const void* auxt, const int64_t* seg_vrow,
+                                     const float4* quarter_bm, void* out, hipStream_t s) {
+    if (n_q < 1) return hipSuccess;
+    hipLaunchKernelGGL(wide_quarter_table, dim3((n_q + kBlock - 1) / kBlock), dim3(kBlock), 0, s, tiles, tile_order,
+                       n_q, ks, static_cast<const int4* const*>(rows8t), static_cast<const float4* const*>(auxt),
+                       seg_vrow, quarter_bm, static_cast<WideQuarter*>(out));
+    return hipGetLastError();
+}
 // The parameters only the cold paths use (quarter-end flushes and drains, list overflows, the pilot's key
 // stores), held in LDS: read from there they are not live across the step loop, whose hot values then keep
 // their SGPRs instead of spilling to VGPR lanes.
@@ -407,22 +455,10 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide(Sq8Params p) {
         for (int i = tid; i < S * kWideQ; i += kWideThreads) s_floor[i] = floor_of(i % kWideQ, i / kWideQ);
     for (int i = tid; i < n_mine; i += kWideThreads) {
         const int j = qbeg + (int)blockIdx.x + i * G;
-        const int tix = p.tile_order ? p.tile_order[j >> 2] : j >> 2, quarter = j & 3;
-        const TileDev tile = p.tiles[tix];
-        const int64_t trows = tile.row_end - tile.row_begin;
-        const int64_t spw = ((trows + 4 * kMfmaScanR - 1) / (4 * kMfmaScanR)) * kMfmaScanR;
-        const int64_t rb = min(tile.row_begin + quarter * spw, tile.row_end);
-        const int64_t re = min(rb + spw, tile.row_end);
-        WideQuarter d;
-        d.xt = p.rows8t[tile.seg] + (rb >> 4) * (KS * 64);
-        d.at = p.auxt[tile.seg] + (rb >> 4) * kAuxGroupF4;
-        d.vrow0 = (uint32_t)(p.seg_vrow[tile.seg] + rb);
-        d.nrows = (int32_t)(pilot ? min<int64_t>(p.pilot_rows > 0 ? p.pilot_rows : kWidePilotRows, re - rb)
-                                  : re - rb);   // the pilot: its first rows
-        d.list = tix * 4 + quarter;
-        d.shard = tile.shard;
-        d.seg = tile.seg;
-        d.bm = p.quarter_bm ? p.quarter_bm[d.list] : make_float4(0.f, 0.f, 0.f, 0.f);
+        WideQuarter d = p.wide_qtable ? static_cast<const WideQuarter*>(p.wide_qtable)[j]
+                                      : wide_quarter_of(p.tiles, p.tile_order, j, KS, p.rows8t, p.auxt, p.seg_vrow,
+                                                        p.quarter_bm);
+        if (pilot) d.nrows = min(d.nrows, p.pilot_rows > 0 ? p.pilot_rows : kWidePilotRows);   // its first rows
         s_quart[i] = d;
     }
 
@@ -1315,22 +1351,10 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
         }
     for (int i = tid; i < n_mine; i += kWideThreads) {
         const int j = qbeg + (int)blockIdx.x + i * G;
-        const int tix = p.tile_order ? p.tile_order[j >> 2] : j >> 2, quarter = j & 3;
-        const TileDev tile = p.tiles[tix];
-        const int64_t trows = tile.row_end - tile.row_begin;
-        const int64_t spw = ((trows + 4 * kMfmaScanR - 1) / (4 * kMfmaScanR)) * kMfmaScanR;
-        const int64_t rb = min(tile.row_begin + quarter * spw, tile.row_end);
-        const int64_t re = min(rb + spw, tile.row_end);
-        WideQuarter d;
-        d.xt = p.rows8t[tile.seg] + (rb >> 4) * (2 * 64);
-        d.at = p.auxt[tile.seg] + (rb >> 4) * kAuxGroupF4;
-        d.vrow0 = (uint32_t)(p.seg_vrow[tile.seg] + rb);
-        // (the pilot: the quarter's first rows only)
-        d.nrows = (int32_t)(PILOT ? min<int64_t>(p.pilot_rows > 0 ? p.pilot_rows : kWidePilotRows, re - rb) : re - rb);
-        d.list = tix * 4 + quarter;
-        d.shard = tile.shard;
-        d.seg = tile.seg;
-        d.bm = PILOT ? make_float4(0.f, 0.f, 0.f, 0.f) : p.quarter_bm[d.list];
+        WideQuarter d = p.wide_qtable ? static_cast<const WideQuarter*>(p.wide_qtable)[j]
+                                      : wide_quarter_of(p.tiles, p.tile_order, j, 2, p.rows8t, p.auxt, p.seg_vrow,
+                                                        p.quarter_bm);
+        if (PILOT) d.nrows = min(d.nrows, p.pilot_rows > 0 ? p.pilot_rows : kWidePilotRows);   // (its first rows)
         s_quart[i] = d;
     }
     // the pilot's per-query best key of the current quarter (the queues' LDS: the pilot has none)

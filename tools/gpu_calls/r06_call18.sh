@@ -1,5 +1,5 @@
 # round 6: the rows kernel's queues with a shared pool per owner (no drops when one producer's sub-queue fills),
-# quarters back to ≤ 16,384 rows — wide / NaN / at-size tests and the full-size C4 tests (fallback-free asserts),
+# quarters back to ≤ 16,384 rows, per-view quarter descriptor table — wide / NaN / at-size tests and the full-size C4 tests (fallback-free asserts),
 # the batched configs, C4's clocks and counters
 set -u
 cd $GRAFT_REPO_ROOT
