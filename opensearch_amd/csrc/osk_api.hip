@@ -329,6 +329,7 @@ int32_t osk_tune_set(const char* key, int64_t value) {
         {"sq8_wide_rows", &g_tuning.sq8_wide_rows, 0, 1, false},
         {"sq8_wide_rows_qcap", &g_tuning.sq8_wide_rows_qcap, 0, 1 << 20, false},
         {"sq8_scan_deep", &g_tuning.sq8_scan_deep, 0, 1, false},
+        {"sq8_wide_rows_claim", &g_tuning.sq8_wide_rows_claim, 0, 1, false},
         {"sq6_rebound_stride", &g_tuning.sq6_rebound_stride, 0, 1, false},
         {"sq6_rebound_retest", &g_tuning.sq6_rebound_retest, 0, 1, false},
         {"sq6_rebound_wgs", &g_tuning.sq6_rebound_wgs, 0, 16, false},
@@ -1760,6 +1761,7 @@ int32_t sq8_search(osk_view* v, const void* d_queries, int nq, int k, int UP, co
             p.floors = nullptr;
             p.quarter_bm = v->d_quarter_bm.as<const float4>();
             p.wide_qtable = v->d_wqtable.p;
+            p.wide_claim = g_tuning.sq8_wide_rows_claim;
             // ≤ 128 dims: the pilot and the main passes without a step barrier (sq8_wide_rows, osk_sq8w.hip)
             const bool rows = g_tuning.sq8_wide_rows && sq8_wide_rows_supported(u8);
             p.wide_qcap = rows ? (int)g_tuning.sq8_wide_rows_qcap : 0;

@@ -193,6 +193,7 @@ struct Sq8Params {
     const uint32_t* floors;          // sq8_wide: [q_count][n_shards] floor score (sortable bits; 0 = none)
     const float4* quarter_bm;        // sq8_wide: [4·n_tiles] the quarters' row maxima (launch_wide_quarter_max)
     const void* wide_qtable;         // sq8_wide: [4·n_tiles] the quarters' descriptors in tile order (null: computed)
+    int wide_claim;                  // sq8_wide_rows: waves claim groups from a per-quarter counter (0: fixed interleave)
 };
 
 struct SettleParams {
@@ -472,6 +473,7 @@ struct Tuning {
     std::atomic<int> sq6_rebound_stride{1};   // sq6_rebound: strided list assignment (0: contiguous)
     std::atomic<int> sq6_rebound_wgs{0};      // sq6_rebound: workgroups per CU (0: as many as fit)
     std::atomic<int> sq8_wide_rows{1};    // wide kernel, ≤ 128 dims: the main passes on sq8_wide_rows (0: sq8_wide)
+    std::atomic<int> sq8_wide_rows_claim{1};   // sq8_wide_rows: dynamic group claims per quarter (0: wave + 8i)
     std::atomic<int> sq8_scan_deep{0};    // single-query sq8_scan ≤ 256 dims: U = 8 row groups in flight per wave
     std::atomic<int> sq8_wide_rows_qcap{0};   // (tests) its deferred queue per owner wave, entries (0: kRowsQC)
     std::atomic<int> sq8_wide_defer{1};   // wide kernel: defer list insertions to each quarter's end (0: immediate)

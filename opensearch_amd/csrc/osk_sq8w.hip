@@ -1308,6 +1308,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     // hold (one LDS atomic per overflowing event) — a heavy quarter for one producer no longer drops entries
     // while the owner's other sub-queues stand empty
     const int qcap = p.wide_qcap, sub = p.wide_qcap / (2 * kWideWaves), pool = p.wide_qcap - kWideWaves * sub;
+    const bool claim_dyn = p.wide_claim != 0;
 #ifdef OSK_TESTING
     const uint64_t t_start = clock64();
     uint64_t cyc_setup = 0, cyc_qend = 0, cyc_first = 0;
@@ -1326,6 +1327,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     __shared__ int32_t s_ovf[kWideQ];                      // queue overflowed this quarter
     __shared__ int32_t s_qn[kWideWaves * kWideWaves];      // [owner][producer] queue fill (published at quarter end)
     __shared__ int32_t s_qo[kWideWaves];                   // [owner] pool fill
+    __shared__ int32_t s_next;                             // the quarter's next unclaimed group
     char* s_ring = smem;                                                                   // [8 waves][NR] slots
     // the lists [kWideQ][kKQ] keys + lower bounds (48 KB) overlay the rings: they live only in the quarter-end
     // drain and flush, when no DMA is in flight (a quarter's items are issued inside the quarter only)
@@ -1521,6 +1523,7 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
     };
     // ---- a quarter starts: its quick-test constants for every query, each wave its own 32 (lanes 0..31) ----
     auto begin_quarter = [&](const WideQuarter& d) {
+        if (tid == 0) s_next = 0;   // (read after the barrier that follows)
         if (!PILOT && lane < 32) {
             const int oq = wq0 + lane;
             float ca, cb = 0.0f;
@@ -1875,28 +1878,58 @@ __global__ __launch_bounds__(kWideThreads, 1) void sq8_wide_rows(Sq8Params p) {
         c_ng = (c_nrows + 15) >> 4;
         c_xt = reinterpret_cast<const int4*>(rfl_ptr_c(s_quart[q].xt));
         c_at = reinterpret_cast<const float4*>(rfl_ptr_c(s_quart[q].at));
-        // this wave's groups: wave + 8i, i < n_it
-        const int n_it = c_ng > wave ? (c_ng - 1 - wave) / kWideWaves + 1 : 0;
+        // this wave's groups: claimed one at a time from the quarter's counter as a ring slot frees (p.wide_claim;
+        // 0: the fixed interleave wave + 8i), so the 8 waves reach the quarter's end together whatever their
+        // slow paths cost — a wave's claims increase, so the first claim past the quarter ends its work
+        int n_claim = 0;
+        auto claim = [&]() -> int {
+            int g;
+            if (claim_dyn) {
+                g = 0;
+                if (lane == 0) g = atomicAdd(&s_next, 1);
+                g = __builtin_amdgcn_readfirstlane(g);
+            } else {
+                g = wave + kWideWaves * n_claim;
+            }
+            ++n_claim;
+            return g;
+        };
+        int gs[NR];
+        int issued = 0, done_items = 0;
 #pragma unroll
-        for (int d = 0; d < NR; ++d)
-            if (d < n_it) issue(d, wave + d * kWideWaves);
-        for (int i0 = 0; i0 < n_it; i0 += NR) {
+        for (int d = 0; d < NR; ++d) {
+            gs[d] = claim();
+            if (gs[d] < c_ng) {
+                issue(d, gs[d]);
+                ++issued;
+            }
+        }
+        bool more = issued > 0;
+        while (more) {
 #pragma unroll
             for (int d = 0; d < NR; ++d) {
-                const int i = i0 + d;
-                if (i < n_it) {
-                    // slot d's three DMAs have landed (the NR − 1 younger items' may not; at the quarter's tail
-                    // fewer are younger: wait for all)
+                if (more) {
+                    if (gs[d] >= c_ng) {
+                        more = false;   // (claims increase: every later slot is past the quarter too)
+                    } else {
+                        // slot d's three DMAs have landed (the NR − 1 younger items' may not; at the quarter's
+                        // tail fewer are younger: wait for all)
 #ifdef OSK_TESTING
-                    const uint64_t t_w0 = clock64();
+                        const uint64_t t_w0 = clock64();
 #endif
-                    if (i + NR - 1 < n_it) vm_wait<(NR - 1) * 3>();
-                    else vm_wait<0>();
+                        if (issued - done_items - 1 >= NR - 1) vm_wait<(NR - 1) * 3>();
+                        else vm_wait<0>();
 #ifdef OSK_TESTING
-                    if (i == 0) cyc_first += clock64() - t_w0;
+                        if (done_items == 0) cyc_first += clock64() - t_w0;
 #endif
-                    process(d, wave + i * kWideWaves);
-                    if (i + NR < n_it) issue(d, wave + (i + NR) * kWideWaves);
+                        process(d, gs[d]);
+                        ++done_items;
+                        gs[d] = claim();
+                        if (gs[d] < c_ng) {
+                            issue(d, gs[d]);
+                            ++issued;
+                        }
+                    }
                 }
             }
         }
