@@ -86,8 +86,8 @@ def pmc_traffic(rows_local: int, batch: int, prefilter: bool, six: bool = False)
 
 
 READ_CEILING = os.path.join(ROOT, "profiles", "r02j", "hbm_read_ceiling.json")
-# the 6-bit tier's pass (tools/gpu_run.sh pmc: FETCH_SIZE / WRITE_SIZE of this bench at N = 1, round 4)
-PMC_SUMMARY_SQ6 = os.path.join(ROOT, "profiles", "r05q", "pmc", "pmc_traffic.json")
+# the 6-bit tier's pass (tools/gpu_run.sh pmc: FETCH_SIZE / WRITE_SIZE of this bench at N = 1, round 6)
+PMC_SUMMARY_SQ6 = os.path.join(ROOT, "profiles", "r06", "pmc", "pmc_traffic.json")
 
 
 def read_ceiling():
@@ -429,7 +429,7 @@ def main():
         bytes_per_launch = rows_local * (((DIM + 255) // 256) * 192 + 16)
         kernel_name = ("sq6_scan<C=3,U=3> the 6-bit pass of the certified prefilter (bytes = 6-bit codes + 16-B "
                        "bound terms per row, one query per launch; its pilot and int8 re-bound kernels read "
-                       "≈ 1 % more: sq6_pilot 0.021 GB, sq6_rebound 0.047 GB after its final-floor re-test, profiles/r05q/pmc/)")
+                       "≈ 1 % more: sq6_pilot 0.021 GB, sq6_rebound 0.047 GB after its final-floor re-test, profiles/r06/pmc/)")
     elif prefilter:
         passes = (B + 7) // 8
         bytes_per_launch = rows_local * (u8 * 16 + 16) * passes
