@@ -615,7 +615,8 @@ static const Sq8Fn kSq8Gather[8][4] = {OSK_SQ8_GROW(4, 1),  OSK_SQ8_GROW(8, 1), 
                                        OSK_SQ8_GROW(32, 4), OSK_SQ8_GROW(64, 4)};
 
 // single queries over ≤ 256-dim rows (V = 1) with twice the row groups in flight per wave (U = 8: 8 KiB per wave
-// of rows; the U = 4 scan's waves each wait out ≈ 8 dependent round trips over a 1M-row view)
+// of rows, 3 waves per SIMD) — an A/B variant, off by default (sq8_scan_deep): at C2 b1 it was slower, 0.048 →
+// 0.061 ms (profiles/r06/call11/cfg_small_d*.jsonl): the U = 4 scan's 5 waves per SIMD hide the latency better
 static const Sq8Fn kSq8Deep[3] = {sq8_scan<4, 1, 1, 8>, sq8_scan<8, 1, 1, 8>, sq8_scan<16, 1, 1, 8>};
 
 hipError_t launch_sq8_scan(int nq, const Sq8Params& p, hipStream_t s, hipEvent_t ev_start, hipEvent_t ev_stop) {
