@@ -36,11 +36,12 @@ def main():
     p2, _ = load(d2)
     # launches in dispatch order, grouped per search: the wide path issues pilot, first pass, second pass
     ids1, ids2 = sorted(p1), sorted(p2)
-    kinds = ["pilot", "first_pass", "second_pass"]
+    # (KINDS="pilot,main": sq8_mfma's two launches per batch, tools/pmc_mfma_sq.sh)
+    kinds = os.environ.get("KINDS", "pilot,first_pass,second_pass").split(",")
     acc = collections.defaultdict(lambda: collections.defaultdict(float))
     cnt = collections.Counter()
     for j, (a, b) in enumerate(zip(ids1, ids2)):
-        k = kinds[j % 3]
+        k = kinds[j % len(kinds)]
         c = dict(p1[a])
         c.update({n: v for n, v in p2[b].items() if n != "GRBM_GUI_ACTIVE"})
         for n, v in c.items():
