@@ -690,6 +690,9 @@ template <int KS, int QB, int NS, int SIM>
 // SIMD need ≤ 128 (C4 b32: 123 VGPRs 2.71 ms, 131 VGPRs 2.89 ms per 32 queries).  KS = 4 rings fit two.
 __global__ __launch_bounds__(kBlock, QB == 1 || (NS && KS == 2) ? 4 : (NS ? 2 : 3)) void sq8_mfma(Sq8Params p) {
     constexpr bool RING = NS > 0;
+    // insertions bounded one pair per lane (see the insertion loop) — not in the 4-workgroup KS = 2 ring
+    // instances capped at 128 VGPRs (nor KS = 16, QB = 1), where its extra live values spilled inside the loop
+    constexpr bool LANE_INS = !(RING && KS == 2 && QB == 2) && !(KS == 16 && QB == 1);
     typedef int i32x4 __attribute__((ext_vector_type(4)));
     constexpr int NQ = 16 * QB, R = 16, UQ = 4 * KS;   // UQ: 16-B units per query in LDS
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform: scalar loop control
@@ -943,6 +946,42 @@ __global__ __launch_bounds__(kBlock, QB == 1 || (NS && KS == 2) ? 4 : (NS ? 2 : 
 #pragma unroll
             for (int qb = 0; qb < QB; ++qb) {
                 if (qb != bq) continue;   // (wave-uniform)
+                if constexpr (LANE_INS) {
+                    // one pair per lane: lane (col c < 4, grp g) takes row 4g + c of query b — its own row's
+                    // terms, the dot from the lane (bc, g) — so the group's 16 candidate rows cost ONE precise
+                    // bound per lane instead of four whole-wave bounds (b32 is VALU-bound, round 6:
+                    // profiles/r06/sq8_mfma_b32/).  (Selects written out: an index into these arrays put them
+                    // in scratch.)
+                    const int c4 = col & 3, src = bc + 16 * grp;
+                    const bool t1 = c4 == 1, t2 = c4 == 2, t3 = c4 == 3;
+                    const int d0 = __shfl(acc[qb][0], src), d1 = __shfl(acc[qb][1], src);
+                    const int d2 = __shfl(acc[qb][2], src), d3 = __shfl(acc[qb][3], src);
+                    const int I = t3 ? d3 : t2 ? d2 : t1 ? d1 : d0;
+                    const float4 r0f = aq.row(0), r1f = aq.row(1), r2f = aq.row(2), r3f = aq.row(3);
+                    const float4 ax = make_float4(t3 ? r3f.x : t2 ? r2f.x : t1 ? r1f.x : r0f.x,
+                                                  t3 ? r3f.y : t2 ? r2f.y : t1 ? r1f.y : r0f.y,
+                                                  t3 ? r3f.z : t2 ? r2f.z : t1 ? r1f.z : r0f.z,
+                                                  t3 ? r3f.w : t2 ? r2f.w : t1 ? r1f.w : r0f.w);
+                    const int64_t ro0 = ro[0], ro1 = ro[1], ro2 = ro[2], ro3 = ro[3];
+                    const int64_t rw = t3 ? ro3 : t2 ? ro2 : t1 ? ro1 : ro0;
+                    const bool vo0 = vo[0], vo1 = vo[1], vo2 = vo[2], vo3 = vo[3];
+                    const bool vw = t3 ? vo3 : t2 ? vo2 : t1 ? vo1 : vo0;
+                    const uint64_t p0 = pm[qb][0], p1 = pm[qb][1], p2 = pm[qb][2], p3 = pm[qb][3];
+                    const uint64_t pmw = t3 ? p3 : t2 ? p2 : t1 ? p1 : p0;
+                    const float4 qcb = p.qc[b];   // (query b's terms: a wave-uniform load, no VGPRs)
+                    const float qndb = sim == SIM_COSINE ? p.qn_dev[b] : 0.0f;
+                    const bool o = col < 4 && ((pmw >> src) & 1ull) && vw;
+                    float xnd = 0.0f;
+                    if (sim == SIM_COSINE && o) xnd = seg.xnorm_f[rw];
+                    float lo, hi;
+                    sq8_bounds(sim, (float)I, ax, qcb, p.gam, p.g2, lo, hi);
+                    const float ub = sim == SIM_EUCLIDEAN ? score_f32_l2(lo) : score_f32(sim, hi, qndb, xnd);
+                    const float lb = sim == SIM_EUCLIDEAN ? score_f32_l2(hi) : score_f32(sim, lo, qndb, xnd);
+                    const uint64_t key = o ? make_key(ub, vbase + (uint32_t)rw) : 0ull;
+                    wave_offer2(key, float_to_sortable(lb), o, lkb, lpb, thrb, lane, kKQ);
+                    if (col == bc) tq[qb] = sq8_quick(sim, thrb > tkey[qb] ? thrb : tkey[qb], sqn[qb], p.cos_slack);
+                    continue;
+                }
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const bool o = ((pm[qb][i] >> lane) & 1ull) && vo[i] && col == bc;
