@@ -264,6 +264,18 @@ int32_t osk_view_scan_time(osk_view* view, double* total_ms, int64_t* calls);
  *   "call_timing"     0|1 host entries time each call on the device (osk_last_call_device_ns; default 0)
  *   "sel_writer"      select path bounds writer: 0 = 4 row groups in flight + Java's transform,
  *                     1 = 4 groups + fp32 COSINE bounds, 2 = 2 groups (default), 3 = 1 group (fast bounds)
+ *   "sq8_wide_min"    unfiltered prefilter batches of at least this many queries may take the wide int8
+ *                     kernels (256 queries per corpus pass; default 64; 0 = never)
+ *   "sq8_wide_rows"   0|1 rows of ≤ 128 dims: the wide pilot and main passes on sq8_wide_rows, without a step
+ *                     barrier (default 1) instead of the ring kernel sq8_wide
+ *   "sq8_wide_rows_claim"  0|1 its waves claim 16-row groups from a per-quarter counter (default 1) or take
+ *                     the fixed interleave
+ *   "sq8_wide_phase"  the wide main pass's first launch covers 1/this of the quarters (default 8)
+ *   "sq8_wide_pilot_rows"  wide pilot rows per quarter (default 0 = 128, 256 at ≥ 512 dims, raised to
+ *                     sample ≥ 64k rows per shard)
+ *   "sq8_wide_quarter_rows"  rows per wide quarter (default 0 = auto, ≤ 16,384; at the view's first wide batch)
+ *   "sq8_scan_deep"   0|1 single-query sq8_scan over ≤ 256 dims with 8 row groups in flight per wave
+ *                     (default 0: measured slower)
  * The testing build (libosknn_testing.so) also accepts "sq8_mfma_ablate", "mfma_ablate" (A/B timing,
  * results wrong), "sq8_force_fallback" (every prefilter list re-scanned exactly) and "settle_trace";
  * the shipped library returns OSK_ERR_UNSUPPORTED for them. */
