@@ -688,11 +688,12 @@ struct AuxQ {
 template <int KS, int QB, int NS, int SIM>
 // KS = 2 ring instances are capped at 128 VGPRs: their LDS holds four workgroups per CU, and 4 waves per
 // SIMD need ≤ 128 (C4 b32: 123 VGPRs 2.71 ms, 131 VGPRs 2.89 ms per 32 queries).  KS = 4 rings fit two.
-__global__ __launch_bounds__(kBlock, QB == 1 || (NS && KS == 2) ? 4 : (NS ? 2 : 3)) void sq8_mfma(Sq8Params p) {
+__global__ __launch_bounds__(kBlock, QB == 1 || (NS == 2 && KS == 2) ? 4 : (NS ? 2 : 3)) void sq8_mfma(Sq8Params p) {
     constexpr bool RING = NS > 0;
-    // insertions bounded one pair per lane (see the insertion loop) — not in the 4-workgroup KS = 2 ring
+    // insertions bounded one pair per lane (see the insertion loop) — not in the 4-workgroup KS = 2, 2-slot ring
     // instances capped at 128 VGPRs (nor KS = 16, QB = 1), where its extra live values spilled inside the loop
-    constexpr bool LANE_INS = !(RING && KS == 2 && QB == 2) && !(KS == 16 && QB == 1);
+    // (the 4-slot ring instances, 2 workgroups per CU, take it)
+    constexpr bool LANE_INS = !(RING && KS == 2 && QB == 2 && NS == 2) && !(KS == 16 && QB == 1);
     typedef int i32x4 __attribute__((ext_vector_type(4)));
     constexpr int NQ = 16 * QB, R = 16, UQ = 4 * KS;   // UQ: 16-B units per query in LDS
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform: scalar loop control
