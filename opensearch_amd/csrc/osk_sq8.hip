@@ -1225,8 +1225,11 @@ int sq8_ring_slots(int u8, int qb, int want) {
     while (c < 5 && 4 * kMfmaKS[c] < u8) ++c;
     if (c > 1 || want == 0) return 0;
     // the kernel is instantiated at depths 2 and 4: 2 by default (four workgroups per CU; deeper rings
-    // measured slower), 4 when asked for a deeper one and it fits one workgroup's LDS
-    if (want > 2 && sq8_mfma_lds(u8, qb, 4) <= 160 * 1024) return 4;
+    // measured slower), 4 when asked for a deeper one and it fits one workgroup's LDS — and by
+    // default for 32-query launches of ≤ 128 dims since round 6, whose 4-slot instances take the lane-compact
+    // insertions (C4 b32 2.84 → 2.67–2.71 ms, profiles/r06/call25/)
+    const bool deep = want > 2 || (want < 0 && c == 0 && qb == 2);
+    if (deep && sq8_mfma_lds(u8, qb, 4) <= 160 * 1024) return 4;
     return 2;
 }
 int sq8_mfma_ks(int u8) {
