@@ -316,13 +316,16 @@ def test_wide_copy_is_built_only_when_a_batch_takes_the_wide_kernel():
         close_all(ds, readers)
 
 
-@pytest.mark.parametrize("qcap", [0, 1, 8])
+@pytest.mark.parametrize("claim", [1, 0])
+@pytest.mark.parametrize("qcap", [0, 1, 8, 64, 128])
 @pytest.mark.parametrize("sim", SIMS, ids=lambda s: s.name)
-def test_wide_rows_kernel_equals_the_ring_kernel(sim, qcap):
-    """≤ 128 dims run the main passes on sq8_wide_rows (rows owned by waves, no step barrier, insertions queued
-    to the query's owner wave).  Its results equal sq8_wide's (tune sq8_wide_rows 0), the fp32 scan and
-    sq8_mfma; with the queues shrunk to 1 or 8 entries (sq8_wide_rows_qcap) most entries are dropped and their
-    (quarter, query) lists marked for the settle's exact re-scan — results still equal, bit for bit."""
+def test_wide_rows_kernel_equals_the_ring_kernel(sim, qcap, claim):
+    """≤ 128 dims run the pilot and the main passes on sq8_wide_rows (rows owned by waves, no step barrier,
+    insertions queued to the query's owner wave).  Its results equal sq8_wide's (tune sq8_wide_rows 0), the fp32
+    scan and sq8_mfma; with the queues shrunk (sq8_wide_rows_qcap: 1 or 8 entries — no sub-queues, a pool of
+    1 / 8; 64 or 128 — sub-queues of 4 / 8 entries spilling into pools of 32 / 64) entries spill into the pool
+    or are dropped and their (quarter, query) lists marked for the settle's exact re-scan — results still
+    equal, bit for bit; with the groups dealt (claim 0) or claimed (claim 1)."""
     rows_list = [corpus(n, 96, sim, 80 + i) for i, n in enumerate([23001, 1, 7000, 16])]
     shard_of, shard_index = [0, 0, 1, 2], [1, 2, 0]
     queries = corpus(300, 96, sim, 90)
@@ -330,10 +333,12 @@ def test_wide_rows_kernel_equals_the_ring_kernel(sim, qcap):
     ds, readers = view_of(rows_list, sim, shard_of, shard_index)
     try:
         _lib.tune("sq8_wide_rows_qcap", qcap)
+        _lib.tune("sq8_wide_rows_claim", claim)
         try:
             rows = three_ways(ds, queries, 10)
         finally:
             _lib.tune("sq8_wide_rows_qcap", 0)
+            _lib.tune("sq8_wide_rows_claim", 1)
         ring = tuned("sq8_wide_rows", 0, 1, lambda: ds.search(queries, 10, 0, 10))
         assert_same(rows, ring)
         for i in (0, 7, 299):
